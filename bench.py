@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Llama-2-7B bf16 full fine-tune, tokens/s for the whole node.
+
+BASELINE.json metric: "tokens/sec (whole node) Llama-2-7B fine-tune at 1/2/4/8 MI355X".
+Config #2 "Llama-2 7B DDP bf16, 8 Ray workers on 8xMI355X (fine_tune_llama_ray.py path)":
+* model: Llama-2-7B architecture (6.74 B params), random init, bf16 params + bf16 grads,
+  fp32 AdamW moments (the reference full-FT path: torch_dtype=bfloat16 + paged_adamw_32bit,
+  reference ray-jobs/fine_tune_llama_ray.py:235-241, fine_tune_config.json:17);
+* data: synthetic Wikitext-2-shaped token batches, seq 1024 (MAX_SEQ_LENGTH), 8 sequences per
+  GPU per optimizer step (= the reference's PER_DEVICE_TRAIN_BATCH_SIZE 2 x
+  GRADIENT_ACCUMULATION_STEPS 4, fine_tune_config.json:13-14) — weak scaling;
+* step: forward + backward + DDP gradient all-reduce (RCCL, bucketed, overlapped) + global
+  grad-norm clip (MAX_GRAD_NORM 0.3) + fused AdamW. Nothing is skipped inside the timed region.
+
+Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
+bench.py --gpus N``. Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--model", default="llama2-7b")
+    ap.add_argument("--batch", type=int, default=8, help="sequences per GPU per step")
+    ap.add_argument("--micro-batch", type=int, default=0, help="micro-batch (grad accumulation); 0 = batch")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--bucket-mb", type=float, default=0.0, help="DDP bucket size (0 = planner)")
+    ap.add_argument("--max-grad-norm", type=float, default=0.3)
+    ap.add_argument("--lr", type=float, default=2e-5)
+    ap.add_argument("--checkpointing", action="store_true", help="activation checkpointing")
+    ap.add_argument("--profile-dir", default="", help="write a torch.profiler trace here")
+    ap.add_argument("--device", default="cuda")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    cpu = a.device == "cpu"
+    if cpu:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("gloo" if cpu else "nccl", device_id=None if cpu else dev)
+
+    from gke_ray_train_amd.models import build_llama, get_config
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    from gke_ray_train_amd.ops import FusedAdamW, clip_grad_norm_
+
+    torch.manual_seed(1234)
+    dtype = torch.float32 if cpu else torch.bfloat16
+    cfg = get_config(a.model)
+    model = build_llama(cfg, device=dev, dtype=dtype, seed=1234)
+    if a.checkpointing:
+        model.gradient_checkpointing_enable()
+    model.train()
+    ddp = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb or None)
+    opt = FusedAdamW(ddp.optimizer_param_groups(weight_decay=0.0), lr=a.lr, betas=(0.9, 0.999), eps=1e-8)
+
+    mb = a.micro_batch or a.batch
+    assert a.batch % mb == 0
+    accum = a.batch // mb
+    g = torch.Generator(device=dev)
+    g.manual_seed(rank + 17)
+    # synthetic Wikitext-2-shaped batches (pre-generated, fixed shapes; random token ids)
+    nbuf = 4
+    batches = [torch.randint(0, cfg.vocab_size, (mb, a.seq), device=dev, generator=g) for _ in range(nbuf * accum)]
+
+    def step(i):
+        for j in range(accum):
+            ids = batches[(i * accum + j) % len(batches)]
+            with ddp.no_sync(j < accum - 1):
+                loss = model(ids, labels=ids)["loss"] / accum
+                loss.backward()
+        ddp.finish_gradient_sync()
+        st = clip_grad_norm_(ddp.grad_buffers(), a.max_grad_norm, prescale=1.0 / ddp.world_size)
+        opt.step(grad_scale=st)
+        ddp.zero_grad()
+        return loss
+
+    for i in range(a.warmup):
+        loss = step(i)
+    if not cpu:
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not cpu:
+        torch.cuda.synchronize()
+    prof = None
+    if a.profile_dir and rank == 0:
+        from torch.profiler import ProfilerActivity, profile
+        prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
+        prof.__enter__()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(a.warmup + i)
+    if not cpu:
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    if not cpu:
+        torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if prof is not None:
+        prof.__exit__(None, None, None)
+        os.makedirs(a.profile_dir, exist_ok=True)
+        prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
+        with open(os.path.join(a.profile_dir, "kernels.txt"), "w") as f:
+            f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev if not cpu else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = 1000.0 * elapsed / a.steps
+    tokens_per_step = a.batch * a.seq * world
+    tps = tokens_per_step / (elapsed / a.steps)
+    fpt = cfg.flops_per_token(a.seq)
+    mfu = tps / world * fpt / 2.5e15
+    if rank == 0:
+        out = {
+            "metric": "tokens/sec (whole node) Llama-2-7B fine-tune",
+            "value": round(tps, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if not cpu else "fp32",
+            "data": "synthetic (random token ids, Wikitext-2-shaped; random-init weights)",
+            "config": {"model": cfg.name, "global_batch": a.batch * world, "seq_len": a.seq,
+                       "parallelism": f"dp{world}", "micro_batch": mb, "grad_accum": accum,
+                       "optimizer": "fused AdamW fp32 states", "max_grad_norm": a.max_grad_norm},
+            "samples_per_sec": round(tps / a.seq, 2),
+            "mfu_bf16_dense": round(mfu, 4),
+            "loss": round(float(loss.item()) * accum, 4),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

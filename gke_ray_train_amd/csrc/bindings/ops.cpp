@@ -1,0 +1,450 @@
+// torch <-> HIP kernel bindings for gke_ray_train_amd._C.
+//
+// Every op launches on the caller's current HIP stream (graph-capturable: no allocation
+// besides the torch caching allocator, no synchronisation) and checks shapes/strides on the
+// host BEFORE launch so a hand-written kernel never sees operands its grid does not expect.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "grt_kernels.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+hipStream_t cur_stream(const Tensor& t) {
+  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+grt::DType dtype_of(const Tensor& t) {
+  if (t.scalar_type() == at::kBFloat16) return grt::DType::BF16;
+  TORCH_CHECK(t.scalar_type() == at::kFloat, "gke_ray_train_amd kernels support bf16/fp32, got ", t.scalar_type());
+  return grt::DType::F32;
+}
+
+void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+void check_contig(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_vec(const Tensor& t, int64_t d, const char* name) {
+  const int64_t vec = t.scalar_type() == at::kBFloat16 ? 8 : 4;
+  TORCH_CHECK(d % vec == 0, name, ": last dim ", d, " must be a multiple of ", vec);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+const void* ptr_or_null(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+// ------------------------------------------------------------------ norms
+std::vector<Tensor> rmsnorm_fwd(const Tensor& x, const optional<Tensor>& residual, const Tensor& w,
+                                double eps) {
+  check_contig(x, "x");
+  check_contig(w, "w");
+  c10::OptionalDeviceGuard g(x.device());
+  const int64_t d = x.size(-1), rows = x.numel() / d;
+  check_vec(x, d, "x");
+  TORCH_CHECK(w.numel() == d && w.scalar_type() == x.scalar_type(), "weight shape/dtype mismatch");
+  auto y = at::empty_like(x);
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  Tensor h;
+  if (residual.has_value()) {
+    check_contig(*residual, "residual");
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type(), "residual mismatch");
+    h = at::empty_like(x);
+  }
+  grt::rmsnorm_fwd(dtype_of(x), x.data_ptr(), ptr_or_null(residual), w.data_ptr(), y.data_ptr(),
+                   residual.has_value() ? h.data_ptr() : nullptr, rstd.data_ptr<float>(), rows, (int)d,
+                   (float)eps, cur_stream(x));
+  return {y, residual.has_value() ? h : x, rstd};
+}
+
+std::vector<Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& h, const Tensor& w, const Tensor& rstd,
+                                const optional<Tensor>& dres) {
+  check_contig(dy, "dy");
+  check_contig(h, "h");
+  c10::OptionalDeviceGuard g(dy.device());
+  const int64_t d = h.size(-1), rows = h.numel() / d;
+  TORCH_CHECK(dy.sizes() == h.sizes() && dy.scalar_type() == h.scalar_type(), "dy/h mismatch");
+  if (dres.has_value()) {
+    check_contig(*dres, "dres");
+    TORCH_CHECK(dres->sizes() == h.sizes() && dres->scalar_type() == h.scalar_type(), "dres mismatch");
+  }
+  auto dx = at::empty_like(h);
+  auto dw = at::empty({d}, h.options().dtype(at::kFloat));
+  auto ws = at::empty({grt::norm_bwd_workspace_floats(rows, (int)d)}, h.options().dtype(at::kFloat));
+  grt::rmsnorm_bwd(dtype_of(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(),
+                   ptr_or_null(dres), dx.data_ptr(), dw.data_ptr<float>(), ws.data_ptr<float>(), rows,
+                   (int)d, cur_stream(h));
+  return {dx, dw};
+}
+
+std::vector<Tensor> layernorm_fwd(const Tensor& x, const optional<Tensor>& residual, const Tensor& w,
+                                  const optional<Tensor>& b, double eps) {
+  check_contig(x, "x");
+  c10::OptionalDeviceGuard g(x.device());
+  const int64_t d = x.size(-1), rows = x.numel() / d;
+  check_vec(x, d, "x");
+  TORCH_CHECK(w.numel() == d && w.scalar_type() == x.scalar_type(), "weight shape/dtype mismatch");
+  auto y = at::empty_like(x);
+  auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  Tensor h;
+  if (residual.has_value()) {
+    check_contig(*residual, "residual");
+    TORCH_CHECK(residual->sizes() == x.sizes(), "residual mismatch");
+    h = at::empty_like(x);
+  }
+  grt::layernorm_fwd(dtype_of(x), x.data_ptr(), ptr_or_null(residual), w.data_ptr(), ptr_or_null(b),
+                     y.data_ptr(), residual.has_value() ? h.data_ptr() : nullptr, mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), rows, (int)d, (float)eps, cur_stream(x));
+  return {y, residual.has_value() ? h : x, mean, rstd};
+}
+
+std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& h, const Tensor& w, const Tensor& mean,
+                                  const Tensor& rstd, const optional<Tensor>& dres) {
+  check_contig(dy, "dy");
+  check_contig(h, "h");
+  c10::OptionalDeviceGuard g(dy.device());
+  const int64_t d = h.size(-1), rows = h.numel() / d;
+  auto dx = at::empty_like(h);
+  auto dw = at::empty({d}, h.options().dtype(at::kFloat));
+  auto db = at::empty({d}, h.options().dtype(at::kFloat));
+  auto ws = at::empty({grt::norm_bwd_workspace_floats(rows, (int)d)}, h.options().dtype(at::kFloat));
+  grt::layernorm_bwd(dtype_of(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), ptr_or_null(dres), dx.data_ptr(), dw.data_ptr<float>(),
+                     db.data_ptr<float>(), ws.data_ptr<float>(), rows, (int)d, cur_stream(h));
+  return {dx, dw, db};
+}
+
+// ------------------------------------------------------------------ elementwise
+Tensor swiglu_fwd(const Tensor& gu) {
+  check_contig(gu, "gu");
+  c10::OptionalDeviceGuard g(gu.device());
+  const int64_t two_f = gu.size(-1), rows = gu.numel() / two_f, f = two_f / 2;
+  check_vec(gu, f, "gu");
+  auto sizes = gu.sizes().vec();
+  sizes.back() = f;
+  auto out = at::empty(sizes, gu.options());
+  grt::swiglu_fwd(dtype_of(gu), gu.data_ptr(), out.data_ptr(), rows, (int)f, cur_stream(gu));
+  return out;
+}
+Tensor swiglu_bwd(const Tensor& gu, const Tensor& dout) {
+  check_contig(gu, "gu");
+  check_contig(dout, "dout");
+  c10::OptionalDeviceGuard g(gu.device());
+  const int64_t two_f = gu.size(-1), rows = gu.numel() / two_f, f = two_f / 2;
+  TORCH_CHECK(dout.numel() == rows * f, "dout shape mismatch");
+  auto dgu = at::empty_like(gu);
+  grt::swiglu_bwd(dtype_of(gu), gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), rows, (int)f, cur_stream(gu));
+  return dgu;
+}
+Tensor gelu_fwd(const Tensor& x) {
+  check_contig(x, "x");
+  c10::OptionalDeviceGuard g(x.device());
+  check_vec(x, x.numel(), "x");
+  auto y = at::empty_like(x);
+  grt::gelu_fwd(dtype_of(x), x.data_ptr(), y.data_ptr(), x.numel(), cur_stream(x));
+  return y;
+}
+Tensor gelu_bwd(const Tensor& x, const Tensor& dy) {
+  check_contig(x, "x");
+  check_contig(dy, "dy");
+  c10::OptionalDeviceGuard g(x.device());
+  check_vec(x, x.numel(), "x");
+  auto dx = at::empty_like(x);
+  grt::gelu_bwd(dtype_of(x), x.data_ptr(), dy.data_ptr(), dx.data_ptr(), x.numel(), cur_stream(x));
+  return dx;
+}
+
+void check_rope(const Tensor& cos, const Tensor& sin, const optional<Tensor>& pos, int64_t T, int64_t S, int64_t D) {
+  check_contig(cos, "cos");
+  check_contig(sin, "sin");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat, "cos/sin must be fp32");
+  TORCH_CHECK(cos.size(-1) == D / 2 && cos.numel() >= S * (D / 2) && sin.sizes() == cos.sizes(), "cos/sin shape");
+  TORCH_CHECK(D % 16 == 0, "head_dim must be a multiple of 16");
+  if (pos.has_value()) {
+    check_contig(*pos, "pos");
+    TORCH_CHECK(pos->scalar_type() == at::kInt && pos->numel() == T, "pos must be int32 [T]");
+  }
+}
+
+// qkv: [T, ld] (row-contiguous), returns q [T, hq, D], k [T, hkv, D]
+std::vector<Tensor> rope_fwd(const Tensor& qkv, const Tensor& cos, const Tensor& sin,
+                             const optional<Tensor>& pos, int64_t hq, int64_t hkv, int64_t D, int64_t S) {
+  check_cuda(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1, "qkv must be [T, ld] with unit column stride");
+  c10::OptionalDeviceGuard g(qkv.device());
+  const int64_t T = qkv.size(0), ld = qkv.stride(0);
+  TORCH_CHECK(qkv.size(1) >= (hq + hkv) * D, "qkv too narrow");
+  TORCH_CHECK(ld % 8 == 0 && reinterpret_cast<uintptr_t>(qkv.data_ptr()) % 16 == 0, "qkv alignment");
+  check_rope(cos, sin, pos, T, S, D);
+  auto q = at::empty({T, hq, D}, qkv.options());
+  auto k = at::empty({T, hkv, D}, qkv.options());
+  grt::rope_fwd(dtype_of(qkv), qkv.data_ptr(), ld, q.data_ptr(), k.data_ptr(), cos.data_ptr<float>(),
+                sin.data_ptr<float>(), pos.has_value() ? pos->data_ptr<int32_t>() : nullptr, T, (int)S,
+                (int)hq, (int)hkv, (int)D, cur_stream(qkv));
+  return {q, k};
+}
+
+void rope_bwd(const Tensor& dq, const Tensor& dk, Tensor& dqkv, const Tensor& cos, const Tensor& sin,
+              const optional<Tensor>& pos, int64_t hq, int64_t hkv, int64_t D, int64_t S) {
+  check_contig(dq, "dq");
+  check_contig(dk, "dk");
+  TORCH_CHECK(dqkv.dim() == 2 && dqkv.stride(1) == 1, "dqkv must be [T, ld]");
+  c10::OptionalDeviceGuard g(dq.device());
+  const int64_t T = dqkv.size(0), ld = dqkv.stride(0);
+  TORCH_CHECK(dq.numel() == T * hq * D && dk.numel() == T * hkv * D, "dq/dk shape");
+  check_rope(cos, sin, pos, T, S, D);
+  grt::rope_bwd(dtype_of(dq), dq.data_ptr(), dk.data_ptr(), dqkv.data_ptr(), ld, cos.data_ptr<float>(),
+                sin.data_ptr<float>(), pos.has_value() ? pos->data_ptr<int32_t>() : nullptr, T, (int)S,
+                (int)hq, (int)hkv, (int)D, cur_stream(dq));
+}
+
+Tensor scale_add_pe(const Tensor& emb, const optional<Tensor>& pe, int64_t S, double scale) {
+  check_contig(emb, "emb");
+  c10::OptionalDeviceGuard g(emb.device());
+  const int64_t d = emb.size(-1), T = emb.numel() / d;
+  check_vec(emb, d, "emb");
+  if (pe.has_value()) {
+    check_contig(*pe, "pe");
+    TORCH_CHECK(pe->scalar_type() == at::kFloat && pe->numel() >= S * d, "pe must be fp32 [>=S, d]");
+  }
+  auto out = at::empty_like(emb);
+  grt::scale_add_pe(dtype_of(emb), emb.data_ptr(), pe.has_value() ? pe->data_ptr<float>() : nullptr,
+                    out.data_ptr(), T, (int)S, (int)d, (float)scale, cur_stream(emb));
+  return out;
+}
+
+std::vector<Tensor> dropout_fwd(const Tensor& x, double p, int64_t seed, int64_t offset) {
+  check_contig(x, "x");
+  c10::OptionalDeviceGuard g(x.device());
+  auto y = at::empty_like(x);
+  auto mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
+  grt::dropout_fwd(dtype_of(x), x.data_ptr(), y.data_ptr(), mask.data_ptr<uint8_t>(), x.numel(), (float)p,
+                   (uint64_t)seed, (uint64_t)offset, cur_stream(x));
+  return {y, mask};
+}
+Tensor dropout_bwd(const Tensor& dy, const Tensor& mask, double p) {
+  check_contig(dy, "dy");
+  check_contig(mask, "mask");
+  c10::OptionalDeviceGuard g(dy.device());
+  auto dx = at::empty_like(dy);
+  grt::dropout_bwd(dtype_of(dy), dy.data_ptr(), mask.data_ptr<uint8_t>(), dx.data_ptr(), dy.numel(), (float)p,
+                   cur_stream(dy));
+  return dx;
+}
+
+// ------------------------------------------------------------------ cross entropy
+std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore_index) {
+  check_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, V] row-major");
+  check_contig(labels, "labels");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == logits.size(0), "labels must be int64 [N]");
+  c10::OptionalDeviceGuard g(logits.device());
+  const int64_t N = logits.size(0);
+  auto loss = at::empty({N}, logits.options().dtype(at::kFloat));
+  auto lse = at::empty({N}, logits.options().dtype(at::kFloat));
+  grt::cross_entropy_fwd(dtype_of(logits), logits.data_ptr(), logits.stride(0), labels.data_ptr<int64_t>(),
+                         loss.data_ptr<float>(), lse.data_ptr<float>(), N, (int)logits.size(1), ignore_index,
+                         cur_stream(logits));
+  return {loss, lse};
+}
+Tensor ce_bwd(const Tensor& logits, const Tensor& labels, const Tensor& lse, const Tensor& gscale,
+              int64_t ignore_index, bool inplace) {
+  check_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, V] row-major");
+  check_contig(gscale, "gscale");
+  TORCH_CHECK(gscale.scalar_type() == at::kFloat && gscale.numel() == logits.size(0), "gscale fp32 [N]");
+  c10::OptionalDeviceGuard g(logits.device());
+  Tensor d = inplace ? logits : at::empty_like(logits, at::MemoryFormat::Contiguous);
+  grt::cross_entropy_bwd(dtype_of(logits), logits.data_ptr(), logits.stride(0), labels.data_ptr<int64_t>(),
+                         lse.data_ptr<float>(), gscale.data_ptr<float>(), d.data_ptr(), d.stride(0),
+                         logits.size(0), (int)logits.size(1), ignore_index, cur_stream(logits));
+  return d;
+}
+
+// ------------------------------------------------------------------ optimizer
+int64_t sumsq_blocks() { return grt::optim_sumsq_blocks(); }
+void sumsq(const Tensor& x, Tensor& ws, int64_t slot) {
+  check_contig(x, "x");
+  check_contig(ws, "ws");
+  TORCH_CHECK(ws.scalar_type() == at::kFloat && ws.numel() >= (slot + 1) * grt::optim_sumsq_blocks(), "ws too small");
+  c10::OptionalDeviceGuard g(x.device());
+  grt::sumsq_accumulate(dtype_of(x), x.data_ptr(), x.numel(), ws.data_ptr<float>(), (int)slot, cur_stream(x));
+}
+void clip_finalize(const Tensor& ws, int64_t nparts, double max_norm, double prescale, Tensor& out) {
+  check_contig(ws, "ws");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() >= 2, "out must be fp32 [2]");
+  c10::OptionalDeviceGuard g(ws.device());
+  grt::clip_coef_finalize(ws.data_ptr<float>(), (int)nparts, (float)max_norm, (float)prescale, out.data_ptr<float>(),
+                          cur_stream(ws));
+}
+void adamw(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const optional<Tensor>& master, const Tensor& hyper,
+           const optional<Tensor>& gscale) {
+  check_contig(p, "p");
+  check_contig(gr, "g");
+  check_contig(m, "m");
+  check_contig(v, "v");
+  const int64_t n = p.numel();
+  TORCH_CHECK(gr.numel() == n && m.numel() == n && v.numel() == n, "adamw size mismatch");
+  TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat, "adam state must be fp32");
+  TORCH_CHECK(hyper.scalar_type() == at::kFloat && hyper.numel() >= 8 && hyper.is_cuda(), "hyper fp32[8] on device");
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&p, &gr, &m, &v})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0 ||
+                    (t->element_size() == 2 && reinterpret_cast<uintptr_t>(t->data_ptr()) % 8 == 0),
+                "adamw operands must be vector aligned");
+  if (master.has_value()) {
+    check_contig(*master, "master");
+    TORCH_CHECK(master->numel() == n && master->scalar_type() == at::kFloat, "master fp32 [n]");
+  }
+  c10::OptionalDeviceGuard g(p.device());
+  grt::adamw_step(dtype_of(p), dtype_of(gr), p.data_ptr(), gr.data_ptr(), m.data_ptr<float>(), v.data_ptr<float>(),
+                  master.has_value() ? master->data_ptr<float>() : nullptr, n, hyper.data_ptr<float>(),
+                  gscale.has_value() ? gscale->data_ptr<float>() : nullptr, cur_stream(p));
+}
+void scale_(Tensor& x, double a, const optional<Tensor>& a_ptr) {
+  check_contig(x, "x");
+  c10::OptionalDeviceGuard g(x.device());
+  grt::scale_inplace(dtype_of(x), x.data_ptr(), x.numel(), (float)a,
+                     a_ptr.has_value() ? a_ptr->data_ptr<float>() : nullptr, cur_stream(x));
+}
+
+// ------------------------------------------------------------------ attention
+void check_bshd(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.dim() == 4, name, " must be [B, S, H, D]");
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
+  TORCH_CHECK(t.size(3) == 128 && t.stride(3) == 1, name, ": head_dim must be 128 and contiguous");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, ": strides must keep 16-byte alignment");
+}
+
+grt::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, Tensor& lse,
+                            double scale, bool causal, const optional<Tensor>& seqlens_k) {
+  check_bshd(q, "q");
+  check_bshd(k, "k");
+  check_bshd(v, "v");
+  check_bshd(o, "o");
+  TORCH_CHECK(k.sizes() == v.sizes(), "k/v shape mismatch");
+  TORCH_CHECK(q.size(0) == k.size(0) && o.sizes() == q.sizes(), "batch/out shape mismatch");
+  TORCH_CHECK(q.size(2) % k.size(2) == 0, "Hq must be a multiple of Hkv");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() &&
+                  lse.numel() == q.size(0) * q.size(2) * q.size(1),
+              "lse must be fp32 [B, Hq, Sq]");
+  grt::AttnParams p{};
+  p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = o.data_ptr(); p.lse = lse.data_ptr<float>();
+  p.q_bs = q.stride(0); p.q_ss = q.stride(1); p.q_hs = q.stride(2);
+  p.k_bs = k.stride(0); p.k_ss = k.stride(1); p.k_hs = k.stride(2);
+  p.v_bs = v.stride(0); p.v_ss = v.stride(1); p.v_hs = v.stride(2);
+  p.o_bs = o.stride(0); p.o_ss = o.stride(1); p.o_hs = o.stride(2);
+  p.B = (int)q.size(0); p.Sq = (int)q.size(1); p.Sk = (int)k.size(1);
+  p.Hq = (int)q.size(2); p.Hkv = (int)k.size(2); p.D = (int)q.size(3);
+  p.scale = (float)scale;
+  p.causal = causal ? 1 : 0;
+  if (causal) TORCH_CHECK(p.Sk >= p.Sq, "causal attention needs Sk >= Sq");
+  p.seqlens_k = nullptr;
+  if (seqlens_k.has_value()) {
+    check_contig(*seqlens_k, "seqlens_k");
+    TORCH_CHECK(seqlens_k->scalar_type() == at::kInt && seqlens_k->numel() == q.size(0), "seqlens_k int32 [B]");
+    p.seqlens_k = seqlens_k->data_ptr<int32_t>();
+  }
+  return p;
+}
+
+std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& out,
+                             double scale, bool causal, const optional<Tensor>& seqlens_k) {
+  c10::OptionalDeviceGuard g(q.device());
+  Tensor o = out.has_value() ? *out : at::empty(q.sizes(), q.options());
+  auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
+  auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k);
+  grt::attn_fwd(p, cur_stream(q));
+  return {o, lse};
+}
+
+std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
+                             Tensor& lse, const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
+                             const optional<Tensor>& dv_out, double scale, bool causal,
+                             const optional<Tensor>& seqlens_k) {
+  c10::OptionalDeviceGuard g(q.device());
+  check_bshd(dout, "dout");
+  TORCH_CHECK(dout.sizes() == q.sizes(), "dout shape");
+  auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k);
+  Tensor dq = dq_out.has_value() ? *dq_out : at::empty(q.sizes(), q.options());
+  Tensor dk = dk_out.has_value() ? *dk_out : at::empty(k.sizes(), k.options());
+  Tensor dv = dv_out.has_value() ? *dv_out : at::empty(v.sizes(), v.options());
+  check_bshd(dq, "dq");
+  check_bshd(dk, "dk");
+  check_bshd(dv, "dv");
+  TORCH_CHECK(dq.sizes() == q.sizes() && dk.sizes() == k.sizes() && dv.sizes() == v.sizes(), "grad shapes");
+  auto ws = at::empty({grt::attn_bwd_workspace_floats(p.B, p.Hq, p.Sq, p.D)}, q.options().dtype(at::kFloat));
+  grt::AttnBwdParams bp{};
+  bp.f = p;
+  bp.dout = dout.data_ptr(); bp.do_bs = dout.stride(0); bp.do_ss = dout.stride(1); bp.do_hs = dout.stride(2);
+  bp.dq = dq.data_ptr(); bp.dq_bs = dq.stride(0); bp.dq_ss = dq.stride(1); bp.dq_hs = dq.stride(2);
+  bp.dk = dk.data_ptr(); bp.dk_bs = dk.stride(0); bp.dk_ss = dk.stride(1); bp.dk_hs = dk.stride(2);
+  bp.dv = dv.data_ptr(); bp.dv_bs = dv.stride(0); bp.dv_ss = dv.stride(1); bp.dv_hs = dv.stride(2);
+  bp.dq_acc = ws.data_ptr<float>();
+  bp.delta = ws.data_ptr<float>() + (int64_t)p.B * p.Hq * p.Sq * p.D;
+  grt::attn_bwd(bp, cur_stream(q));
+  return {dq, dk, dv};
+}
+
+// ------------------------------------------------------------------ NF4
+std::vector<Tensor> nf4_quantize(const Tensor& w, int64_t blocksize) {
+  check_contig(w, "w");
+  c10::OptionalDeviceGuard g(w.device());
+  const int64_t n = w.numel();
+  TORCH_CHECK(n % blocksize == 0 && (blocksize == 32 || blocksize == 64 || blocksize == 128),
+              "numel must be a multiple of blocksize (32/64/128)");
+  auto q = at::empty({n / 2}, w.options().dtype(at::kByte));
+  auto absmax = at::empty({n / blocksize}, w.options().dtype(at::kFloat));
+  grt::nf4_quantize(dtype_of(w), w.data_ptr(), q.data_ptr<uint8_t>(), absmax.data_ptr<float>(), n, (int)blocksize,
+                    cur_stream(w));
+  return {q, absmax};
+}
+Tensor nf4_dequantize(const Tensor& q, const Tensor& absmax, int64_t n, int64_t blocksize, at::ScalarType dt,
+                      const optional<Tensor>& out) {
+  check_contig(q, "q");
+  check_contig(absmax, "absmax");
+  c10::OptionalDeviceGuard g(q.device());
+  TORCH_CHECK(q.numel() * 2 == n && absmax.numel() * blocksize == n, "nf4 shapes");
+  Tensor w = out.has_value() ? *out : at::empty({n}, q.options().dtype(dt));
+  TORCH_CHECK(w.numel() == n && w.is_contiguous(), "out shape");
+  grt::nf4_dequantize(dtype_of(w), q.data_ptr<uint8_t>(), absmax.data_ptr<float>(), w.data_ptr(), n, (int)blocksize,
+                      cur_stream(q));
+  return w;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "gke_ray_train_amd HIP kernels for gfx950 (MI355X)";
+  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("rope_fwd", &rope_fwd);
+  m.def("rope_bwd", &rope_bwd);
+  m.def("scale_add_pe", &scale_add_pe);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("dropout_bwd", &dropout_bwd);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("sumsq_blocks", &sumsq_blocks);
+  m.def("sumsq", &sumsq);
+  m.def("clip_finalize", &clip_finalize);
+  m.def("adamw", &adamw);
+  m.def("scale_", &scale_);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("nf4_quantize", &nf4_quantize);
+  m.def("nf4_dequantize", &nf4_dequantize);
+}

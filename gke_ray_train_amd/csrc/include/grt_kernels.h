@@ -1,0 +1,111 @@
+// Host-side launcher API of the HIP kernels. Kernel translation units (*.hip) implement these;
+// the torch bindings (bindings/ops.cpp) call them with raw pointers on the current HIP stream.
+// Keeping torch headers out of the device TUs keeps them fast to compile and free of any
+// framework coupling.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace grt {
+
+enum class DType : int { F32 = 0, BF16 = 1 };
+
+// ---------------- normalisation (norm.hip) ----------------
+// y = norm(x [+ residual]) * w [+ b]; writes rstd (and mean for LayerNorm) per row in fp32.
+// If residual != nullptr, h = x + residual is written to h_out (the new residual stream).
+void rmsnorm_fwd(DType dt, const void* x, const void* residual, const void* w, void* y, void* h_out,
+                 float* rstd, int64_t rows, int d, float eps, hipStream_t s);
+// dx = d/dh (norm) + dres ; dw accumulated through fp32 partials (workspace of
+// rmsnorm_bwd_workspace(rows, d) floats).
+void rmsnorm_bwd(DType dt, const void* dy, const void* h, const void* w, const float* rstd,
+                 const void* dres, void* dx, float* dw_f32, float* ws, int64_t rows, int d,
+                 hipStream_t s);
+int64_t norm_bwd_workspace_floats(int64_t rows, int d);
+void layernorm_fwd(DType dt, const void* x, const void* residual, const void* w, const void* b,
+                   void* y, void* h_out, float* mean, float* rstd, int64_t rows, int d, float eps,
+                   hipStream_t s);
+void layernorm_bwd(DType dt, const void* dy, const void* h, const void* w, const float* mean,
+                   const float* rstd, const void* dres, void* dx, float* dw_f32, float* db_f32,
+                   float* ws, int64_t rows, int d, hipStream_t s);
+
+// ---------------- elementwise (elementwise.hip) ----------------
+void swiglu_fwd(DType dt, const void* gu, void* out, int64_t rows, int f, hipStream_t s);
+void swiglu_bwd(DType dt, const void* gu, const void* dout, void* dgu, int64_t rows, int f,
+                hipStream_t s);
+// GELU (erf form) with optional fused dropout mask (uint8, 1 = keep, scale applied).
+void gelu_fwd(DType dt, const void* x, void* y, int64_t n, hipStream_t s);
+void gelu_bwd(DType dt, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s);
+// RoPE (rotate-half convention). qkv: [T, (hq + 2*hkv) * D] fused projection output with row
+// stride `ld`; writes q_out [T, hq, D], k_out [T, hkv, D] contiguous. cos/sin: [S, D/2] fp32,
+// position of token t is pos[t] (int32) or t % S when pos == nullptr.
+void rope_fwd(DType dt, const void* qkv, int64_t ld, void* q_out, void* k_out, const float* cos,
+              const float* sin, const int32_t* pos, int64_t T, int S, int hq, int hkv, int D,
+              hipStream_t s);
+// Inverse rotation of dq/dk, written into the q and k column ranges of dqkv (row stride ld).
+void rope_bwd(DType dt, const void* dq, const void* dk, void* dqkv, int64_t ld, const float* cos,
+              const float* sin, const int32_t* pos, int64_t T, int S, int hq, int hkv, int D,
+              hipStream_t s);
+// out = emb * scale + pe[t % S]   (BasicLLM input path; pe may be null)
+void scale_add_pe(DType dt, const void* emb, const float* pe, void* out, int64_t T, int S, int d,
+                  float scale, hipStream_t s);
+// Dropout with a counter-based hash RNG; mask bytes written for backward.
+void dropout_fwd(DType dt, const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed,
+                 uint64_t offset, hipStream_t s);
+void dropout_bwd(DType dt, const void* dy, const uint8_t* mask, void* dx, int64_t n, float p,
+                 hipStream_t s);
+
+// ---------------- cross entropy (cross_entropy.hip) ----------------
+void cross_entropy_fwd(DType dt, const void* logits, int64_t ld, const int64_t* labels, float* loss,
+                       float* lse, int64_t rows, int V, int64_t ignore_index, hipStream_t s);
+// dlogits = (softmax - onehot) * gscale[row]  (gscale = dloss per row); may alias logits.
+void cross_entropy_bwd(DType dt, const void* logits, int64_t ld, const int64_t* labels,
+                       const float* lse, const float* gscale, void* dlogits, int64_t ldd,
+                       int64_t rows, int V, int64_t ignore_index, hipStream_t s);
+
+// ---------------- optimizer (optim.hip) ----------------
+// Sum of squares of flat tensors; writes partials into ws[nblocks] then total into out[0].
+int optim_sumsq_blocks();
+void sumsq_accumulate(DType dt, const void* x, int64_t n, float* ws, int slot, hipStream_t s);
+// Finalise: norm = sqrt(sum(ws[0:nparts])) * prescale; out[0] = norm,
+// out[1] = min(1, max_norm / (norm + 1e-6)) * prescale  (clip disabled when max_norm <= 0).
+void clip_coef_finalize(const float* ws, int nparts, float max_norm, float prescale, float* out,
+                        hipStream_t s);
+// Fused AdamW on a flat range. hyper (device): [lr, beta1, beta2, eps, weight_decay, bc1, bc2,
+// grad_scale]; grad_scale_ptr (device, may be null) multiplies grads (clip coefficient).
+void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
+                int64_t n, const float* hyper, const float* grad_scale_ptr, hipStream_t s);
+// Scale in place: x *= a (device scalar pointer or host value when a_ptr == null).
+void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s);
+
+// ---------------- attention (attention.hip) ----------------
+struct AttnParams {
+  const void* q; const void* k; const void* v; void* o; float* lse;
+  int64_t q_bs, q_ss, q_hs;   // strides (elements) for batch, seq, head; last dim contiguous
+  int64_t k_bs, k_ss, k_hs;
+  int64_t v_bs, v_ss, v_hs;
+  int64_t o_bs, o_ss, o_hs;
+  int B, Sq, Sk, Hq, Hkv, D;
+  float scale;
+  int causal;
+  const int32_t* seqlens_k;   // optional per-batch valid key length (right padding), may be null
+};
+void attn_fwd(const AttnParams& p, hipStream_t s);
+struct AttnBwdParams {
+  AttnParams f;
+  const void* dout; int64_t do_bs, do_ss, do_hs;
+  void* dq; int64_t dq_bs, dq_ss, dq_hs;
+  void* dk; int64_t dk_bs, dk_ss, dk_hs;
+  void* dv; int64_t dv_bs, dv_ss, dv_hs;
+  float* dq_acc;   // fp32 workspace [B, Hq, Sq, D]
+  float* delta;    // fp32 workspace [B, Hq, Sq]
+};
+void attn_bwd(const AttnBwdParams& p, hipStream_t s);
+int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int D);
+
+// ---------------- 4-bit NormalFloat (nf4.hip) ----------------
+void nf4_quantize(DType dt, const void* w, uint8_t* q, float* absmax, int64_t n, int blocksize,
+                  hipStream_t s);
+void nf4_dequantize(DType dt, const uint8_t* q, const float* absmax, void* w, int64_t n,
+                    int blocksize, hipStream_t s);
+
+}  // namespace grt

@@ -1,0 +1,284 @@
+// Elementwise / layout kernels for gfx950: SwiGLU, GELU(erf), RoPE, embedding-scale+PE, dropout.
+//
+// Reference roles: K-B08 SwiGLU and K-B06 RoPE of the Llama SFT path
+// (reference ray-jobs/fine_tune_llama_ray.py:240), K-A02/K-A08 scale+PE / GELU / dropout of
+// BasicLLM (reference ray-jobs/pytorch_llm_ray.py:57-105).
+//
+// All are HBM-bound: 16-byte vector accesses per lane (cdna_hip_programming.md Guideline 13),
+// grid capped at 256 CUs x 8 workgroups and grid-strided (Guideline 11). RoPE reads the fused
+// QKV projection output in place (row stride `ld`) and writes attention-ready q/k, so there is
+// no transpose or split copy anywhere in the attention block.
+#include "grt_common.h"
+#include "grt_kernels.h"
+
+namespace grt {
+namespace {
+
+constexpr int kNT = 256;
+constexpr int kMaxGrid = 256 * 8;
+
+inline unsigned grid_for(int64_t work) {
+  int64_t g = (work + kNT - 1) / kNT;
+  if (g > kMaxGrid) g = kMaxGrid;
+  if (g < 1) g = 1;
+  return (unsigned)g;
+}
+
+// ------------------------------- SwiGLU -------------------------------------
+// gu: [rows, 2F] = [gate | up]; out = silu(gate) * up
+template <typename T>
+__global__ __launch_bounds__(kNT) void swiglu_fwd_kernel(const T* __restrict__ gu, T* __restrict__ out,
+                                                         int64_t rows, int f) {
+  constexpr int V = Vec16<T>::N;
+  const int vpr = f / V;
+  const int64_t total = rows * vpr;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kNT) {
+    const int64_t r = i / vpr;
+    const int c = (int)(i - r * vpr) * V;
+    float g[V], u[V], o[V];
+    load16(gu + r * 2 * f + c, g);
+    load16(gu + r * 2 * f + f + c, u);
+#pragma unroll
+    for (int k = 0; k < V; ++k) o[k] = g[k] * sigmoidf_(g[k]) * u[k];
+    store16(out + r * f + c, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void swiglu_bwd_kernel(const T* __restrict__ gu, const T* __restrict__ dout,
+                                                         T* __restrict__ dgu, int64_t rows, int f) {
+  constexpr int V = Vec16<T>::N;
+  const int vpr = f / V;
+  const int64_t total = rows * vpr;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kNT) {
+    const int64_t r = i / vpr;
+    const int c = (int)(i - r * vpr) * V;
+    float g[V], u[V], d[V], dg[V], du[V];
+    load16(gu + r * 2 * f + c, g);
+    load16(gu + r * 2 * f + f + c, u);
+    load16(dout + r * f + c, d);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float sg = sigmoidf_(g[k]);
+      const float silu = g[k] * sg;
+      du[k] = d[k] * silu;
+      dg[k] = d[k] * u[k] * sg * (1.f + g[k] * (1.f - sg));
+    }
+    store16(dgu + r * 2 * f + c, dg);
+    store16(dgu + r * 2 * f + f + c, du);
+  }
+}
+
+// ------------------------------- GELU (erf) ---------------------------------
+template <typename T>
+__global__ __launch_bounds__(kNT) void gelu_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t nv) {
+  constexpr int V = Vec16<T>::N;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kNT) {
+    float a[V];
+    load16(x + i * V, a);
+#pragma unroll
+    for (int k = 0; k < V; ++k) a[k] = 0.5f * a[k] * (1.f + erff(a[k] * 0.70710678118654752f));
+    store16(y + i * V, a);
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(kNT) void gelu_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                       T* __restrict__ dx, int64_t nv) {
+  constexpr int V = Vec16<T>::N;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < nv; i += (int64_t)gridDim.x * kNT) {
+    float a[V], g[V];
+    load16(x + i * V, a);
+    load16(dy + i * V, g);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      const float cdf = 0.5f * (1.f + erff(a[k] * 0.70710678118654752f));
+      const float pdf = 0.3989422804014327f * __expf(-0.5f * a[k] * a[k]);
+      g[k] *= cdf + a[k] * pdf;
+    }
+    store16(dx + i * V, g);
+  }
+}
+
+// ------------------------------- RoPE ---------------------------------------
+// One thread = 8 rotation pairs (i .. i+7 with partners i+D/2 ..) of one (token, head).
+template <typename T, bool FWD>
+__global__ __launch_bounds__(kNT) void rope_kernel(const T* __restrict__ src_q, const T* __restrict__ src_k,
+                                                   int64_t src_ld_q, int64_t src_ld_k,
+                                                   T* __restrict__ dst_q, T* __restrict__ dst_k,
+                                                   int64_t dst_ld_q, int64_t dst_ld_k,
+                                                   const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                   const int32_t* __restrict__ pos, int64_t T_, int S,
+                                                   int hq, int hkv, int D) {
+  const int half = D / 2;
+  const int gpp = half / 8;                 // 8-pair groups per head
+  const int heads = hq + hkv;
+  const int64_t total = T_ * heads * gpp;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kNT) {
+    const int g = (int)(i % gpp);
+    const int64_t th = i / gpp;
+    const int h = (int)(th % heads);
+    const int64_t t = th / heads;
+    const int p = pos ? pos[t] : (int)(t % S);
+    const T* src;
+    T* dst;
+    if (h < hq) {
+      src = src_q + t * src_ld_q + (int64_t)h * D;
+      dst = dst_q + t * dst_ld_q + (int64_t)h * D;
+    } else {
+      src = src_k + t * src_ld_k + (int64_t)(h - hq) * D;
+      dst = dst_k + t * dst_ld_k + (int64_t)(h - hq) * D;
+    }
+    const int c = g * 8;
+    float x1[8], x2[8], cs[8], sn[8], o1[8], o2[8];
+    if constexpr (Vec16<T>::N == 8) {
+      load16(src + c, x1);
+      load16(src + half + c, x2);
+    } else {
+      load16(src + c, x1); load16(src + c + 4, x1 + 4);
+      load16(src + half + c, x2); load16(src + half + c + 4, x2 + 4);
+    }
+    load16(cosb + (int64_t)p * half + c, cs); load16(cosb + (int64_t)p * half + c + 4, cs + 4);
+    load16(sinb + (int64_t)p * half + c, sn); load16(sinb + (int64_t)p * half + c + 4, sn + 4);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float s = FWD ? sn[k] : -sn[k];
+      o1[k] = x1[k] * cs[k] - x2[k] * s;
+      o2[k] = x2[k] * cs[k] + x1[k] * s;
+    }
+    if constexpr (Vec16<T>::N == 8) {
+      store16(dst + c, o1);
+      store16(dst + half + c, o2);
+    } else {
+      store16(dst + c, o1); store16(dst + c + 4, o1 + 4);
+      store16(dst + half + c, o2); store16(dst + half + c + 4, o2 + 4);
+    }
+  }
+}
+
+// ------------------------- embedding scale + sinusoidal PE ------------------
+template <typename T>
+__global__ __launch_bounds__(kNT) void scale_add_pe_kernel(const T* __restrict__ emb, const float* __restrict__ pe,
+                                                           T* __restrict__ out, int64_t T_, int S, int d,
+                                                           float scale) {
+  constexpr int V = Vec16<T>::N;
+  const int vpr = d / V;
+  const int64_t total = T_ * vpr;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kNT) {
+    const int64_t t = i / vpr;
+    const int c = (int)(i - t * vpr) * V;
+    float a[V];
+    load16(emb + t * d + c, a);
+    if (pe != nullptr) {
+      float p[V];
+      const float* pr = pe + (int64_t)(t % S) * d + c;
+#pragma unroll
+      for (int k = 0; k < V; k += 4) load16(pr + k, p + k);
+#pragma unroll
+      for (int k = 0; k < V; ++k) a[k] = a[k] * scale + p[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k) a[k] *= scale;
+    }
+    store16(out + t * d + c, a);
+  }
+}
+
+// ------------------------------- dropout -------------------------------------
+__device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
+  // splitmix64 finaliser: counter-based, stateless, graph-replay safe (seed/offset are args)
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)x;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void dropout_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                          uint8_t* __restrict__ mask, int64_t n, float p,
+                                                          uint64_t seed, uint64_t offset) {
+  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  const float sc = 1.f / (1.f - p);
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+    const uint32_t r = hash_u32((seed << 40) ^ (offset + (uint64_t)i));
+    const bool keep = r >= thr;
+    mask[i] = keep;
+    y[i] = from_f<T>(keep ? to_f(x[i]) * sc : 0.f);
+  }
+}
+template <typename T>
+__global__ __launch_bounds__(kNT) void dropout_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ mask,
+                                                          T* __restrict__ dx, int64_t n, float p) {
+  const float sc = 1.f / (1.f - p);
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+    dx[i] = from_f<T>(mask[i] ? to_f(dy[i]) * sc : 0.f);
+}
+
+}  // namespace
+
+#define GRT_DISPATCH(dt, KERNEL, ...)                                  \
+  do {                                                                 \
+    if ((dt) == DType::BF16) { KERNEL(bf16, __VA_ARGS__); }            \
+    else { KERNEL(float, __VA_ARGS__); }                               \
+  } while (0)
+
+void swiglu_fwd(DType dt, const void* gu, void* out, int64_t rows, int f, hipStream_t s) {
+#define K(T, ...) hipLaunchKernelGGL(swiglu_fwd_kernel<T>, dim3(grid_for(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)gu, (T*)out, rows, f)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+void swiglu_bwd(DType dt, const void* gu, const void* dout, void* dgu, int64_t rows, int f, hipStream_t s) {
+#define K(T, ...) hipLaunchKernelGGL(swiglu_bwd_kernel<T>, dim3(grid_for(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)gu, (const T*)dout, (T*)dgu, rows, f)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+void gelu_fwd(DType dt, const void* x, void* y, int64_t n, hipStream_t s) {
+#define K(T, ...) hipLaunchKernelGGL(gelu_fwd_kernel<T>, dim3(grid_for(n / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)x, (T*)y, n / Vec16<T>::N)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+void gelu_bwd(DType dt, const void* x, const void* dy, void* dx, int64_t n, hipStream_t s) {
+#define K(T, ...) hipLaunchKernelGGL(gelu_bwd_kernel<T>, dim3(grid_for(n / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)x, (const T*)dy, (T*)dx, n / Vec16<T>::N)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+void rope_fwd(DType dt, const void* qkv, int64_t ld, void* q_out, void* k_out, const float* cos,
+              const float* sin, const int32_t* pos, int64_t T_, int S, int hq, int hkv, int D,
+              hipStream_t s) {
+  const int64_t work = T_ * (hq + hkv) * (D / 16);
+#define K(TY, ...) hipLaunchKernelGGL((rope_kernel<TY, true>), dim3(grid_for(work)), dim3(kNT), 0, s, \
+      (const TY*)qkv, (const TY*)qkv + (int64_t)hq * D, ld, ld, (TY*)q_out, (TY*)k_out, (int64_t)hq * D, \
+      (int64_t)hkv * D, cos, sin, pos, T_, S, hq, hkv, D)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+void rope_bwd(DType dt, const void* dq, const void* dk, void* dqkv, int64_t ld, const float* cos,
+              const float* sin, const int32_t* pos, int64_t T_, int S, int hq, int hkv, int D,
+              hipStream_t s) {
+  const int64_t work = T_ * (hq + hkv) * (D / 16);
+#define K(TY, ...) hipLaunchKernelGGL((rope_kernel<TY, false>), dim3(grid_for(work)), dim3(kNT), 0, s, \
+      (const TY*)dq, (const TY*)dk, (int64_t)hq * D, (int64_t)hkv * D, (TY*)dqkv, (TY*)dqkv + (int64_t)hq * D, \
+      ld, ld, cos, sin, pos, T_, S, hq, hkv, D)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+void scale_add_pe(DType dt, const void* emb, const float* pe, void* out, int64_t T_, int S, int d,
+                  float scale, hipStream_t s) {
+#define K(T, ...) hipLaunchKernelGGL(scale_add_pe_kernel<T>, dim3(grid_for(T_ * d / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)emb, pe, (T*)out, T_, S, d, scale)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+void dropout_fwd(DType dt, const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed,
+                 uint64_t offset, hipStream_t s) {
+#define K(T, ...) hipLaunchKernelGGL(dropout_fwd_kernel<T>, dim3(grid_for(n)), dim3(kNT), 0, s, (const T*)x, (T*)y, mask, n, p, seed, offset)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+void dropout_bwd(DType dt, const void* dy, const uint8_t* mask, void* dx, int64_t n, float p,
+                 hipStream_t s) {
+#define K(T, ...) hipLaunchKernelGGL(dropout_bwd_kernel<T>, dim3(grid_for(n)), dim3(kNT), 0, s, (const T*)dy, mask, (T*)dx, n, p)
+  GRT_DISPATCH(dt, K, 0);
+#undef K
+}
+
+}  // namespace grt

@@ -1,0 +1,94 @@
+// 4-bit NormalFloat (NF4) block quantisation for QLoRA on gfx950.
+//
+// Reference role: BitsAndBytesConfig(load_in_4bit, bnb_4bit_quant_type="nf4",
+// compute_dtype=bf16) in the SFT job (reference ray-jobs/fine_tune_llama_ray.py:215-227,
+// ray-jobs/fine_tune_config.json:9-11); SURVEY §2.6 K-B03 / K-B14.
+//
+// Format: blocks of `blocksize` (64) consecutive weights share one fp32 absmax; each weight is a
+// 4-bit index into the 16-level NF4 code book (quantiles of N(0,1), QLoRA paper). Two codes
+// per byte, element 2i in the high nibble. Dequantisation writes 16 bytes of bf16 per lane.
+#include "grt_common.h"
+#include "grt_kernels.h"
+
+namespace grt {
+namespace {
+
+__constant__ float kNF4[16] = {
+    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
+    -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
+    0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f, 0.33791524171829224f,
+    0.44070982933044434f, 0.5626170039176941f, 0.7229568362236023f, 1.0f};
+
+__device__ __forceinline__ uint32_t nf4_code(float x) {
+  // nearest code: midpoints between sorted levels
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 15; ++i) c += (x > 0.5f * (kNF4[i] + kNF4[i + 1])) ? 1u : 0u;
+  return c;
+}
+
+// one lane = 2 consecutive weights; blocksize/2 lanes share an absmax (blocksize in {32,64,128})
+template <typename T>
+__global__ __launch_bounds__(256) void nf4_quant_kernel(const T* __restrict__ w, uint8_t* __restrict__ q,
+                                                        float* __restrict__ absmax, int64_t n, int bs) {
+  const int64_t pair = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t i = pair * 2;
+  const float a = i < n ? to_f(w[i]) : 0.f;
+  const float b = i + 1 < n ? to_f(w[i + 1]) : 0.f;
+  float m = fmaxf(fabsf(a), fabsf(b));
+  const int lanes = bs / 2;  // lanes per quant block, power of two <= 64
+  for (int o = lanes / 2; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (i < n) {
+    const float inv = m > 0.f ? 1.f / m : 0.f;
+    q[pair] = (uint8_t)((nf4_code(a * inv) << 4) | nf4_code(b * inv));
+    if ((threadIdx.x & (lanes - 1)) == 0) absmax[i / bs] = m;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restrict__ q,
+                                                          const float* __restrict__ absmax, T* __restrict__ w,
+                                                          int64_t n, int bs) {
+  // one lane = 8 weights (4 code bytes)
+  const int64_t n8 = n / 8;
+  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < n8; g += (int64_t)gridDim.x * 256) {
+    const uint32_t codes = *reinterpret_cast<const uint32_t*>(q + g * 4);
+    const float s = absmax[(g * 8) / bs];
+    float o[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t byte = (codes >> (8 * k)) & 0xFF;
+      o[2 * k] = kNF4[byte >> 4] * s;
+      o[2 * k + 1] = kNF4[byte & 15] * s;
+    }
+    if constexpr (Vec16<T>::N == 8) {
+      store16(w + g * 8, o);
+    } else {
+      store16(w + g * 8, o);
+      store16(w + g * 8 + 4, o + 4);
+    }
+  }
+}
+
+}  // namespace
+
+void nf4_quantize(DType dt, const void* w, uint8_t* q, float* absmax, int64_t n, int blocksize, hipStream_t s) {
+  const unsigned grid = (unsigned)((n / 2 + 255) / 256);
+  if (dt == DType::BF16)
+    hipLaunchKernelGGL(nf4_quant_kernel<bf16>, dim3(grid), dim3(256), 0, s, (const bf16*)w, q, absmax, n, blocksize);
+  else
+    hipLaunchKernelGGL(nf4_quant_kernel<float>, dim3(grid), dim3(256), 0, s, (const float*)w, q, absmax, n, blocksize);
+}
+
+void nf4_dequantize(DType dt, const uint8_t* q, const float* absmax, void* w, int64_t n, int blocksize,
+                    hipStream_t s) {
+  int64_t g = (n / 8 + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  if (dt == DType::BF16)
+    hipLaunchKernelGGL(nf4_dequant_kernel<bf16>, dim3((unsigned)g), dim3(256), 0, s, q, absmax, (bf16*)w, n, blocksize);
+  else
+    hipLaunchKernelGGL(nf4_dequant_kernel<float>, dim3((unsigned)g), dim3(256), 0, s, q, absmax, (float*)w, n, blocksize);
+}
+
+}  // namespace grt

@@ -1,0 +1,280 @@
+// RMSNorm / LayerNorm forward + backward for gfx950, with a fused residual add.
+//
+// Role in the reference: every Llama decoder layer runs two RMSNorms and BasicLLM's post-LN
+// nn.TransformerEncoderLayer runs two LayerNorms after a residual add
+// (reference ray-jobs/pytorch_llm_ray.py:82-86).
+//
+// Design (memory-bound, MI355X_MICROARCH.md §HBM):
+//   * one 64-lane wave per row, 16-byte vector loads (8 x bf16 / 4 x f32 per lane),
+//     the row stays in VGPRs between the reduction and the normalisation (one HBM read);
+//   * the residual add is fused: h = x + residual is produced and stored in the same pass,
+//     so the decoder layer never runs a separate elementwise add;
+//   * backward keeps the weight-gradient partial sums in registers across the rows a
+//     workgroup visits and writes one fp32 slab per workgroup; a second tiny kernel sums the
+//     slabs column-wise (no float atomics, bitwise reproducible).
+#include "grt_common.h"
+#include "grt_kernels.h"
+
+namespace grt {
+namespace {
+
+constexpr int kNT = 256;          // 4 waves per workgroup
+constexpr int kRowsPerBlock = kNT / kWave;
+constexpr int kBwdMaxBlocks = 512;
+
+template <typename T, int MAXC, bool RMS>
+__global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
+                                                       const T* __restrict__ res,
+                                                       const T* __restrict__ w,
+                                                       const T* __restrict__ b, T* __restrict__ y,
+                                                       T* __restrict__ h_out, float* __restrict__ mean_out,
+                                                       float* __restrict__ rstd_out, int64_t rows,
+                                                       int d, float eps) {
+  constexpr int V = Vec16<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nchunk = d / V;
+  const T* xr = x + row * d;
+  float hv[MAXC][V];
+  float s1 = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * kWave;
+    if (ch < nchunk) {
+      load16(xr + ch * V, hv[c]);
+      if (res != nullptr) {
+        float rv[V];
+        load16(res + row * d + ch * V, rv);
+#pragma unroll
+        for (int i = 0; i < V; ++i) hv[c][i] = to_f(from_f<T>(hv[c][i] + rv[i]));  // round like torch
+        store16(h_out + row * d + ch * V, hv[c]);
+      }
+#pragma unroll
+      for (int i = 0; i < V; ++i) s1 += RMS ? hv[c][i] * hv[c][i] : hv[c][i];
+    }
+  }
+  s1 = wave_sum(s1);
+  float mu = 0.f, rstd;
+  if (RMS) {
+    rstd = rsqrtf(s1 / d + eps);
+  } else {
+    mu = s1 / d;
+    float s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = lane + c * kWave;
+      if (ch < nchunk) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) { const float t = hv[c][i] - mu; s2 += t * t; }
+      }
+    }
+    s2 = wave_sum(s2);
+    rstd = rsqrtf(s2 / d + eps);
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = lane + c * kWave;
+    if (ch < nchunk) {
+      float wv[V], o[V];
+      load16(w + ch * V, wv);
+      if (!RMS && b != nullptr) {
+        float bv[V];
+        load16(b + ch * V, bv);
+#pragma unroll
+        for (int i = 0; i < V; ++i) o[i] = (hv[c][i] - mu) * rstd * wv[i] + bv[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) o[i] = (hv[c][i] - mu) * rstd * wv[i];
+      }
+      store16(y + row * d + ch * V, o);
+    }
+  }
+  if (lane == 0) {
+    rstd_out[row] = rstd;
+    if (!RMS) mean_out[row] = mu;
+  }
+}
+
+// Backward: one 256-thread workgroup per row (grid-strided), each thread owns MAXC 16-byte
+// column chunks, so the dw/db partial sums stay in a handful of VGPRs per thread for every
+// row the workgroup visits and are written once as this workgroup's fp32 slab.
+template <typename T, int MAXC, bool RMS>
+__global__ __launch_bounds__(kNT) void norm_bwd_kernel(const T* __restrict__ dy,
+                                                       const T* __restrict__ h,
+                                                       const T* __restrict__ w,
+                                                       const float* __restrict__ mean,
+                                                       const float* __restrict__ rstd,
+                                                       const T* __restrict__ dres, T* __restrict__ dx,
+                                                       float* __restrict__ ws, int64_t rows, int d) {
+  constexpr int V = Vec16<T>::N;
+  __shared__ float red[2 * kRowsPerBlock];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nchunk = d / V;
+  float dwp[MAXC][V], dbp[MAXC][V], wv[MAXC][V];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = tid + c * kNT;
+#pragma unroll
+    for (int i = 0; i < V; ++i) { dwp[c][i] = 0.f; dbp[c][i] = 0.f; wv[c][i] = 0.f; }
+    if (ch < nchunk) load16(w + ch * V, wv[c]);
+  }
+  for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    const float r = rstd[row];
+    const float mu = RMS ? 0.f : mean[row];
+    float xh[MAXC][V], g[MAXC][V];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = tid + c * kNT;
+      if (ch < nchunk) {
+        float dv[V];
+        load16(h + row * d + ch * V, xh[c]);
+        load16(dy + row * d + ch * V, dv);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+          xh[c][i] = (xh[c][i] - mu) * r;
+          g[c][i] = dv[i] * wv[c][i];
+          sg += g[c][i];
+          sgx += g[c][i] * xh[c][i];
+          dwp[c][i] += dv[i] * xh[c][i];
+          if (!RMS) dbp[c][i] += dv[i];
+        }
+      }
+    }
+    // two-value block reduction, one barrier pair per row
+    sgx = wave_sum(sgx);
+    if (!RMS) sg = wave_sum(sg);
+    if (lane == 0) { red[wid] = sgx; red[kRowsPerBlock + wid] = sg; }
+    __syncthreads();
+    float tsgx = 0.f, tsg = 0.f;
+#pragma unroll
+    for (int i = 0; i < kRowsPerBlock; ++i) { tsgx += red[i]; tsg += red[kRowsPerBlock + i]; }
+    __syncthreads();
+    tsgx /= d;
+    tsg = RMS ? 0.f : tsg / d;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int ch = tid + c * kNT;
+      if (ch < nchunk) {
+        float o[V];
+        if (dres != nullptr) {
+          load16(dres + row * d + ch * V, o);
+        } else {
+#pragma unroll
+          for (int i = 0; i < V; ++i) o[i] = 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i) o[i] += r * (g[c][i] - tsg - xh[c][i] * tsgx);
+        store16(dx + row * d + ch * V, o);
+      }
+    }
+  }
+  float* wsb = ws + (int64_t)blockIdx.x * 2 * d;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = tid + c * kNT;
+    if (ch < nchunk) {
+#pragma unroll
+      for (int i = 0; i < V; ++i) {
+        wsb[ch * V + i] = dwp[c][i];
+        wsb[d + ch * V + i] = dbp[c][i];
+      }
+    }
+  }
+}
+
+// dw[j] = sum_b ws[b][0][j], db[j] = sum_b ws[b][1][j]
+__global__ __launch_bounds__(kNT) void colsum_kernel(const float* __restrict__ ws, int nb, int d,
+                                                     float* __restrict__ dw, float* __restrict__ db) {
+  const int j = blockIdx.x * kNT + threadIdx.x;
+  if (j >= 2 * d) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += ws[(int64_t)b * 2 * d + j];
+  if (j < d) { if (dw) dw[j] = s; }
+  else { if (db) db[j - d] = s; }
+}
+
+template <typename T, bool RMS>
+void launch_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* h_out,
+                float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t s) {
+  constexpr int V = Vec16<T>::N;
+  const int per_lane = (d / V + kWave - 1) / kWave;
+  const dim3 grid((unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock));
+#define GRT_NF(MC)                                                                              \
+  hipLaunchKernelGGL((norm_fwd_kernel<T, MC, RMS>), grid, dim3(kNT), 0, s, (const T*)x,          \
+                     (const T*)res, (const T*)w, (const T*)b, (T*)y, (T*)h_out, mean, rstd, rows, \
+                     d, eps)
+  if (per_lane <= 1) GRT_NF(1);
+  else if (per_lane <= 2) GRT_NF(2);
+  else if (per_lane <= 4) GRT_NF(4);
+  else if (per_lane <= 8) GRT_NF(8);
+  else if (per_lane <= 16) GRT_NF(16);
+  else GRT_NF(32);
+#undef GRT_NF
+}
+
+int bwd_blocks(int64_t rows) {
+  return (int)(rows < kBwdMaxBlocks ? (rows > 0 ? rows : 1) : kBwdMaxBlocks);
+}
+
+template <typename T, bool RMS>
+void launch_bwd(const void* dy, const void* h, const void* w, const float* mean, const float* rstd,
+                const void* dres, void* dx, float* dw, float* db, float* ws, int64_t rows, int d,
+                hipStream_t s) {
+  constexpr int V = Vec16<T>::N;
+  const int per_thr = (d / V + kNT - 1) / kNT;
+  const int nb = bwd_blocks(rows);
+  const size_t lds = 0;
+#define GRT_NB(MC)                                                                             \
+  hipLaunchKernelGGL((norm_bwd_kernel<T, MC, RMS>), dim3(nb), dim3(kNT), lds, s, (const T*)dy, \
+                     (const T*)h, (const T*)w, mean, rstd, (const T*)dres, (T*)dx, ws, rows, d)
+  if (per_thr <= 1) GRT_NB(1);
+  else if (per_thr <= 2) GRT_NB(2);
+  else if (per_thr <= 4) GRT_NB(4);
+  else GRT_NB(8);
+#undef GRT_NB
+  hipLaunchKernelGGL(colsum_kernel, dim3((2 * d + kNT - 1) / kNT), dim3(kNT), 0, s, ws, nb, d, dw,
+                     db);
+}
+
+}  // namespace
+
+int64_t norm_bwd_workspace_floats(int64_t rows, int d) { return (int64_t)bwd_blocks(rows) * 2 * d; }
+
+void rmsnorm_fwd(DType dt, const void* x, const void* residual, const void* w, void* y, void* h_out,
+                 float* rstd, int64_t rows, int d, float eps, hipStream_t s) {
+  if (dt == DType::BF16)
+    launch_fwd<bf16, true>(x, residual, w, nullptr, y, h_out, nullptr, rstd, rows, d, eps, s);
+  else
+    launch_fwd<float, true>(x, residual, w, nullptr, y, h_out, nullptr, rstd, rows, d, eps, s);
+}
+
+void rmsnorm_bwd(DType dt, const void* dy, const void* h, const void* w, const float* rstd,
+                 const void* dres, void* dx, float* dw_f32, float* ws, int64_t rows, int d,
+                 hipStream_t s) {
+  if (dt == DType::BF16)
+    launch_bwd<bf16, true>(dy, h, w, nullptr, rstd, dres, dx, dw_f32, nullptr, ws, rows, d, s);
+  else
+    launch_bwd<float, true>(dy, h, w, nullptr, rstd, dres, dx, dw_f32, nullptr, ws, rows, d, s);
+}
+
+void layernorm_fwd(DType dt, const void* x, const void* residual, const void* w, const void* b,
+                   void* y, void* h_out, float* mean, float* rstd, int64_t rows, int d, float eps,
+                   hipStream_t s) {
+  if (dt == DType::BF16)
+    launch_fwd<bf16, false>(x, residual, w, b, y, h_out, mean, rstd, rows, d, eps, s);
+  else
+    launch_fwd<float, false>(x, residual, w, b, y, h_out, mean, rstd, rows, d, eps, s);
+}
+
+void layernorm_bwd(DType dt, const void* dy, const void* h, const void* w, const float* mean,
+                   const float* rstd, const void* dres, void* dx, float* dw_f32, float* db_f32,
+                   float* ws, int64_t rows, int d, hipStream_t s) {
+  if (dt == DType::BF16)
+    launch_bwd<bf16, false>(dy, h, w, mean, rstd, dres, dx, dw_f32, db_f32, ws, rows, d, s);
+  else
+    launch_bwd<float, false>(dy, h, w, mean, rstd, dres, dx, dw_f32, db_f32, ws, rows, d, s);
+}
+
+}  // namespace grt

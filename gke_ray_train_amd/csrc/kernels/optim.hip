@@ -1,0 +1,193 @@
+// Fused optimizer kernels for gfx950: global grad-norm (clip_grad_norm_) and AdamW.
+//
+// Reference roles: torch.nn.utils.clip_grad_norm_(…, 1.0) + torch.optim.AdamW(wd=0.01) in the
+// BasicLLM hot loop (reference ray-jobs/pytorch_llm_ray.py:236,277-278), and
+// max_grad_norm=0.3 + paged_adamw_32bit in SFT (ray-jobs/fine_tune_config.json:17,19).
+// SURVEY §2.6 K-A12/K-A13, K-B11/K-B12.
+//
+// Design: the data-parallel engines keep parameters and gradients in flat buckets, so the whole
+// optimizer step is TWO passes over HBM for any model size:
+//   1. sum-of-squares of the flat gradient (one fp32 partial per workgroup, no atomics),
+//      finalised on device into [norm, clip_coef] — no host synchronisation, graph-capturable;
+//   2. one fused AdamW pass reading p, g, m, v (+fp32 master) once and writing p, m, v once,
+//      with the clip coefficient read from device memory.
+// Hyper-parameters come from a small device array so lr schedules do not bake into a captured
+// hipGraph. Optimizer state is always fp32 ("32-bit" AdamW); params may be bf16 or fp32.
+#include "grt_common.h"
+#include "grt_kernels.h"
+
+namespace grt {
+namespace {
+
+constexpr int kNT = 256;
+constexpr int kSumBlocks = 1024;
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void sumsq_kernel(const T* __restrict__ x, int64_t n, float* __restrict__ out) {
+  __shared__ float red[kNT / kWave];
+  constexpr int V = Vec16<T>::N;
+  const int64_t nv = n / V;
+  float acc = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * kNT;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < nv; i += stride) {
+    float a[V];
+    load16(x + i * V, a);
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc += a[k] * a[k];
+  }
+  for (int64_t j = nv * V + (int64_t)blockIdx.x * kNT + threadIdx.x; j < n; j += stride) {
+    const float a = to_f(x[j]);
+    acc += a * a;
+  }
+  acc = block_sum<kNT>(acc, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
+}
+
+__global__ __launch_bounds__(kNT) void clip_finalize_kernel(const float* __restrict__ ws, int nparts,
+                                                            float max_norm, float prescale,
+                                                            float* __restrict__ out) {
+  __shared__ float red[kNT / kWave];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += kNT) acc += ws[i];
+  acc = block_sum<kNT>(acc, red);
+  if (threadIdx.x == 0) {
+    // prescale folds the data-parallel 1/world average into the same coefficient, so the
+    // reducer can all-reduce with SUM and no separate averaging pass ever touches the grads.
+    const float norm = sqrtf(acc) * prescale;
+    out[0] = norm;
+    out[1] = ((max_norm > 0.f) ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f) * prescale;
+  }
+}
+
+template <typename P, typename G>
+__global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    float* __restrict__ master, int64_t n,
+                                                    const float* __restrict__ hyper,
+                                                    const float* __restrict__ gsp) {
+  const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const float bc1 = hyper[5], bc2 = hyper[6];
+  const float gs = hyper[7] * (gsp ? gsp[1] : 1.f);
+  const float step = lr / bc1;
+  const float rbc2 = rsqrtf(bc2);
+  const float decay = 1.f - lr * wd;
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * kNT;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n4; i += stride) {
+    const int64_t o = i * 4;
+    f32x4 mv = *reinterpret_cast<const f32x4*>(m + o);
+    f32x4 vv = *reinterpret_cast<const f32x4*>(v + o);
+    float pf[4], gf[4];
+    if (master) {
+      f32x4 t = *reinterpret_cast<const f32x4*>(master + o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pf[k] = t[k];
+    } else if constexpr (sizeof(P) == 2) {
+      bf16x4 t = *reinterpret_cast<const bf16x4*>(p + o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pf[k] = to_f(t[k]);
+    } else {
+      f32x4 t = *reinterpret_cast<const f32x4*>(p + o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) pf[k] = t[k];
+    }
+    if constexpr (sizeof(G) == 2) {
+      bf16x4 t = *reinterpret_cast<const bf16x4*>(g + o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gf[k] = to_f(t[k]) * gs;
+    } else {
+      f32x4 t = *reinterpret_cast<const f32x4*>(g + o);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gf[k] = t[k] * gs;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      mv[k] = b1 * mv[k] + (1.f - b1) * gf[k];
+      vv[k] = b2 * vv[k] + (1.f - b2) * gf[k] * gf[k];
+      const float denom = sqrtf(vv[k]) * rbc2 + eps;
+      pf[k] = pf[k] * decay - step * mv[k] / denom;
+    }
+    *reinterpret_cast<f32x4*>(m + o) = mv;
+    *reinterpret_cast<f32x4*>(v + o) = vv;
+    if (master) {
+      f32x4 t;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] = pf[k];
+      *reinterpret_cast<f32x4*>(master + o) = t;
+    }
+    if constexpr (sizeof(P) == 2) {
+      bf16x4 t;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] = from_f<bf16>(pf[k]);
+      *reinterpret_cast<bf16x4*>(p + o) = t;
+    } else {
+      f32x4 t;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) t[k] = pf[k];
+      *reinterpret_cast<f32x4*>(p + o) = t;
+    }
+  }
+  // scalar tail (n % 4)
+  for (int64_t j = n4 * 4 + (int64_t)blockIdx.x * kNT + threadIdx.x; j < n; j += stride) {
+    float pf = master ? master[j] : to_f(p[j]);
+    const float gf = to_f(g[j]) * gs;
+    m[j] = b1 * m[j] + (1.f - b1) * gf;
+    v[j] = b2 * v[j] + (1.f - b2) * gf * gf;
+    pf = pf * decay - step * m[j] / (sqrtf(v[j]) * rbc2 + eps);
+    if (master) master[j] = pf;
+    p[j] = from_f<P>(pf);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void scale_kernel(T* __restrict__ x, int64_t n, float a,
+                                                    const float* __restrict__ ap) {
+  const float s = ap ? ap[0] : a;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+    x[i] = from_f<T>(to_f(x[i]) * s);
+}
+
+unsigned grid_for(int64_t work) {
+  int64_t g = (work + kNT - 1) / kNT;
+  if (g > 256 * 8) g = 256 * 8;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+}  // namespace
+
+int optim_sumsq_blocks() { return kSumBlocks; }
+
+void sumsq_accumulate(DType dt, const void* x, int64_t n, float* ws, int slot, hipStream_t s) {
+  float* out = ws + (int64_t)slot * kSumBlocks;
+  if (dt == DType::BF16)
+    hipLaunchKernelGGL(sumsq_kernel<bf16>, dim3(kSumBlocks), dim3(kNT), 0, s, (const bf16*)x, n, out);
+  else
+    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(kSumBlocks), dim3(kNT), 0, s, (const float*)x, n, out);
+}
+
+void clip_coef_finalize(const float* ws, int nparts, float max_norm, float prescale, float* out,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(clip_finalize_kernel, dim3(1), dim3(kNT), 0, s, ws, nparts, max_norm, prescale, out);
+}
+
+void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
+                int64_t n, const float* hyper, const float* gsp, hipStream_t s) {
+  const dim3 grid(grid_for(n / 4 + 1));
+  if (pdt == DType::BF16 && gdt == DType::BF16)
+    hipLaunchKernelGGL((adamw_kernel<bf16, bf16>), grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, master, n, hyper, gsp);
+  else if (pdt == DType::BF16)
+    hipLaunchKernelGGL((adamw_kernel<bf16, float>), grid, dim3(kNT), 0, s, (bf16*)p, (const float*)g, m, v, master, n, hyper, gsp);
+  else if (gdt == DType::BF16)
+    hipLaunchKernelGGL((adamw_kernel<float, bf16>), grid, dim3(kNT), 0, s, (float*)p, (const bf16*)g, m, v, master, n, hyper, gsp);
+  else
+    hipLaunchKernelGGL((adamw_kernel<float, float>), grid, dim3(kNT), 0, s, (float*)p, (const float*)g, m, v, master, n, hyper, gsp);
+}
+
+void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s) {
+  if (dt == DType::BF16)
+    hipLaunchKernelGGL(scale_kernel<bf16>, dim3(grid_for(n)), dim3(kNT), 0, s, (bf16*)x, n, a, a_ptr);
+  else
+    hipLaunchKernelGGL(scale_kernel<float>, dim3(grid_for(n)), dim3(kNT), 0, s, (float*)x, n, a, a_ptr);
+}
+
+}  // namespace grt

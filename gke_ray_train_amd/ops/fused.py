@@ -1,0 +1,326 @@
+"""Autograd wrappers around the gfx950 HIP kernels.
+
+Every op dispatches on the tensor's device: GPU tensors ALWAYS go to the native kernel (a
+missing ``_C.so`` raises, see ``_native.py``); CPU tensors use ``_ref`` so the whole framework
+(models, DDP over gloo, trainers) runs and is tested on CPU-only hosts.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .. import _native
+from . import _ref
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ----------------------------------------------------------------------------- RMSNorm
+class _RMSNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        C = _native.kernels()
+        xc = x.contiguous()
+        y, _, rstd = C.rmsnorm_fwd(xc, None, w.contiguous(), eps)
+        ctx.save_for_backward(xc, w, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, rstd = ctx.saved_tensors
+        dx, dw = _native.kernels().rmsnorm_bwd(dy.contiguous(), x, w, rstd, None)
+        return dx, dw.to(w.dtype), None
+
+
+class _AddRMSNorm(torch.autograd.Function):
+    """h = x + residual ; y = rmsnorm(h) * w  -> (y, h), residual add fused into the norm."""
+
+    @staticmethod
+    def forward(ctx, x, residual, w, eps):
+        C = _native.kernels()
+        y, h, rstd = C.rmsnorm_fwd(x.contiguous(), residual.contiguous(), w.contiguous(), eps)
+        ctx.save_for_backward(h, w, rstd)
+        return y, h
+
+    @staticmethod
+    def backward(ctx, dy, dh):
+        h, w, rstd = ctx.saved_tensors
+        dy = torch.zeros_like(h) if dy is None else dy.contiguous()
+        dres = None if dh is None else dh.contiguous()
+        dx, dw = _native.kernels().rmsnorm_bwd(dy, h, w, rstd, dres)
+        return dx, dx, dw.to(w.dtype), None
+
+
+def rms_norm(x, w, eps=1e-5):
+    if _gpu(x):
+        return _RMSNorm.apply(x, w, eps)
+    return _ref.rmsnorm(x, w, eps)[0]
+
+
+def add_rms_norm(x, residual, w, eps=1e-5):
+    """Returns (rmsnorm(x + residual) * w, x + residual)."""
+    if _gpu(x):
+        return _AddRMSNorm.apply(x, residual, w, eps)
+    return _ref.rmsnorm(x, w, eps, residual=residual)
+
+
+# ----------------------------------------------------------------------------- LayerNorm
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, w, b, eps):
+        C = _native.kernels()
+        y, h, mean, rstd = C.layernorm_fwd(x.contiguous(), None if residual is None else residual.contiguous(),
+                                           w.contiguous(), None if b is None else b.contiguous(), eps)
+        ctx.has_res = residual is not None
+        ctx.has_b = b is not None
+        ctx.save_for_backward(h, w, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        h, w, mean, rstd = ctx.saved_tensors
+        dx, dw, db = _native.kernels().layernorm_bwd(dy.contiguous(), h, w, mean, rstd, None)
+        return dx, (dx if ctx.has_res else None), dw.to(w.dtype), (db.to(w.dtype) if ctx.has_b else None), None
+
+
+def layer_norm(x, w, b=None, eps=1e-5, residual=None):
+    """LayerNorm(x [+ residual]) — the post-LN block of nn.TransformerEncoderLayer."""
+    if _gpu(x):
+        return _LayerNorm.apply(x, residual, w, b, eps)
+    return _ref.layernorm(x, w, b, eps, residual=residual)[0]
+
+
+# ----------------------------------------------------------------------------- activations
+class _SwiGLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        gu = gu.contiguous()
+        ctx.save_for_backward(gu)
+        return _native.kernels().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (gu,) = ctx.saved_tensors
+        return _native.kernels().swiglu_bwd(gu, dout.contiguous())
+
+
+def swiglu(gu):
+    """silu(gu[..., :F]) * gu[..., F:] for the fused [gate | up] projection output."""
+    if _gpu(gu):
+        return _SwiGLU.apply(gu)
+    return _ref.swiglu(gu)
+
+
+class _GELU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        ctx.save_for_backward(x)
+        return _native.kernels().gelu_fwd(x)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return _native.kernels().gelu_bwd(x, dy.contiguous())
+
+
+def gelu(x):
+    if _gpu(x) and x.numel() % (8 if x.dtype == torch.bfloat16 else 4) == 0:
+        return _GELU.apply(x)
+    return _ref.gelu(x)
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed, offset):
+        y, mask = _native.kernels().dropout_fwd(x.contiguous(), p, seed, offset)
+        ctx.p = p
+        ctx.save_for_backward(mask)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (mask,) = ctx.saved_tensors
+        return _native.kernels().dropout_bwd(dy.contiguous(), mask, ctx.p), None, None, None
+
+
+_dropout_counter = [0]
+
+
+def dropout(x, p, training=True, seed=None):
+    if not training or p == 0.0:
+        return x
+    if _gpu(x):
+        if seed is None:
+            seed = int(torch.cuda.default_generators[x.device.index or 0].initial_seed()) & 0xFFFFFF
+        off = _dropout_counter[0]
+        _dropout_counter[0] += x.numel()
+        return _Dropout.apply(x, p, seed, off)
+    return torch.nn.functional.dropout(x, p, training=True)
+
+
+# ----------------------------------------------------------------------------- attention
+class _FlashAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, causal, scale, seqlens_k):
+        C = _native.kernels()
+        o, lse = C.attn_fwd(q, k, v, None, scale, causal, seqlens_k)
+        ctx.save_for_backward(q, k, v, o, lse, seqlens_k)
+        ctx.causal, ctx.scale = causal, scale
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, seqlens_k = ctx.saved_tensors
+        dq, dk, dv = _native.kernels().attn_bwd(do.contiguous(), q, k, v, o, lse, None, None, None,
+                                                ctx.scale, ctx.causal, seqlens_k)
+        return dq, dk, dv, None, None, None
+
+
+def flash_attention(q, k, v, causal=True, scale=None, seqlens_k=None):
+    """q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] (any batch/seq/head strides) -> o [B,Sq,Hq,D]."""
+    scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if _gpu(q) and q.dtype == torch.bfloat16 and q.shape[-1] == 128:
+        return _FlashAttn.apply(q, k, v, causal, scale, seqlens_k)
+    if _gpu(q):
+        _warn_once(f"flash_attention: no gfx950 kernel for dtype={q.dtype} head_dim={q.shape[-1]}; "
+                   "using the fp32 math path")
+    return _ref.attention(q, k, v, causal=causal, scale=scale, seqlens_k=seqlens_k)
+
+
+_warned = set()
+
+
+def _warn_once(msg):
+    if msg not in _warned:
+        _warned.add(msg)
+        import warnings
+        warnings.warn(msg)
+
+
+class _RopeAttention(torch.autograd.Function):
+    """qkv [B*S, (Hq + 2 Hkv) * D] -> o [B*S, Hq * D]: RoPE + causal flash attention fused.
+
+    Backward writes dV straight into the V columns of dqkv (strided) and the un-rotated dQ/dK into
+    its Q/K columns, so the fused-QKV gradient is produced with no split/cat copies.
+    """
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, B, S, hq, hkv, D, causal, scale):
+        C = _native.kernels()
+        qkv = qkv.contiguous()
+        q, k = C.rope_fwd(qkv, cos, sin, None, hq, hkv, D, S)
+        q4 = q.view(B, S, hq, D)
+        k4 = k.view(B, S, hkv, D)
+        v4 = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
+        o = torch.empty(B, S, hq, D, device=qkv.device, dtype=qkv.dtype)
+        _, lse = C.attn_fwd(q4, k4, v4, o, scale, causal, None)
+        ctx.save_for_backward(qkv, q, k, o, lse, cos, sin)
+        ctx.dims = (B, S, hq, hkv, D, causal, scale)
+        return o.view(B * S, hq * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, q, k, o, lse, cos, sin = ctx.saved_tensors
+        B, S, hq, hkv, D, causal, scale = ctx.dims
+        C = _native.kernels()
+        dqkv = torch.empty_like(qkv)
+        q4 = q.view(B, S, hq, D)
+        k4 = k.view(B, S, hkv, D)
+        v4 = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
+        dv4 = dqkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
+        dq, dk, _ = C.attn_bwd(do.contiguous().view(B, S, hq, D), q4, k4, v4, o, lse, None, None, dv4,
+                               scale, causal, None)
+        C.rope_bwd(dq, dk, dqkv, cos, sin, None, hq, hkv, D, S)
+        return dqkv, None, None, None, None, None, None, None, None, None
+
+
+def rope_attention(qkv, cos, sin, B, S, hq, hkv, D, causal=True, scale=None):
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if _gpu(qkv) and qkv.dtype == torch.bfloat16 and D == 128:
+        return _RopeAttention.apply(qkv, cos, sin, B, S, hq, hkv, D, causal, scale)
+    x = qkv.view(B * S, hq + 2 * hkv, D)
+    q = _ref.apply_rope(x[:, :hq], cos, sin)
+    k = _ref.apply_rope(x[:, hq:hq + hkv], cos, sin)
+    v = x[:, hq + hkv:]
+    o = flash_attention(q.view(B, S, hq, D), k.view(B, S, hkv, D), v.reshape(B, S, hkv, D), causal, scale)
+    return o.reshape(B * S, hq * D)
+
+
+# ----------------------------------------------------------------------------- cross entropy
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index, inplace):
+        C = _native.kernels()
+        loss_rows, lse = C.ce_fwd(logits, labels, ignore_index)
+        nvalid = (labels != ignore_index).sum().clamp_min(1).float()
+        ctx.save_for_backward(logits, labels, lse, nvalid)
+        ctx.ignore_index, ctx.inplace = ignore_index, inplace
+        return loss_rows.sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, labels, lse, nvalid = ctx.saved_tensors
+        gscale = (g.float() / nvalid).expand(logits.shape[0]).contiguous()
+        d = _native.kernels().ce_bwd(logits, labels, lse, gscale, ctx.ignore_index, ctx.inplace)
+        return d, None, None, None
+
+
+def cross_entropy(logits, labels, ignore_index=-100, inplace_backward=False):
+    """Mean CE over non-ignored rows. logits [N, V] (row-major), labels int64 [N]."""
+    if _gpu(logits):
+        return _CrossEntropy.apply(logits, labels.contiguous(), ignore_index, inplace_backward)
+    return _ref.cross_entropy(logits, labels, ignore_index)
+
+
+class _LMHeadCE(torch.autograd.Function):
+    """loss = CE(hidden @ W^T [+ b], labels): the logits never escape, so the backward writes
+    dlogits over the logits buffer in place (saves a [tokens, V] allocation per step)."""
+
+    @staticmethod
+    def forward(ctx, hidden, weight, bias, labels, ignore_index):
+        C = _native.kernels()
+        logits = torch.nn.functional.linear(hidden, weight, bias)
+        loss_rows, lse = C.ce_fwd(logits, labels, ignore_index)
+        nvalid = (labels != ignore_index).sum().clamp_min(1).float()
+        ctx.save_for_backward(hidden, weight, logits, labels, lse, nvalid)
+        ctx.ignore_index = ignore_index
+        ctx.has_bias = bias is not None
+        return loss_rows.sum() / nvalid
+
+    @staticmethod
+    def backward(ctx, g):
+        hidden, weight, logits, labels, lse, nvalid = ctx.saved_tensors
+        gscale = (g.float() / nvalid).expand(logits.shape[0]).contiguous()
+        dlogits = _native.kernels().ce_bwd(logits, labels, lse, gscale, ctx.ignore_index, True)
+        dh = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dh = dlogits @ weight
+        if ctx.needs_input_grad[1]:
+            dw = dlogits.t() @ hidden
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dlogits.sum(0)
+        return dh, dw, db, None, None
+
+
+def lm_head_cross_entropy(hidden, weight, labels, bias=None, ignore_index=-100):
+    if _gpu(hidden):
+        return _LMHeadCE.apply(hidden, weight, bias, labels.contiguous(), ignore_index)
+    logits = torch.nn.functional.linear(hidden, weight, bias)
+    return _ref.cross_entropy(logits, labels, ignore_index)
+
+
+# ----------------------------------------------------------------------------- NF4
+def nf4_quantize(w, blocksize=64):
+    if _gpu(w):
+        return tuple(_native.kernels().nf4_quantize(w.contiguous().view(-1), blocksize))
+    return _ref.nf4_quantize(w, blocksize)
+
+
+def nf4_dequantize(packed, absmax, n, blocksize=64, dtype=torch.bfloat16, out=None):
+    if _gpu(packed):
+        return _native.kernels().nf4_dequantize(packed, absmax, n, blocksize, dtype, out)
+    return _ref.nf4_dequantize(packed, absmax, n, blocksize, dtype)

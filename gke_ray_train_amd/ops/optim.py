@@ -1,0 +1,154 @@
+"""Fused AdamW + device-side gradient clipping on the gfx950 kernels.
+
+``FusedAdamW`` is a drop-in ``torch.optim.Optimizer`` (state_dict layout compatible with
+``torch.optim.AdamW``: ``exp_avg`` / ``exp_avg_sq`` / ``step`` per parameter). On GPU every
+parameter tensor is updated by ONE HIP kernel pass; the data-parallel engines hand it a single
+flat parameter per dtype/decay group, so a whole 7B model updates in one launch.
+
+Gradient clipping never synchronises with the host: ``clip_grad_norm_`` leaves the global
+norm and the clip coefficient in a device buffer that the AdamW kernel reads directly
+(reference ``clip_grad_norm_(…, 1.0)``/``max_grad_norm``: ray-jobs/pytorch_llm_ray.py:277,
+ray-jobs/fine_tune_config.json:19).
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, Optional
+
+import torch
+
+from .. import _native
+from . import _ref
+
+
+class GradClipState:
+    """Device scalars produced by clip_grad_norm_: buf[0] = global norm, buf[1] = grad scale."""
+
+    def __init__(self, device):
+        self.buf = torch.ones(2, device=device, dtype=torch.float32)
+
+    @property
+    def norm(self) -> torch.Tensor:
+        return self.buf[0]
+
+
+_ws_cache: dict = {}
+
+
+def clip_grad_norm_(params_or_grads: Iterable, max_norm: float, prescale: float = 1.0,
+                    state: Optional[GradClipState] = None, apply: bool = False) -> GradClipState:
+    """Global L2 norm of all grads (times ``prescale``) and clip coefficient, on device.
+
+    With ``apply=False`` (the fused path) grads are left untouched and the coefficient is
+    consumed by ``FusedAdamW.step(grad_scale=state)``; ``apply=True`` scales grads in place
+    (torch semantics) for optimizers that are not fused.
+    """
+    grads = []
+    for t in params_or_grads:
+        g = t.grad if isinstance(t, torch.nn.Parameter) or (isinstance(t, torch.Tensor) and t.grad is not None) else t
+        if g is not None:
+            grads.append(g)
+    if not grads:
+        dev = torch.device("cpu")
+        st = state or GradClipState(dev)
+        st.buf.fill_(1.0)
+        st.buf[0] = 0.0
+        return st
+    dev = grads[0].device
+    st = state or GradClipState(dev)
+    if dev.type == "cuda":
+        C = _native.kernels()
+        nb = C.sumsq_blocks()
+        key = (dev, len(grads))
+        ws = _ws_cache.get(key)
+        if ws is None:
+            ws = torch.empty(len(grads) * nb, device=dev, dtype=torch.float32)
+            _ws_cache[key] = ws
+        for i, g in enumerate(grads):
+            C.sumsq(g.contiguous() if not g.is_contiguous() else g, ws, i)
+        C.clip_finalize(ws, len(grads) * nb, float(max_norm), float(prescale), st.buf)
+        if apply:
+            for g in grads:
+                C.scale_(g, 1.0, st.buf[1:2])
+    else:
+        total = torch.stack([g.float().pow(2).sum() for g in grads]).sum().sqrt() * prescale
+        coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) if max_norm > 0 else torch.ones(())
+        st.buf[0] = total
+        st.buf[1] = coef * prescale
+        if apply:
+            for g in grads:
+                g.mul_(st.buf[1].to(g.dtype))
+    return st
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    """AdamW with fp32 moments; bf16 or fp32 params (optionally with an fp32 master copy).
+
+    ``name`` aliases accepted by the trainer: ``adamw_torch``, ``adamw_32bit``,
+    ``paged_adamw_32bit`` (the reference's OPTIM, ray-jobs/fine_tune_config.json:17 — paging is
+    unnecessary with 288 GB of HBM, the states simply stay resident).
+    """
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
+                 master_weights: bool = False):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        self.master_weights = master_weights
+        self._hyper = {}
+
+    def _hyper_buf(self, dev, key):
+        hb = self._hyper.get((dev, key))
+        if hb is None:
+            hb = torch.empty(8, dtype=torch.float32, device=dev)
+            self._hyper[(dev, key)] = hb
+        return hb
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: Optional[GradClipState] = None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            lr = group["lr"]
+            b1, b2 = group["betas"]
+            eps, wd = group["eps"], group["weight_decay"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
+                    if self.master_weights and p.dtype != torch.float32:
+                        st["master"] = p.detach().float().contiguous()
+                st["step"] += 1
+                step = float(st["step"].item()) if st["step"].device.type == "cpu" else float(st["step"])
+                bc1 = 1.0 - b1 ** step
+                bc2 = 1.0 - b2 ** step
+                master = st.get("master")
+                if p.is_cuda:
+                    hb = self._hyper_buf(p.device, (gi,))
+                    hb.copy_(torch.tensor([lr, b1, b2, eps, wd, bc1, bc2, 1.0], dtype=torch.float32),
+                             non_blocking=True)
+                    g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                    _native.kernels().adamw(p.data, g, st["exp_avg"], st["exp_avg_sq"], master, hb,
+                                            None if grad_scale is None else grad_scale.buf)
+                else:
+                    gs = 1.0 if grad_scale is None else float(grad_scale.buf[1])
+                    _ref.adamw_(p.data, p.grad, st["exp_avg"], st["exp_avg_sq"], step, lr, b1, b2, eps, wd,
+                                grad_scale=gs, master=master)
+        return loss
+
+
+def make_optimizer(name: str, params, lr: float, weight_decay: float, betas=(0.9, 0.999), eps=1e-8,
+                   master_weights=False):
+    name = (name or "adamw_torch").lower()
+    if name in ("adamw", "adamw_torch", "adamw_hf", "adamw_32bit", "paged_adamw_32bit", "adamw_torch_fused",
+                "fused_adamw", "paged_adamw_8bit", "adamw_8bit"):
+        return FusedAdamW(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                          master_weights=master_weights)
+    if name == "sgd":
+        return torch.optim.SGD(params, lr=lr, weight_decay=weight_decay)
+    raise ValueError(f"unknown optimizer {name!r}")

@@ -1,0 +1,290 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _C():
+    from gke_ray_train_amd import _native
+    return _native.kernels()
+
+
+def _close(a, b, atol, rtol, what=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol)
+    assert not torch.isnan(a).any(), f"{what}: NaN in kernel output"
+    assert bad.float().mean().item() < 1e-3, f"{what}: max err {err.max().item():.4g} (mean {err.mean().item():.3g})"
+
+
+def test_native_loaded():
+    C = _C()
+    assert hasattr(C, "attn_fwd")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("d", [256, 4096, 2048 + 512])
+def test_rmsnorm(dtype, d):
+    from gke_ray_train_amd import ops
+    torch.manual_seed(0)
+    x = torch.randn(37, d, device=DEV, dtype=dtype, requires_grad=True)
+    r = torch.randn(37, d, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(d, device=DEV, dtype=dtype)).requires_grad_()
+    y, h = ops.add_rms_norm(x, r, w, 1e-5)
+    gy = torch.randn_like(y)
+    gh = torch.randn_like(h)
+    (y.float() * gy.float()).sum().add((h.float() * gh.float()).sum()).backward()
+    xr, rr, wr = (t.detach().float().requires_grad_() for t in (x, r, w))
+    hr = xr + rr
+    yr = hr * torch.rsqrt(hr.pow(2).mean(-1, keepdim=True) + 1e-5) * wr
+    (yr * gy.float()).sum().add((hr * gh.float()).sum()).backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    _close(y, yr, tol, tol, "rms y")
+    _close(h, hr, tol, tol, "rms h")
+    _close(x.grad, xr.grad, tol * 5, tol, "rms dx")
+    _close(w.grad, wr.grad, tol * 20, tol * 2, "rms dw")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_layernorm(dtype):
+    from gke_ray_train_amd import ops
+    torch.manual_seed(1)
+    d = 2048
+    x = torch.randn(64, d, device=DEV, dtype=dtype, requires_grad=True)
+    r = torch.randn(64, d, device=DEV, dtype=dtype, requires_grad=True)
+    w = (1 + 0.1 * torch.randn(d, device=DEV, dtype=dtype)).requires_grad_()
+    b = (0.1 * torch.randn(d, device=DEV, dtype=dtype)).requires_grad_()
+    y = ops.layer_norm(x, w, b, 1e-5, residual=r)
+    gy = torch.randn_like(y)
+    (y.float() * gy.float()).sum().backward()
+    xr, rr, wr, br = (t.detach().float().requires_grad_() for t in (x, r, w, b))
+    yr = torch.nn.functional.layer_norm(xr + rr, (d,), wr, br, 1e-5)
+    (yr * gy.float()).sum().backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    _close(y, yr, tol, tol, "ln y")
+    _close(x.grad, xr.grad, tol * 5, tol, "ln dx")
+    _close(r.grad, rr.grad, tol * 5, tol, "ln dres")
+    _close(w.grad, wr.grad, tol * 30, tol * 2, "ln dw")
+    _close(b.grad, br.grad, tol * 30, tol * 2, "ln db")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_swiglu_gelu(dtype):
+    from gke_ray_train_amd import ops
+    torch.manual_seed(2)
+    gu = torch.randn(33, 2 * 688, device=DEV, dtype=dtype, requires_grad=True)
+    y = ops.swiglu(gu)
+    g = torch.randn_like(y)
+    (y.float() * g.float()).sum().backward()
+    gr = gu.detach().float().requires_grad_()
+    a, u = gr.chunk(2, -1)
+    yr = torch.nn.functional.silu(a) * u
+    (yr * g.float()).sum().backward()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    _close(y, yr, tol, tol, "swiglu")
+    _close(gu.grad, gr.grad, tol, tol, "swiglu bwd")
+    x = torch.randn(1024, 64, device=DEV, dtype=dtype, requires_grad=True)
+    y = ops.gelu(x)
+    (y.float() * x.detach().float()).sum().backward()
+    xr = x.detach().float().requires_grad_()
+    yr = torch.nn.functional.gelu(xr)
+    (yr * xr.detach()).sum().backward()
+    _close(y, yr, tol, tol, "gelu")
+    _close(x.grad, xr.grad, tol, tol, "gelu bwd")
+
+
+def test_dropout():
+    from gke_ray_train_amd import ops
+    x = torch.ones(1 << 16, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.dropout(x, 0.1, True, seed=7)
+    keep = (y != 0).float().mean().item()
+    assert abs(keep - 0.9) < 0.01
+    assert torch.allclose(y[y != 0].float(), torch.full_like(y[y != 0].float(), 1 / 0.9), atol=1e-2)
+    y.float().sum().backward()
+    assert torch.equal((x.grad != 0), (y != 0))
+
+
+def test_rope():
+    from gke_ray_train_amd.ops import _ref
+    C = _C()
+    torch.manual_seed(3)
+    B, S, hq, hkv, D = 2, 40, 4, 2, 128
+    T = B * S
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, device=DEV, dtype=torch.bfloat16)
+    cos, sin = _ref.rope_tables(S, D, 10000.0, device=DEV)
+    q, k = C.rope_fwd(qkv, cos, sin, None, hq, hkv, D, S)
+    x = qkv.view(T, hq + 2 * hkv, D)
+    qr = _ref.apply_rope(x[:, :hq].float(), cos, sin)
+    kr = _ref.apply_rope(x[:, hq:hq + hkv].float(), cos, sin)
+    _close(q, qr, 2e-2, 2e-2, "rope q")
+    _close(k, kr, 2e-2, 2e-2, "rope k")
+    dq = torch.randn_like(q)
+    dk = torch.randn_like(k)
+    dqkv = torch.zeros_like(qkv)
+    C.rope_bwd(dq, dk, dqkv, cos, sin, None, hq, hkv, D, S)
+    # inverse rotation == rotation by -theta
+    qi = _ref.apply_rope(dq.float(), cos, -sin)
+    _close(dqkv.view(T, -1, D)[:, :hq], qi, 2e-2, 2e-2, "rope bwd")
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("V", [32000, 283])
+def test_cross_entropy(dtype, V):
+    from gke_ray_train_amd import ops
+    torch.manual_seed(4)
+    N = 67
+    logits = (3 * torch.randn(N, V, device=DEV, dtype=torch.float32)).to(dtype).requires_grad_()
+    labels = torch.randint(0, V, (N,), device=DEV)
+    labels[::7] = -100
+    loss = ops.cross_entropy(logits, labels)
+    loss.backward()
+    lr = logits.detach().float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(lr, labels, ignore_index=-100)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1.0, abs(ref.item()))
+    _close(logits.grad, lr.grad, 1e-4 if dtype == torch.float32 else 3e-3, 2e-2, "ce grad")
+
+
+def test_lm_head_ce():
+    from gke_ray_train_amd import ops
+    torch.manual_seed(5)
+    N, d, V = 64, 256, 1000
+    h = torch.randn(N, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    W = (0.05 * torch.randn(V, d, device=DEV, dtype=torch.bfloat16)).requires_grad_()
+    lab = torch.randint(0, V, (N,), device=DEV)
+    loss = ops.lm_head_cross_entropy(h, W, lab)
+    loss.backward()
+    hr, Wr = h.detach().float().requires_grad_(), W.detach().float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(hr @ Wr.t(), lab)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 2e-2
+    _close(h.grad, hr.grad, 2e-3, 5e-2, "lmce dh")
+    _close(W.grad, Wr.grad, 2e-3, 5e-2, "lmce dW")
+
+
+@pytest.mark.parametrize("pdt", [torch.bfloat16, torch.float32])
+def test_adamw_and_clip(pdt):
+    from gke_ray_train_amd.ops import FusedAdamW, clip_grad_norm_, _ref
+    torch.manual_seed(6)
+    n = 10007
+    p = torch.randn(n, device=DEV, dtype=pdt)
+    g = torch.randn(n, device=DEV, dtype=pdt) * 3
+    P = torch.nn.Parameter(p.clone())
+    P.grad = g.clone()
+    opt = FusedAdamW([P], lr=1e-2, weight_decay=0.01)
+    st = clip_grad_norm_([P], 1.0)
+    norm = g.float().norm()
+    assert abs(st.norm.item() - norm.item()) < 1e-3 * norm.item()
+    opt.step(grad_scale=st)
+    pr = p.float().clone()
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    _ref.adamw_(pr, g.float(), m, v, 1, 1e-2, 0.9, 0.999, 1e-8, 0.01, grad_scale=min(1.0, 1.0 / (norm.item() + 1e-6)))
+    _close(P.data, pr, 1e-2 if pdt == torch.bfloat16 else 1e-6, 1e-2 if pdt == torch.bfloat16 else 1e-5, "adamw")
+    _close(opt.state[P]["exp_avg"], m, 1e-6, 1e-4, "adamw m")
+
+
+def test_nf4_roundtrip():
+    from gke_ray_train_amd import ops
+    from gke_ray_train_amd.ops import _ref
+    torch.manual_seed(7)
+    w = torch.randn(4096 * 64, device=DEV, dtype=torch.bfloat16)
+    q, a = ops.nf4_quantize(w, 64)
+    qr, ar = _ref.nf4_quantize(w.cpu(), 64)
+    assert torch.allclose(a.cpu(), ar, rtol=1e-6)
+    assert (q.cpu() != qr).float().mean().item() < 1e-3
+    wd = ops.nf4_dequantize(q, a, w.numel(), 64, torch.bfloat16)
+    wr = _ref.nf4_dequantize(qr, ar, w.numel(), 64, torch.bfloat16)
+    _close(wd.cpu(), wr, 1e-2, 1e-2, "nf4 dequant")
+    rel = (wd.float() - w.float()).norm() / w.float().norm()
+    assert rel < 0.15
+
+
+def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False):
+    from gke_ray_train_amd import ops
+    from gke_ray_train_amd.ops import _ref
+    torch.manual_seed(8)
+    D = 128
+    if strided:
+        qkv = torch.randn(B, Sq, Hq + 2 * Hkv, D, device=DEV, dtype=torch.bfloat16)
+        q = qkv[:, :, :Hq].detach().requires_grad_()
+        base = torch.randn(B, Sk, 2 * Hkv, D, device=DEV, dtype=torch.bfloat16)
+        k = base[:, :, :Hkv]
+        v = base[:, :, Hkv:]
+        k = k.detach().requires_grad_()
+        v = v.detach().requires_grad_()
+    else:
+        q = torch.randn(B, Sq, Hq, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    sl = None if seqlens is None else torch.tensor(seqlens, device=DEV, dtype=torch.int32)
+    o = ops.flash_attention(q, k, v, causal=causal, seqlens_k=sl)
+    do = torch.randn_like(o)
+    (o.float() * do.float()).sum().backward()
+    qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
+    orf = _ref.attention(qr, kr, vr, causal=causal, seqlens_k=sl)
+    (orf * do.float()).sum().backward()
+    valid = torch.ones(B, Sq, dtype=torch.bool, device=DEV)
+    _close(o, orf, 2e-2, 2e-2, "attn o")
+    _close(q.grad, qr.grad, 3e-2, 3e-2, "attn dq")
+    _close(k.grad, kr.grad, 3e-2, 3e-2, "attn dk")
+    _close(v.grad, vr.grad, 3e-2, 3e-2, "attn dv")
+
+
+@pytest.mark.parametrize("case", [
+    dict(B=2, Sq=256, Sk=256, Hq=4, Hkv=4, causal=True),
+    dict(B=1, Sq=200, Sk=200, Hq=4, Hkv=2, causal=True),
+    dict(B=2, Sq=130, Sk=130, Hq=2, Hkv=2, causal=False),
+    dict(B=1, Sq=64, Sk=192, Hq=2, Hkv=1, causal=True),
+    dict(B=2, Sq=256, Sk=256, Hq=4, Hkv=2, causal=True, strided=True),
+    dict(B=2, Sq=160, Sk=160, Hq=2, Hkv=2, causal=False, seqlens=[160, 77]),
+])
+def test_flash_attention(case):
+    _attn_case(**case)
+
+
+def test_rope_attention_fused():
+    from gke_ray_train_amd import ops
+    from gke_ray_train_amd.ops import _ref
+    torch.manual_seed(9)
+    B, S, hq, hkv, D = 2, 192, 4, 2, 128
+    qkv = torch.randn(B * S, (hq + 2 * hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    cos, sin = _ref.rope_tables(S, D, 10000.0, device=DEV)
+    o = ops.rope_attention(qkv, cos, sin, B, S, hq, hkv, D)
+    g = torch.randn_like(o)
+    (o.float() * g.float()).sum().backward()
+    xr = qkv.detach().float().requires_grad_()
+    x = xr.view(B * S, hq + 2 * hkv, D)
+    q = _ref.apply_rope(x[:, :hq], cos, sin).view(B, S, hq, D)
+    k = _ref.apply_rope(x[:, hq:hq + hkv], cos, sin).view(B, S, hkv, D)
+    v = x[:, hq + hkv:].reshape(B, S, hkv, D)
+    orf = _ref.attention(q, k, v, causal=True).reshape(B * S, hq * D)
+    (orf * g.float()).sum().backward()
+    _close(o, orf, 2e-2, 2e-2, "rope-attn o")
+    _close(qkv.grad, xr.grad, 3e-2, 3e-2, "rope-attn dqkv")
+
+
+def test_llama_tiny_matches_reference_math():
+    """Whole-model parity: native kernels vs the CPU reference path on the same weights."""
+    from gke_ray_train_amd.models import build_llama
+    torch.manual_seed(10)
+    m = build_llama("llama-tiny-gqa", device=DEV, dtype=torch.bfloat16, seed=1)
+    ids = torch.randint(0, m.config.vocab_size, (2, 128), device=DEV)
+    loss = m(ids, labels=ids)["loss"]
+    loss.backward()
+    g_native = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    mc = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32, seed=None)
+    mc.load_state_dict({k: v.float().cpu() for k, v in m.state_dict().items()})
+    lc = mc(ids.cpu(), labels=ids.cpu())["loss"]
+    lc.backward()
+    assert abs(loss.item() - lc.item()) < 2e-2 * max(1.0, lc.item())
+    for n, p in mc.named_parameters():
+        a, b = g_native[n].cpu(), p.grad
+        rel = (a - b).norm() / (b.norm() + 1e-8)
+        assert rel < 0.08, f"{n}: rel grad err {rel:.3f}"
