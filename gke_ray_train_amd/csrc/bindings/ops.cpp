@@ -387,8 +387,7 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   bp.dq = dq.data_ptr(); bp.dq_bs = dq.stride(0); bp.dq_ss = dq.stride(1); bp.dq_hs = dq.stride(2);
   bp.dk = dk.data_ptr(); bp.dk_bs = dk.stride(0); bp.dk_ss = dk.stride(1); bp.dk_hs = dk.stride(2);
   bp.dv = dv.data_ptr(); bp.dv_bs = dv.stride(0); bp.dv_ss = dv.stride(1); bp.dv_hs = dv.stride(2);
-  bp.dq_acc = ws.data_ptr<float>();
-  bp.delta = ws.data_ptr<float>() + (int64_t)p.B * p.Hq * p.Sq * p.D;
+  bp.delta = ws.data_ptr<float>();
   grt::attn_bwd(bp, cur_stream(q));
   return {dq, dk, dv};
 }

@@ -96,7 +96,6 @@ struct AttnBwdParams {
   void* dq; int64_t dq_bs, dq_ss, dq_hs;
   void* dk; int64_t dk_bs, dk_ss, dk_hs;
   void* dv; int64_t dv_bs, dv_ss, dv_hs;
-  float* dq_acc;   // fp32 workspace [B, Hq, Sq, D]
   float* delta;    // fp32 workspace [B, Hq, Sq]
 };
 void attn_bwd(const AttnBwdParams& p, hipStream_t s);

@@ -235,48 +235,47 @@ __global__ __launch_bounds__(FNT, 2) void attn_fwd_kernel(const AttnParams p) {
 // ---------------------------------------------------------------------------------------------
 constexpr int BBN = 128, BBM = 32, BNT = 256;
 
-// delta[b,h,q] = sum_d dO*O   (fp32), one wave per (b, h, q) row
+// delta[b,h,q] = sum_d dO*O (fp32): 16 lanes x 8 elements per row, 4 rows per wave, 16 per block
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int l16 = threadIdx.x & 15;
+  const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
   const int64_t nrows = (int64_t)p.f.B * p.f.Hq * p.f.Sq;
-  if (row >= nrows) return;
-  const int q = (int)(row % p.f.Sq);
-  const int64_t bh = row / p.f.Sq;
-  const int hq = (int)(bh % p.f.Hq), b = (int)(bh / p.f.Hq);
-  const bf16* O = (const bf16*)p.f.o + (int64_t)b * p.f.o_bs + (int64_t)hq * p.f.o_hs + (int64_t)q * p.f.o_ss;
-  const bf16* dO = (const bf16*)p.dout + (int64_t)b * p.do_bs + (int64_t)hq * p.do_hs + (int64_t)q * p.do_ss;
   float acc = 0.f;
-  if (lane < D / 8) {
+  if (row < nrows) {
+    const int q = (int)(row % p.f.Sq);
+    const int64_t bh = row / p.f.Sq;
+    const int hq = (int)(bh % p.f.Hq), b = (int)(bh / p.f.Hq);
+    const bf16* O = (const bf16*)p.f.o + (int64_t)b * p.f.o_bs + (int64_t)hq * p.f.o_hs + (int64_t)q * p.f.o_ss;
+    const bf16* dO = (const bf16*)p.dout + (int64_t)b * p.do_bs + (int64_t)hq * p.do_hs + (int64_t)q * p.do_ss;
     float a[8], g[8];
-    load16(O + lane * 8, a);
-    load16(dO + lane * 8, g);
+    load16(O + l16 * 8, a);
+    load16(dO + l16 * 8, g);
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc += a[k] * g[k];
   }
-  acc = wave_sum(acc);
-  if (lane == 0) p.delta[row] = acc;
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (row < nrows && l16 == 0) p.delta[row] = acc;
 }
 
-__global__ __launch_bounds__(BNT, 1) void attn_bwd_kernel(const AttnBwdParams P) {
+// dK / dV kernel: one workgroup = 128 keys of one (batch, kv head), 32 keys per wave with the key on
+// the MFMA lane; K and V fragments stay in VGPRs for the whole sweep over the group's query heads
+// x 32-row query tiles (Q / dO tiles double-buffered in LDS, one barrier per tile). No atomics:
+// dK and dV are complete in registers at the end.
+__global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdParams P) {
   const AttnParams& p = P.f;
-  // LDS: K img [128][D], V img [128][D], Q img [2][32][D], dO img [2][32][D], dS^T [128][32],
-  // lse/delta [2][32]
-  constexpr int KB = BBN * D * 2, QB = BBM * D * 2, SB = BBN * BBM * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * KB + 4 * QB + SB + 2 * 2 * BBM * 4];
-  char* Kl = smem;
-  char* Vl = smem + KB;
-  auto Ql = [&](int buf) -> char* { return smem + 2 * KB + buf * QB; };
-  auto dOl = [&](int buf) -> char* { return smem + 2 * KB + (2 + buf) * QB; };
-  char* dSl = smem + 2 * KB + 4 * QB;
-  float* lsel = (float*)(smem + 2 * KB + 4 * QB + SB);  // [2][32]
-  float* dell = lsel + 2 * BBM;                          // [2][32]
+  constexpr int QB = BBM * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[4 * QB + 2 * 2 * BBM * 4];
+  auto Ql = [&](int buf) -> char* { return smem + buf * QB; };
+  auto dOl = [&](int buf) -> char* { return smem + (2 + buf) * QB; };
+  float* lsel = (float*)(smem + 4 * QB);  // [2][32]
+  float* dell = lsel + 2 * BBM;           // [2][32]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int g = lane >> 4, l16 = lane & 15;
   const int nkb = (p.Sk + BBN - 1) / BBN;
-  const int kblk = blockIdx.x % nkb;
-  const int bhk = blockIdx.x / nkb;
+  const int kblk = nkb - 1 - (int)(blockIdx.x / (p.B * p.Hkv));  // causal: lightest key blocks last
+  const int bhk = blockIdx.x % (p.B * p.Hkv);
   const int b = bhk / p.Hkv, hkv = bhk % p.Hkv;
   const int grp = p.Hq / p.Hkv;
   const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
@@ -286,32 +285,30 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_kernel(const AttnBwdParams P)
   const int mykey = kw0 + l32;
   const float c = p.scale * kLog2e;
 
+  // K / V fragments (B operands of S = Q K^T and dP = dO V^T): lane holds row `mykey`
   const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs;
   const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs;
-
-  // K, V tiles of this workgroup -> LDS (8 chunks per thread each)
+  bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
-  for (int r = 0; r < (BBN * kChunks) / BNT; ++r) {
-    const int i = tid + BNT * r, row = i / kChunks, ch = i % kChunks, key = k0 + row;
-    bf16x8 kv = bf16x8{}, vv = bf16x8{};
-    if (key < sk) {
-      kv = *reinterpret_cast<const bf16x8*>(K + (int64_t)key * p.k_ss + ch * 8);
-      vv = *reinterpret_cast<const bf16x8*>(Vg + (int64_t)key * p.v_ss + ch * 8);
+  for (int ks = 0; ks < D / 16; ++ks) {
+    if (mykey < sk) {
+      kf[ks] = *reinterpret_cast<const bf16x8*>(K + (int64_t)mykey * p.k_ss + ks * 16 + 8 * h);
+      vf[ks] = *reinterpret_cast<const bf16x8*>(Vg + (int64_t)mykey * p.v_ss + ks * 16 + 8 * h);
+    } else {
+      kf[ks] = bf16x8{};
+      vf[ks] = bf16x8{};
     }
-    *reinterpret_cast<bf16x8*>(Kl + img_off(row, ch)) = kv;
-    *reinterpret_cast<bf16x8*>(Vl + img_off(row, ch)) = vv;
   }
 
   f32x16 dk[4], dv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
 
-  // first query row that can see this key block
   int qstart = 0;
   if (p.causal) qstart = max(0, k0 - off);
   qstart = (qstart / BBM) * BBM;
   const int nqt = qstart < p.Sq ? (p.Sq - qstart + BBM - 1) / BBM : 0;
-  const int total = nqt * grp;  // (head, q-tile) iterations
+  const int total = (k0 < sk) ? nqt * grp : 0;
 
   bf16x8 qreg[2], oreg[2];
   float lse_r = 0.f, del_r = 0.f;
@@ -353,84 +350,50 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_kernel(const AttnBwdParams P)
 
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
-    const int hq = hkv * grp + it / nqt;
     const int qt = qstart + (it % nqt) * BBM;
     if (it + 1 < total) load_q(it + 1);
-
-    // ---- S = Q K^T and dP = dO V^T (key on lane, q on registers)
-    f32x16 s = f32x16{}, dp = f32x16{};
+    const bool skip = p.causal && (kw0 > qt + BBM - 1 + off);   // all 32 keys after every q row
+    if (!skip) {
+      f32x16 s = f32x16{}, dp = f32x16{};
 #pragma unroll
-    for (int ks = 0; ks < D / 16; ++ks) {
-      const bf16x8 kb = lds_row_read(Kl, w * 32 + l32, 2 * ks + h);
-      const bf16x8 qa = lds_row_read(Ql(cur), l32, 2 * ks + h);
-      s = mfma32(qa, kb, s);
-      const bf16x8 vb = lds_row_read(Vl, w * 32 + l32, 2 * ks + h);
-      const bf16x8 oa = lds_row_read(dOl(cur), l32, 2 * ks + h);
-      dp = mfma32(oa, vb, dp);
-    }
-    // ---- P, dS
-    const bool need_mask = (k0 + BBN > sk) || (p.causal && kw0 + 31 > qt + off) || (qt + BBM > p.Sq);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int qi = acc_row(r, h);
-      const int q = qt + qi;
-      float pv = fast_exp2(s[r] * c - lsel[cur * BBM + qi]);
-      if (need_mask && (mykey >= sk || q >= p.Sq || (p.causal && mykey > q + off))) pv = 0.f;
-      s[r] = pv;
-      dp[r] = pv * (dp[r] - dell[cur * BBM + qi]);
-    }
-    // ---- dV^T += dO^T P ; dK^T += Q^T dS   (A operands via transposed LDS reads)
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const bf16x8 pb = pack8(s, 8 * st);
-      const bf16x8 sb = pack8(dp, 8 * st);
-      const int kk = 16 * st + 4 * h;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) {
-        const int c0 = db * 32 + (g & 1) * 16;
-        const bf16x8 oa = cat(lds_tr_read(dOl(cur), kk, c0, l16), lds_tr_read(dOl(cur), kk + 8, c0, l16));
-        dv[db] = mfma32(oa, pb, dv[db]);
-        const bf16x8 qa = cat(lds_tr_read(Ql(cur), kk, c0, l16), lds_tr_read(Ql(cur), kk + 8, c0, l16));
-        dk[db] = mfma32(qa, sb, dk[db]);
+      for (int ks = 0; ks < D / 16; ++ks) {
+        s = mfma32(lds_row_read(Ql(cur), l32, 2 * ks + h), kf[ks], s);
+        dp = mfma32(lds_row_read(dOl(cur), l32, 2 * ks + h), vf[ks], dp);
       }
-    }
-    // ---- dS^T -> LDS [key][q] (bf16), 4 x 8-byte writes per lane
+      const bool need_mask = (k0 + BBN > sk) || (p.causal && kw0 + 31 > qt + off) || (qt + BBM > p.Sq);
 #pragma unroll
-    for (int gg = 0; gg < 4; ++gg) {
-      bf16x4 v;
+      for (int gg = 0; gg < 4; ++gg) {
+        const f32x4 ls = *reinterpret_cast<const f32x4*>(lsel + cur * BBM + 8 * gg + 4 * h);
+        const f32x4 de = *reinterpret_cast<const f32x4*>(dell + cur * BBM + 8 * gg + 4 * h);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(dp[4 * gg + j]);
-      *reinterpret_cast<bf16x4*>(dSl + (w * 32 + l32) * (BBM * 2) + (8 * gg + 4 * h) * 2) = v;
-    }
-    __syncthreads();
-    // ---- dQ[q][d-block w] += dS[q][128 keys] K[128 keys][d]
-    {
-      f32x16 dq = f32x16{};
-#pragma unroll
-      for (int ks = 0; ks < BBN / 16; ++ks) {
-        // A: lane holds dS[q = l32][key = 16ks + 8h + j]  (tr read of the [key][q] image, 64-B rows)
-        const int kr = 16 * ks + 8 * h;
-        const int qq = (g & 1) * 16 + 4 * (l16 & 3);
-        const char* a0 = dSl + (kr + (l16 >> 2)) * (BBM * 2) + qq * 2;
-        const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)a0);
-        const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(a0 + 4 * BBM * 2));
-        // B: lane holds K[key = 16ks + 8h + j][d = 32w + l32]
-        const int c0 = w * 32 + (g & 1) * 16;
-        const bf16x8 kbv = cat(lds_tr_read(Kl, kr, c0, l16), lds_tr_read(Kl, kr + 4, c0, l16));
-        dq = mfma32(cat(lo, hi), kbv, dq);
+        for (int j = 0; j < 4; ++j) {
+          const int r = 4 * gg + j;
+          const int q = qt + 8 * gg + 4 * h + j;
+          float pv = fast_exp2(s[r] * c - ls[j]);
+          if (need_mask && (mykey >= sk || q >= p.Sq || (p.causal && mykey > q + off))) pv = 0.f;
+          s[r] = pv;
+          dp[r] = pv * (dp[r] - de[j]);
+        }
       }
-      float* dqa = P.dq_acc + (((int64_t)b * p.Hq + hq) * p.Sq) * D;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int q = qt + acc_row(r, h);
-        if (q < p.Sq) atomicAdd(dqa + (int64_t)q * D + w * 32 + l32, dq[r] * p.scale);
+      for (int st = 0; st < 2; ++st) {
+        const bf16x8 pb = pack8(s, 8 * st);
+        const bf16x8 sb = pack8(dp, 8 * st);
+        const int kk = 16 * st + 4 * h;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int c0 = db * 32 + (g & 1) * 16;
+          const bf16x8 oa = cat(lds_tr_read(dOl(cur), kk, c0, l16), lds_tr_read(dOl(cur), kk + 8, c0, l16));
+          dv[db] = mfma32(oa, pb, dv[db]);
+          const bf16x8 qa = cat(lds_tr_read(Ql(cur), kk, c0, l16), lds_tr_read(Ql(cur), kk + 8, c0, l16));
+          dk[db] = mfma32(qa, sb, dk[db]);
+        }
       }
     }
     if (it + 1 < total) store_q(cur ^ 1);
     __syncthreads();
   }
 
-  // ---- write dK, dV (lane = key, registers = d)
   if (mykey < p.Sk) {
     bf16* dK = (bf16*)P.dk + (int64_t)b * P.dk_bs + (int64_t)hkv * P.dk_hs + (int64_t)mykey * P.dk_ss;
     bf16* dV = (bf16*)P.dv + (int64_t)b * P.dv_bs + (int64_t)hkv * P.dv_hs + (int64_t)mykey * P.dv_ss;
@@ -450,20 +413,136 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_kernel(const AttnBwdParams P)
   }
 }
 
-// dq (bf16, strided) = dq_acc (fp32, [B, Hq, Sq, D])
-__global__ __launch_bounds__(256) void attn_dq_convert_kernel(const AttnBwdParams p) {
-  const int64_t n = (int64_t)p.f.B * p.f.Hq * p.f.Sq * (D / 8);
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int c = (int)(i % (D / 8));
-    const int64_t row = i / (D / 8);
-    const int q = (int)(row % p.f.Sq);
-    const int64_t bh = row / p.f.Sq;
-    const int hq = (int)(bh % p.f.Hq), b = (int)(bh / p.f.Hq);
-    float a[8];
-    load16(p.dq_acc + row * D + c * 8, a);
-    load16(p.dq_acc + row * D + c * 8 + 4, a + 4);
-    bf16* dst = (bf16*)p.dq + (int64_t)b * p.dq_bs + (int64_t)hq * p.dq_hs + (int64_t)q * p.dq_ss + c * 8;
-    store16(dst, a);
+// dQ kernel: the forward's structure (32 query rows per wave, query on the MFMA lane, K/V tiles of
+// 64 keys double-buffered in LDS). S^T = K Q^T and dP^T = V dO^T are recomputed, dS^T stays in
+// registers and feeds dQ^T += K^T dS^T as the B operand (K^T by transposed reads of the same K
+// tile). lse and delta are lane-local. No atomics, dQ written once in bf16.
+__global__ __launch_bounds__(FNT, 2) void attn_bwd_dq_kernel(const AttnBwdParams P) {
+  const AttnParams& p = P.f;
+  __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // K[2], V[2]
+  auto Kl = [&](int buf) -> char* { return smem + buf * kTileBytes; };
+  auto Vl = [&](int buf) -> char* { return smem + (2 + buf) * kTileBytes; };
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int nqb = (p.Sq + FBM - 1) / FBM;
+  const int BH = p.B * p.Hq;
+  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);
+  const int bh = blockIdx.x % BH;
+  const int b = bh / p.Hq, hq = bh % p.Hq;
+  const int hkv = hq / (p.Hq / p.Hkv);
+  const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
+  const int off = p.Sk - p.Sq;
+  const int q0 = qblk * FBM, qw0 = q0 + w * 32;
+  const int myq = qw0 + l32;
+  const bool qok = myq < p.Sq;
+
+  const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + (int64_t)hq * p.q_hs;
+  const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + (int64_t)hq * P.do_hs;
+  const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs;
+  const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs;
+
+  bf16x8 qf[D / 16], of[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks) {
+    if (qok) {
+      qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)myq * p.q_ss + ks * 16 + 8 * h);
+      of[ks] = *reinterpret_cast<const bf16x8*>(dO + (int64_t)myq * P.do_ss + ks * 16 + 8 * h);
+    } else {
+      qf[ks] = bf16x8{};
+      of[ks] = bf16x8{};
+    }
+  }
+  const int64_t ri = ((int64_t)b * p.Hq + hq) * p.Sq + (qok ? myq : 0);
+  const float lse2 = qok ? p.lse[ri] * kLog2e : INFINITY;
+  const float dlt = qok ? P.delta[ri] : 0.f;
+  const float c = p.scale * kLog2e;
+
+  int kend = sk;
+  if (p.causal) kend = min(kend, q0 + FBM + off);
+  const int nt = kend > 0 ? (kend + FBN - 1) / FBN : 0;
+
+  bf16x8 kreg[4], vreg[4];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = tid + FNT * r, row = i / kChunks, ch = i % kChunks, key = t * FBN + row;
+      if (key < sk) {
+        kreg[r] = *reinterpret_cast<const bf16x8*>(K + (int64_t)key * p.k_ss + ch * 8);
+        vreg[r] = *reinterpret_cast<const bf16x8*>(Vg + (int64_t)key * p.v_ss + ch * 8);
+      } else {
+        kreg[r] = bf16x8{};
+        vreg[r] = bf16x8{};
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = tid + FNT * r, row = i / kChunks, ch = i % kChunks;
+      *reinterpret_cast<bf16x8*>(Kl(buf) + img_off(row, ch)) = kreg[r];
+      *reinterpret_cast<bf16x8*>(Vl(buf) + img_off(row, ch)) = vreg[r];
+    }
+  };
+
+  f32x16 dq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) dq[i] = f32x16{};
+
+  if (nt > 0) { load_tile(0); store_tile(0); }
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int cur = t & 1;
+    const int kb = t * FBN;
+    if (t + 1 < nt) load_tile(t + 1);
+    const bool skip = p.causal && (kb > qw0 + 31 + off);
+    if (!skip) {
+      const bool need_mask = (kb + FBN > sk) || (p.causal && kb + FBN - 1 > qw0 + off);
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        f32x16 s = f32x16{}, dp = f32x16{};
+#pragma unroll
+        for (int ks = 0; ks < D / 16; ++ks) {
+          s = mfma32(lds_row_read(Kl(cur), n * 32 + l32, 2 * ks + h), qf[ks], s);
+          dp = mfma32(lds_row_read(Vl(cur), n * 32 + l32, 2 * ks + h), of[ks], dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float pv = fast_exp2(s[r] * c - lse2);
+          if (need_mask) {
+            const int key = kb + n * 32 + acc_row(r, h);
+            if (key >= sk || (p.causal && key > myq + off)) pv = 0.f;
+          }
+          s[r] = pv * (dp[r] - dlt);
+        }
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 sb = pack8(s, 8 * st);
+          const int kk = n * 32 + 16 * st + 4 * h;
+#pragma unroll
+          for (int db = 0; db < 4; ++db) {
+            const int c0 = db * 32 + (g & 1) * 16;
+            const bf16x8 a = cat(lds_tr_read(Kl(cur), kk, c0, l16), lds_tr_read(Kl(cur), kk + 8, c0, l16));
+            dq[db] = mfma32(a, sb, dq[db]);
+          }
+        }
+      }
+    }
+    if (t + 1 < nt) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  if (qok) {
+    bf16* dQ = (bf16*)P.dq + (int64_t)b * P.dq_bs + (int64_t)hq * P.dq_hs + (int64_t)myq * P.dq_ss;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int gg = 0; gg < 4; ++gg) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(dq[db][4 * gg + j] * p.scale);
+        *reinterpret_cast<bf16x4*>(dQ + db * 32 + 8 * gg + 4 * h) = v;
+      }
   }
 }
 
@@ -476,18 +555,17 @@ void attn_fwd(const AttnParams& p, hipStream_t s) {
 }
 
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
-  return (int64_t)B * Hq * Sq * Dh + (int64_t)B * Hq * Sq;
+  (void)Dh;
+  return (int64_t)B * Hq * Sq;  // delta
 }
 
 void attn_bwd(const AttnBwdParams& p, hipStream_t s) {
   const int64_t rows = (int64_t)p.f.B * p.f.Hq * p.f.Sq;
-  (void)hipMemsetAsync(p.dq_acc, 0, sizeof(float) * rows * D, s);
-  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
   const int nkb = (p.f.Sk + BBN - 1) / BBN;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(nkb * p.f.B * p.f.Hkv)), dim3(BNT), 0, s, p);
-  int64_t g = (rows * (D / 8) + 255) / 256;
-  if (g > 2048) g = 2048;
-  hipLaunchKernelGGL(attn_dq_convert_kernel, dim3((unsigned)g), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((unsigned)(nkb * p.f.B * p.f.Hkv)), dim3(BNT), 0, s, p);
+  const int nqb = (p.f.Sq + FBM - 1) / FBM;
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((unsigned)(nqb * p.f.B * p.f.Hq)), dim3(FNT), 0, s, p);
 }
 
 }  // namespace grt

@@ -20,7 +20,7 @@ namespace {
 
 constexpr int kNT = 256;          // 4 waves per workgroup
 constexpr int kRowsPerBlock = kNT / kWave;
-constexpr int kBwdMaxBlocks = 512;
+constexpr int kBwdMaxBlocks = 256;
 
 template <typename T, int MAXC, bool RMS>
 __global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
@@ -184,15 +184,33 @@ __global__ __launch_bounds__(kNT) void norm_bwd_kernel(const T* __restrict__ dy,
   }
 }
 
-// dw[j] = sum_b ws[b][0][j], db[j] = sum_b ws[b][1][j]
-__global__ __launch_bounds__(kNT) void colsum_kernel(const float* __restrict__ ws, int nb, int d,
+// dw[j] = sum_b ws[b][0][j], db[j] = sum_b ws[b][1][j] over ncols (= d for RMSNorm, 2d for
+// LayerNorm). One workgroup = 64 columns x 4 row phases; each thread keeps 4 independent
+// accumulators so the slab loads (256 contiguous bytes per wave) stay in flight.
+__global__ __launch_bounds__(kNT) void colsum_kernel(const float* __restrict__ ws, int nb, int d, int ncols,
                                                      float* __restrict__ dw, float* __restrict__ db) {
-  const int j = blockIdx.x * kNT + threadIdx.x;
-  if (j >= 2 * d) return;
-  float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += ws[(int64_t)b * 2 * d + j];
-  if (j < d) { if (dw) dw[j] = s; }
-  else { if (db) db[j - d] = s; }
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + c;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (j < ncols) {
+    const int64_t ld = 2 * (int64_t)d;
+    int b = rg;
+    for (; b + 12 < nb; b += 16) {
+      a0 += ws[(int64_t)b * ld + j];
+      a1 += ws[(int64_t)(b + 4) * ld + j];
+      a2 += ws[(int64_t)(b + 8) * ld + j];
+      a3 += ws[(int64_t)(b + 12) * ld + j];
+    }
+    for (; b < nb; b += 4) a0 += ws[(int64_t)b * ld + j];
+  }
+  red[rg][c] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (rg == 0 && j < ncols) {
+    const float s = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    if (j < d) { if (dw) dw[j] = s; }
+    else { if (db) db[j - d] = s; }
+  }
 }
 
 template <typename T, bool RMS>
@@ -234,8 +252,8 @@ void launch_bwd(const void* dy, const void* h, const void* w, const float* mean,
   else if (per_thr <= 4) GRT_NB(4);
   else GRT_NB(8);
 #undef GRT_NB
-  hipLaunchKernelGGL(colsum_kernel, dim3((2 * d + kNT - 1) / kNT), dim3(kNT), 0, s, ws, nb, d, dw,
-                     db);
+  const int ncols = RMS ? d : 2 * d;
+  hipLaunchKernelGGL(colsum_kernel, dim3((ncols + 63) / 64), dim3(kNT), 0, s, ws, nb, d, ncols, dw, db);
 }
 
 }  // namespace

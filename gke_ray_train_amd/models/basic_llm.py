@@ -23,6 +23,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
+from ..ops.linear import Linear
 
 
 @dataclass
@@ -72,7 +73,7 @@ class _MHA(nn.Module):
         self.embed_dim, self.num_heads, self.dropout = d, nhead, dropout
         self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d, device=device, dtype=dtype))
         self.in_proj_bias = nn.Parameter(torch.zeros(3 * d, device=device, dtype=dtype))
-        self.out_proj = nn.Linear(d, d, device=device, dtype=dtype)
+        self.out_proj = Linear(d, d, device=device, dtype=dtype)
         nn.init.xavier_uniform_(self.in_proj_weight)
         nn.init.zeros_(self.out_proj.bias)
 
@@ -97,8 +98,8 @@ class EncoderLayer(nn.Module):
     def __init__(self, d, nhead, dim_ff, dropout, device=None, dtype=None):
         super().__init__()
         self.self_attn = _MHA(d, nhead, dropout, device, dtype)
-        self.linear1 = nn.Linear(d, dim_ff, device=device, dtype=dtype)
-        self.linear2 = nn.Linear(dim_ff, d, device=device, dtype=dtype)
+        self.linear1 = Linear(d, dim_ff, device=device, dtype=dtype)
+        self.linear2 = Linear(dim_ff, d, device=device, dtype=dtype)
         self.norm1 = nn.LayerNorm(d, eps=1e-5, device=device, dtype=dtype)
         self.norm2 = nn.LayerNorm(d, eps=1e-5, device=device, dtype=dtype)
         self.p = dropout
@@ -128,7 +129,7 @@ class BasicLLM(nn.Module):
         self.positional_encoding = PositionalEncoding(embed_dim, max_seq_len)
         self.transformer_decoder = _Encoder(
             [EncoderLayer(embed_dim, num_heads, hidden_dim, dropout, device, dtype) for _ in range(num_layers)])
-        self.fc_out = nn.Linear(embed_dim, vocab_size, device=device, dtype=dtype)
+        self.fc_out = Linear(embed_dim, vocab_size, device=device, dtype=dtype)
         self.dropout_p = dropout
         self.max_seq_len = max_seq_len
         if device is not None:

@@ -28,6 +28,7 @@ import torch.nn as nn
 import torch.utils.checkpoint as ckpt
 
 from .. import ops
+from ..ops.linear import Linear
 from ..ops import _ref
 
 
@@ -120,7 +121,7 @@ def get_config(name: str, **overrides) -> LlamaConfig:
     return LlamaConfig(**d)
 
 
-class FusedLinear(nn.Linear):
+class FusedLinear(Linear):
     """nn.Linear whose output columns are the concatenation of named HF projections."""
 
     def __init__(self, in_features, slices, bias=False, device=None, dtype=None):
@@ -136,7 +137,7 @@ class LlamaAttention(nn.Module):
         self.hq, self.hkv, self.hd = cfg.num_attention_heads, cfg.num_key_value_heads, hd
         self.qkv_proj = FusedLinear(cfg.hidden_size, [("q_proj", self.hq * hd), ("k_proj", self.hkv * hd),
                                                       ("v_proj", self.hkv * hd)], device=device, dtype=dtype)
-        self.o_proj = nn.Linear(self.hq * hd, cfg.hidden_size, bias=False, device=device, dtype=dtype)
+        self.o_proj = Linear(self.hq * hd, cfg.hidden_size, bias=False, device=device, dtype=dtype)
 
     def forward(self, x, B, S, cos, sin):
         qkv = self.qkv_proj(x)
@@ -149,7 +150,7 @@ class LlamaMLP(nn.Module):
         super().__init__()
         f = cfg.intermediate_size
         self.gate_up_proj = FusedLinear(cfg.hidden_size, [("gate_proj", f), ("up_proj", f)], device=device, dtype=dtype)
-        self.down_proj = nn.Linear(f, cfg.hidden_size, bias=False, device=device, dtype=dtype)
+        self.down_proj = Linear(f, cfg.hidden_size, bias=False, device=device, dtype=dtype)
 
     def forward(self, x):
         return self.down_proj(ops.swiglu(self.gate_up_proj(x)))
@@ -198,7 +199,7 @@ class LlamaForCausalLM(nn.Module):
         super().__init__()
         self.config = cfg
         self.model = LlamaModel(cfg, device, dtype)
-        self.lm_head = nn.Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
+        self.lm_head = Linear(cfg.hidden_size, cfg.vocab_size, bias=False, device=device, dtype=dtype)
         if cfg.tie_word_embeddings:
             self.lm_head.weight = self.model.embed_tokens.weight
         self.gradient_checkpointing = False

@@ -300,7 +300,12 @@ class _LMHeadCE(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dh = dlogits @ weight
         if ctx.needs_input_grad[1]:
-            dw = dlogits.t() @ hidden
+            slot = getattr(weight, "_grt_slot", None)
+            if slot is not None:   # GEMM writes dW straight into the DDP bucket (ops/linear.py)
+                slot.write(lambda v: torch.mm(dlogits.t(), hidden, out=v), lambda v: v.addmm_(dlogits.t(), hidden))
+                slot.notify(weight)
+            else:
+                dw = dlogits.t() @ hidden
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dlogits.sum(0)
         return dh, dw, db, None, None

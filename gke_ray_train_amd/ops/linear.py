@@ -1,0 +1,77 @@
+"""Linear layer whose weight gradient is written by the GEMM straight into the DDP/FSDP bucket.
+
+Torch's autograd produces a fresh dW tensor per backward and AccumulateGrad then adds it into
+``param.grad`` — with gradient-as-bucket-view DDP that is an extra read+read+write of every
+weight gradient per step plus a memset of the whole gradient buffer in ``zero_grad``
+(profiles/r1_bench1gpu_kernel_stats.md: ~2.5 % of a Llama-2-7B step). Here the backward GEMM
+writes dW into its slot of the flat gradient buffer directly: ``beta = 0`` on the first
+contribution of a step (no zeroing pass needed) and ``beta = 1`` — hipBLASLt's in-epilogue
+accumulation — on later gradient-accumulation micro-steps. The data-parallel engine is then
+notified exactly like a post-accumulate-grad hook so bucketed all-reduce overlap is unchanged.
+
+The engine attaches ``param._grt_slot = GradSlot(view, notify)``; without it this is F.linear.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class GradSlot:
+    __slots__ = ("view", "fresh", "notify")
+
+    def __init__(self, view: torch.Tensor, notify):
+        self.view = view
+        self.fresh = True
+        self.notify = notify
+
+    def write(self, fn_out, fn_acc):
+        if self.fresh:
+            fn_out(self.view)
+            self.fresh = False
+        else:
+            fn_acc(self.view)
+
+
+class _DirectGradLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_b = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = dy @ w
+        x2 = x.reshape(-1, x.shape[-1])
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            slot = getattr(w, "_grt_slot", None)
+            if slot is not None:
+                slot.write(lambda v: torch.mm(dy2.t(), x2, out=v), lambda v: v.addmm_(dy2.t(), x2))
+                slot.notify(w)
+            else:
+                dw = dy2.t() @ x2
+        if ctx.has_b:
+            b_needs = ctx.needs_input_grad[2]
+            if b_needs:
+                db = dy2.sum(0)
+        return dx, dw, db
+
+
+def linear(x, weight, bias=None):
+    if weight.requires_grad and getattr(weight, "_grt_slot", None) is not None and torch.is_grad_enabled():
+        return _DirectGradLinear.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+class Linear(nn.Linear):
+    """nn.Linear (same parameters / state_dict) routed through ``ops.linear``."""
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias)

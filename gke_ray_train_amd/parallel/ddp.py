@@ -28,6 +28,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..ops.linear import GradSlot, Linear as _DirectLinear
 from .comm import plan_bucket_bytes
 
 
@@ -78,6 +79,15 @@ class DistributedDataParallel(nn.Module):
         self._sync = True
         self._hooks = []
         self._grad_view = {}
+        self._bucket_of = {}
+        # weights whose backward GEMM writes straight into the flat gradient buffer
+        self._direct = set()
+        for m in module.modules():
+            if isinstance(m, _DirectLinear) and m.weight.requires_grad:
+                self._direct.add(id(m.weight))
+        lm_head = getattr(module, "lm_head", None)
+        if isinstance(lm_head, nn.Linear) and lm_head.weight.requires_grad:
+            self._direct.add(id(lm_head.weight))
         named = []
         seen = set()
         for n, p in module.named_parameters():
@@ -100,6 +110,18 @@ class DistributedDataParallel(nn.Module):
                 for g in self.groups:
                     dist.broadcast(g.flat, src=dist.get_global_rank(process_group, 0) if process_group else 0,
                                    group=process_group)
+        # every parameter owns a GradSlot (its view into the flat gradient buffer + a "fresh"
+        # flag); weights of ops.Linear / the LM head are additionally written in place by their
+        # backward GEMM. zero_grad() only flips flags: no memset of the gradient buffer.
+        self._slots = {}
+        for g in self.groups:
+            for b in g.buckets:
+                for p in b.params:
+                    self._bucket_of[p] = (g, b)
+                    sl = GradSlot(self._grad_view[p], self._notify)
+                    self._slots[p] = sl
+                    if id(p) in self._direct:
+                        p._grt_slot = sl
         self._register_hooks()
 
     # ------------------------------------------------------------------ layout
@@ -141,18 +163,31 @@ class DistributedDataParallel(nn.Module):
 
     def _make_hook(self, g: _FlatGroup, b: _Bucket):
         def hook(p):
-            view = self._grad_view[p]
+            # AccumulateGrad path (params not written by a direct-grad GEMM, or CPU fallbacks)
+            sl = self._slots[p]
+            view = sl.view
             if p.grad is not view and p.grad.data_ptr() != view.data_ptr():
-                # a caller reset .grad (e.g. zero_grad(set_to_none=True)): fold it back in
                 with torch.no_grad():
-                    view.copy_(p.grad)
+                    if sl.fresh:
+                        view.copy_(p.grad)
+                    else:
+                        view.add_(p.grad)
                 p.grad = view
-            if not self._sync or self.world_size == 1:
-                return
-            b.ready += 1
-            if b.ready == len(b.params):
-                self._launch(g, b)
+            sl.fresh = False
+            self._mark_ready(g, b)
         return hook
+
+    def _notify(self, p):
+        p.grad = self._slots[p].view
+        g, b = self._bucket_of[p]
+        self._mark_ready(g, b)
+
+    def _mark_ready(self, g, b):
+        if not self._sync or self.world_size == 1:
+            return
+        b.ready += 1
+        if b.ready == len(b.params):
+            self._launch(g, b)
 
     def _launch(self, g: _FlatGroup, b: _Bucket):
         if b.work is None:
@@ -170,6 +205,12 @@ class DistributedDataParallel(nn.Module):
 
     def finish_gradient_sync(self):
         """Wait for every bucket's all-reduce (launching any whose params got no gradient)."""
+        stale = [p for p, sl in self._slots.items() if sl.fresh]
+        if stale:  # parameters that got no gradient this step: their slots hold last step's data
+            torch._foreach_zero_([self._slots[p].view for p in stale])
+            for p in stale:
+                self._slots[p].fresh = False
+                p.grad = self._slots[p].view
         if self.world_size == 1:
             return
         for g in self.groups:
@@ -185,12 +226,11 @@ class DistributedDataParallel(nn.Module):
     def grad_buffers(self) -> List[torch.Tensor]:
         return [g.grad for g in self.groups]
 
-    def zero_grad(self, set_to_none: bool = False):
-        for g in self.groups:
-            g.grad.zero_()
-        for p, v in self._grad_view.items():
-            if p.grad is None or p.grad.data_ptr() != v.data_ptr():
-                p.grad = v
+    def zero_grad(self, set_to_none: bool = True):
+        """Mark every gradient slot fresh: the next write overwrites (GEMM beta = 0 / copy)."""
+        for p, sl in self._slots.items():
+            sl.fresh = True
+            p.grad = None
 
     def optimizer_param_groups(self, weight_decay: float = 0.0):
         """One flat Parameter per (dtype, decay) group; its .grad is the flat gradient buffer."""
