@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""BasicLLM char-level LM trained data-parallel through TorchTrainer (reference:
+ray-jobs/pytorch_llm_ray.py). Same config keys, same data files / vocab JSON / sentinel, same
+epoch report + rank-0 checkpoint (model.pth / optimizer.pth / scheduler.pth) kept best-1 by loss.
+
+MI355X path: the model runs on the fused HIP ops (LayerNorm+residual, GELU, dropout, flash
+attention, fused CE), ``prepare_model`` wraps it in the flat-buffer RCCL DDP at every world size,
+gradients are clipped on device and applied by the fused AdamW; batches come from the native
+window gatherer with pinned-memory H2D prefetch. ``--dtype fp32`` keeps the reference's fp32
+training; ``--dtype bf16`` runs the bf16 kernels.
+
+Run: ``python jobs/pytorch_llm_ray.py`` (all GPUs of the node) or
+``python jobs/pytorch_llm_ray.py --cpu --workers 2 --preset tiny`` (gloo plumbing, BASELINE config #1).
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from gke_ray_train_amd import train  # noqa: E402
+from gke_ray_train_amd.train import Checkpoint, CheckpointConfig, RunConfig, ScalingConfig  # noqa: E402
+from gke_ray_train_amd.train.torch import TorchConfig, TorchTrainer  # noqa: E402
+
+PVC = os.environ.get("GRT_PVC", os.path.abspath("pvc"))
+
+
+def warmup_cosine(total_steps: int, warmup_ratio: float, min_lr_ratio: float):
+    warm = int(total_steps * warmup_ratio)
+    decay = total_steps - warm
+
+    def f(step):
+        if step < warm:
+            return step / max(1, warm)
+        if step < total_steps:
+            prog = (step - warm) / max(1, decay)
+            return min_lr_ratio + (1.0 - min_lr_ratio) * 0.5 * (1.0 + math.cos(math.pi * prog))
+        return min_lr_ratio
+    return f
+
+
+def _prepare_char_data(cfg, rank):
+    """Rank 0 tokenizes the raw text once; the others wait on a store barrier (not a 5 s poll)."""
+    import torch.distributed as dist
+    from gke_ray_train_amd.data import CharTokenizer, wikitext
+
+    out_dir = cfg["processed_data_dir"]
+    ids_f = os.path.join(out_dir, "train.ids.pt")
+    vocab_f = os.path.join(out_dir, "char_vocab.json")
+    vs_f = os.path.join(out_dir, "vocab_size.txt")
+    done_f = os.path.join(out_dir, "_DATA_PREP_DONE")
+    if rank == 0:
+        os.makedirs(out_dir, exist_ok=True)
+        if not os.path.exists(done_f):
+            raw = cfg["raw_data_path"]
+            if not os.path.exists(raw):
+                wikitext.prepare(os.path.dirname(raw), scale=cfg.get("synthetic_scale", 1.0))
+            with open(raw, encoding="utf-8") as f:
+                text = f.read()
+            tok = CharTokenizer()
+            tok.fit_on_text(text)
+            tok.save_vocab(vocab_f)
+            ids = torch.from_numpy(tok.encode_np(text))
+            tmp = ids_f + ".tmp"
+            torch.save(ids, tmp)
+            os.replace(tmp, ids_f)
+            with open(vs_f, "w") as f:
+                f.write(str(tok.vocab_size))
+            with open(done_f, "w") as f:
+                f.write("done")
+            print(f"rank0: prepared {len(ids):,} chars, vocab {tok.vocab_size}", flush=True)
+    if dist.is_initialized():
+        dist.barrier()
+    with open(vs_f) as f:
+        vocab = int(f.read().strip())
+    return torch.load(ids_f, weights_only=True), vocab
+
+
+def train_loop_per_worker(config: dict):
+    from gke_ray_train_amd.data import TokenBatchLoader
+    from gke_ray_train_amd.models import BasicLLM
+    from gke_ray_train_amd.ops import clip_grad_norm_, make_optimizer
+
+    ctx = train.get_context()
+    rank, world = ctx.get_world_rank(), ctx.get_world_size()
+    device = train.torch.get_device()
+    dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[config.get("dtype", "fp32")]
+
+    ids, vocab = _prepare_char_data(config, rank)
+    S, B = config["dataset_seq_len"], config["batch_size_per_worker"]
+    loader = TokenBatchLoader(ids, S, B, device=device, rank=rank, world=world, shuffle=True, seed=0,
+                              max_windows=config.get("max_windows") or (16000 if config.get("test_run", True) else None))
+    if len(loader) == 0:
+        raise ValueError(f"rank {rank}: empty dataset ({len(ids)} tokens, seq_len {S})")
+    torch.manual_seed(config.get("seed", 0))
+    model = BasicLLM(vocab_size=vocab, embed_dim=config["embed_dim"], num_heads=config["num_heads"],
+                     num_layers=config["num_layers"], hidden_dim=config["hidden_dim"],
+                     max_seq_len=config["model_max_seq_len"], dropout=config.get("dropout", 0.1),
+                     device=device, dtype=dtype)
+    model = train.torch.prepare_model(model)
+    if rank == 0:
+        n = sum(p.numel() for p in model.parameters() if p.requires_grad)
+        print(f"BasicLLM: {n:,} trainable params, vocab {vocab}, {len(loader)} batches/epoch/rank", flush=True)
+    opt = make_optimizer("adamw_torch", model.optimizer_param_groups(weight_decay=0.01) if config.get("flat_optimizer", True)
+                         else model.parameters(), lr=config["lr"], weight_decay=0.01)
+    total = config["num_epochs"] * len(loader)
+    sched = torch.optim.lr_scheduler.LambdaLR(opt, warmup_cosine(total, config.get("warmup_steps_ratio", 0.05),
+                                                                 config.get("min_lr_ratio", 0.01)))
+    start_epoch, step = 0, 0
+    ck = train.get_checkpoint()
+    if ck is not None:
+        with ck.as_directory() as d:
+            model.module.load_state_dict(torch.load(os.path.join(d, "model.pth"), map_location=device, weights_only=True))
+            opt.load_state_dict(torch.load(os.path.join(d, "optimizer.pth"), map_location=device, weights_only=False))
+            sched.load_state_dict(torch.load(os.path.join(d, "scheduler.pth"), weights_only=False))
+            start_epoch = sched.state_dict().get("last_epoch", 0) // max(1, len(loader))
+            step = sched.last_epoch
+    log_every = config.get("log_frequency_batches", 20)
+    for epoch in range(start_epoch, config["num_epochs"]):
+        loader.set_epoch(epoch)
+        model.train()
+        t0, ntok = time.time(), 0
+        for bi, (x, y) in enumerate(loader):
+            loss = model.module.loss(x, y)
+            loss.backward()
+            model.finish_gradient_sync()
+            st = clip_grad_norm_(model.grad_buffers(), 1.0, prescale=1.0 / world)
+            opt.step(grad_scale=st)
+            sched.step()
+            model.zero_grad()
+            step += 1
+            ntok += x.numel()
+            if rank == 0 and (bi % log_every == 0 or bi == len(loader) - 1):
+                dt = time.time() - t0
+                print(f"epoch {epoch + 1} batch {bi + 1}/{len(loader)} step {step} loss {loss.item():.4f} "
+                      f"lr {sched.get_last_lr()[0]:.2e} tok/s/rank {ntok / max(dt, 1e-9):,.0f}", flush=True)
+        metrics = {"loss": float(loss.item()), "epoch": epoch + 1, "learning_rate_epoch_end": sched.get_last_lr()[0],
+                   "global_step_epoch_end": step, "tokens_per_sec": ntok * world / max(time.time() - t0, 1e-9)}
+        with tempfile.TemporaryDirectory() as d:
+            ckpt = None
+            if rank == 0:
+                torch.save(model.module.state_dict(), os.path.join(d, "model.pth"))
+                torch.save(opt.state_dict(), os.path.join(d, "optimizer.pth"))
+                torch.save(sched.state_dict(), os.path.join(d, "scheduler.pth"))
+                ckpt = Checkpoint.from_directory(d)
+            train.report(metrics, checkpoint=ckpt)
+
+
+PRESETS = {
+    "reference": dict(embed_dim=2048, num_layers=24, num_heads=16, hidden_dim=8192),  # ~1.21 B params
+    "gpt2-small": dict(embed_dim=768, num_layers=12, num_heads=12, hidden_dim=3072),
+    "tiny": dict(embed_dim=256, num_layers=2, num_heads=2, hidden_dim=512),
+}
+
+
+def build_config(a):
+    cfg = {
+        "lr": 3e-4, "batch_size_per_worker": a.batch, "num_epochs": a.epochs, "model_max_seq_len": 1024,
+        "dataset_seq_len": a.seq, "dataloader_num_workers": 0, "log_frequency_batches": 20,
+        "train_report_frequency_steps": 20, "warmup_steps_ratio": 0.05, "min_lr_ratio": 0.01,
+        "raw_data_path": os.path.join(a.pvc, "datasets", "wikitext-2-raw", "wiki.train.tokens"),
+        "processed_data_dir": os.path.join(a.pvc, "datasets", "wikitext-2-processed"),
+        "storage_path_base_on_fuse": os.path.join(a.pvc, "ray_llm_training_runs"),
+        "experiment_name_for_tb": a.name, "test_run": not a.full, "dtype": a.dtype,
+        "synthetic_scale": a.data_scale, "max_windows": a.max_windows,
+    }
+    cfg.update(PRESETS[a.preset])
+    return cfg
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workers", type=int, default=int(os.environ.get("NUM_GPUS_PER_NODE", "0")) or None)
+    ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--preset", default="reference", choices=sorted(PRESETS))
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--seq", type=int, default=256)
+    ap.add_argument("--epochs", type=int, default=1)
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--full", action="store_true", help="disable test_run subsampling")
+    ap.add_argument("--pvc", default=PVC)
+    ap.add_argument("--name", default="wikitext2_manualTB_v1")
+    ap.add_argument("--data-scale", type=float, default=1.0)
+    ap.add_argument("--max-windows", type=int, default=None, help="override test_run's 16,000-window subset")
+    a = ap.parse_args(argv)
+    use_gpu = not a.cpu and torch.cuda.is_available()
+    workers = a.workers or (torch.cuda.device_count() if use_gpu else 2)
+    cfg = build_config(a)
+    trainer = TorchTrainer(
+        train_loop_per_worker, train_loop_config=cfg,
+        scaling_config=ScalingConfig(num_workers=workers, use_gpu=use_gpu, resources_per_worker={"GPU": 1} if use_gpu else None),
+        run_config=RunConfig(name=a.name, storage_path=cfg["storage_path_base_on_fuse"],
+                             checkpoint_config=CheckpointConfig(num_to_keep=1, checkpoint_score_attribute="loss",
+                                                                checkpoint_score_order="min")),
+        torch_config=TorchConfig(backend="nccl" if use_gpu else "gloo"))
+    result = trainer.fit()
+    print(f"--- training finished: {a.name} ---\nmetrics: {result.metrics}\ncheckpoint: {result.checkpoint}")
+    return result
+
+
+if __name__ == "__main__":
+    main()
