@@ -1,0 +1,244 @@
+"""LoRA adapters (PEFT semantics) for the fused-projection Llama layout.
+
+Reference: ``LoraConfig(lora_alpha=16, lora_dropout=0.1, r=64, bias="none", task_type="CAUSAL_LM",
+target_modules=[q,k,v,o,gate,up,down]_proj)`` passed to SFTTrainer, then ``merge_and_unload()``
+(ray-jobs/fine_tune_llama_ray.py:243-254,353; fine_tune_config.json:6-8,30-33).
+
+The model keeps q/k/v and gate/up as ONE fused base GEMM each. A LoRA wrapper over a fused
+projection holds one (A, B) pair per targeted HF sub-projection; the A matrices of all targeted
+slices are concatenated so the down-projection is ONE GEMM ``x @ A_cat^T`` ([tokens, r * k]), and
+the up-projection is one GEMM against a block-diagonal ``B`` assembled on the fly (k x r columns,
+< 5 % of the base GEMM's FLOPs at r = 64). The adapter output is added to the base output in one
+elementwise pass. Parameter names on disk follow HF PEFT
+(``base_model.model.<module>.<proj>.lora_A.weight`` / ``lora_B.weight``).
+
+Documented deviation: one dropout mask per fused input (HF draws separate masks for q, k, v).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import re
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .quant import NF4Linear
+
+
+@dataclass
+class LoraConfig:
+    r: int = 8
+    lora_alpha: int = 8
+    lora_dropout: float = 0.0
+    target_modules: Optional[List[str]] = None
+    bias: str = "none"
+    task_type: str = "CAUSAL_LM"
+    modules_to_save: Optional[List[str]] = None
+    init_lora_weights: bool = True
+    use_rslora: bool = False
+
+    @property
+    def scaling(self) -> float:
+        return self.lora_alpha / (math.sqrt(self.r) if self.use_rslora else self.r)
+
+    def to_dict(self):
+        d = asdict(self)
+        d["peft_type"] = "LORA"
+        return d
+
+
+class LoraLinear(nn.Module):
+    """base(x) + scaling * B(dropout(A(x))) for every targeted (sub-)projection of ``base``."""
+
+    def __init__(self, base: nn.Module, targets: List[tuple], cfg: LoraConfig):
+        super().__init__()
+        self.base = base
+        self.r = cfg.r
+        self.scaling = cfg.scaling
+        self.dropout_p = cfg.lora_dropout
+        dev = next((t.device for t in base.buffers()), None) or next(base.parameters()).device
+        dt = getattr(base, "compute_dtype", None) or next(base.parameters()).dtype
+        self.in_features = base.in_features
+        self.out_features = base.out_features
+        self.targets = [(name, off, n) for name, off, n in targets]
+        self.lora_A = nn.ParameterDict()
+        self.lora_B = nn.ParameterDict()
+        for name, off, n in self.targets:
+            a = torch.empty(cfg.r, self.in_features, device=dev, dtype=dt)
+            nn.init.kaiming_uniform_(a, a=math.sqrt(5))  # PEFT default init (B = 0)
+            self.lora_A[name] = nn.Parameter(a)
+            self.lora_B[name] = nn.Parameter(torch.zeros(n, cfg.r, device=dev, dtype=dt))
+        self.full_cover = (len(self.targets) == 1 and self.targets[0][1] == 0 and
+                           self.targets[0][2] == self.out_features)
+
+    def forward(self, x):
+        y = self.base(x)
+        xd = ops.dropout(x, self.dropout_p, self.training) if self.dropout_p > 0 else x
+        names = [t[0] for t in self.targets]
+        a = torch.cat([self.lora_A[n] for n in names], 0) if len(names) > 1 else self.lora_A[names[0]]
+        h = F.linear(xd, a) * self.scaling                      # [T, r * k]
+        if self.full_cover:
+            return y + F.linear(h, self.lora_B[names[0]])
+        # block-diagonal B placed at each target's output columns
+        bfull = h.new_zeros(self.out_features, self.r * len(names))
+        for i, (n, off, cnt) in enumerate(self.targets):
+            bfull = bfull.index_copy(0, torch.arange(off, off + cnt, device=h.device),
+                                     F.pad(self.lora_B[n], (i * self.r, (len(names) - 1 - i) * self.r)))
+        return y + F.linear(h, bfull)
+
+    @torch.no_grad()
+    def merged_weight(self) -> torch.Tensor:
+        w = self.base.dequantize() if isinstance(self.base, NF4Linear) else self.base.weight.detach().clone()
+        w = w.clone()
+        for n, off, cnt in self.targets:
+            w[off:off + cnt] += (self.lora_B[n].float() @ self.lora_A[n].float() * self.scaling).to(w.dtype)
+        return w
+
+
+_ALL_PROJ = ["q_proj", "k_proj", "v_proj", "o_proj", "gate_proj", "up_proj", "down_proj"]
+
+
+def _targets_for(module_name: str, mod: nn.Module, wanted: List[str]):
+    slices = getattr(mod, "slices", None)
+    if slices:
+        out, off = [], 0
+        for sub, n in slices:
+            if sub in wanted:
+                out.append((sub, off, n))
+            off += n
+        return out
+    leaf = module_name.rsplit(".", 1)[-1]
+    if leaf in wanted:
+        return [(leaf, 0, mod.out_features)]
+    return []
+
+
+class PeftModel(nn.Module):
+    def __init__(self, model: nn.Module, cfg: LoraConfig):
+        super().__init__()
+        self.base_model = model
+        self.peft_config = {"default": cfg}
+        wanted = cfg.target_modules or _ALL_PROJ
+        if isinstance(wanted, str):
+            wanted = [m for m in _ALL_PROJ if re.fullmatch(wanted, m)]
+        for p in model.parameters():
+            p.requires_grad_(False)
+        self.lora_modules: Dict[str, LoraLinear] = {}
+        for name, parent in list(model.named_modules()):
+            for cname, child in list(parent.named_children()):
+                full = f"{name}.{cname}" if name else cname
+                if isinstance(child, (nn.Linear, NF4Linear)) and not full.endswith("lm_head"):
+                    tg = _targets_for(full, child, wanted)
+                    if tg:
+                        lw = LoraLinear(child, tg, cfg)
+                        setattr(parent, cname, lw)
+                        self.lora_modules[full] = lw
+        if cfg.modules_to_save:
+            for n, p in model.named_parameters():
+                if any(m in n for m in cfg.modules_to_save):
+                    p.requires_grad_(True)
+        if not self.lora_modules:
+            raise ValueError(f"no module matched target_modules={wanted}")
+
+    @property
+    def config(self):
+        return self.base_model.config
+
+    def forward(self, *a, **k):
+        return self.base_model(*a, **k)
+
+    def trainable_parameters(self):
+        return [p for p in self.parameters() if p.requires_grad]
+
+    def print_trainable_parameters(self):
+        t = sum(p.numel() for p in self.parameters() if p.requires_grad)
+        tot = sum(p.numel() for p in self.parameters()) + sum(
+            m.base.in_features * m.base.out_features for m in self.lora_modules.values() if isinstance(m.base, NF4Linear))
+        print(f"trainable params: {t:,} || all params: {tot:,} || trainable%: {100 * t / max(tot, 1):.4f}")
+        return t, tot
+
+    # ------------------------------------------------------------------ adapters on disk
+    def adapter_state_dict(self) -> Dict[str, torch.Tensor]:
+        out = {}
+        for full, m in self.lora_modules.items():
+            base = full.rsplit(".", 1)[0] if getattr(m.base, "slices", None) else full
+            for sub, _, _ in m.targets:
+                key = f"{base}.{sub}" if getattr(m.base, "slices", None) else full
+                out[f"base_model.model.{key}.lora_A.weight"] = m.lora_A[sub].detach().contiguous()
+                out[f"base_model.model.{key}.lora_B.weight"] = m.lora_B[sub].detach().contiguous()
+        return out
+
+    def load_adapter_state_dict(self, sd: Dict[str, torch.Tensor]):
+        with torch.no_grad():
+            for full, m in self.lora_modules.items():
+                base = full.rsplit(".", 1)[0] if getattr(m.base, "slices", None) else full
+                for sub, _, _ in m.targets:
+                    key = f"{base}.{sub}" if getattr(m.base, "slices", None) else full
+                    m.lora_A[sub].copy_(sd[f"base_model.model.{key}.lora_A.weight"])
+                    m.lora_B[sub].copy_(sd[f"base_model.model.{key}.lora_B.weight"])
+
+    def save_pretrained(self, path: str):
+        from safetensors.torch import save_file
+        os.makedirs(path, exist_ok=True)
+        save_file({k: v.cpu() for k, v in self.adapter_state_dict().items()},
+                  os.path.join(path, "adapter_model.safetensors"))
+        cfg = self.peft_config["default"].to_dict()
+        cfg["base_model_name_or_path"] = getattr(self.config, "name", "llama")
+        with open(os.path.join(path, "adapter_config.json"), "w") as f:
+            json.dump(cfg, f, indent=2)
+
+    def load_adapter(self, path: str):
+        from safetensors.torch import load_file
+        self.load_adapter_state_dict(load_file(os.path.join(path, "adapter_model.safetensors")))
+
+    # ------------------------------------------------------------------ merge
+    @torch.no_grad()
+    def merge_and_unload(self) -> nn.Module:
+        """W <- W + scaling * B A for every adapter (NF4 bases are dequantised to bf16 first);
+        returns the plain base model with ordinary (ops.Linear) projections."""
+        from ..ops.linear import Linear
+        model = self.base_model
+        for full, m in list(self.lora_modules.items()):
+            w = m.merged_weight()
+            parent_name, cname = full.rsplit(".", 1) if "." in full else ("", full)
+            parent = model.get_submodule(parent_name) if parent_name else model
+            lin = Linear(m.in_features, m.out_features, bias=False, device=w.device, dtype=w.dtype)
+            lin.weight.copy_(w)
+            if getattr(m.base, "slices", None):
+                from ..models.llama import FusedLinear
+                fl = FusedLinear(m.in_features, m.base.slices, device=w.device, dtype=w.dtype)
+                fl.weight.copy_(w)
+                lin = fl
+            setattr(parent, cname, lin)
+        for name, parent in list(model.named_modules()):  # remaining (non-adapted) NF4 layers
+            for cname, child in list(parent.named_children()):
+                if isinstance(child, NF4Linear):
+                    w = child.dequantize()
+                    slices = getattr(child, "slices", None)
+                    if slices:
+                        from ..models.llama import FusedLinear
+                        lin = FusedLinear(child.in_features, slices, device=w.device, dtype=w.dtype)
+                    else:
+                        lin = Linear(child.in_features, child.out_features, bias=False, device=w.device, dtype=w.dtype)
+                    lin.weight.copy_(w)
+                    setattr(parent, cname, lin)
+        self.lora_modules = {}
+        return model
+
+
+def get_peft_model(model: nn.Module, cfg: LoraConfig) -> PeftModel:
+    return PeftModel(model, cfg)
+
+
+def prepare_model_for_kbit_training(model: nn.Module, use_gradient_checkpointing: bool = True):
+    for p in model.parameters():
+        p.requires_grad_(False)
+    if use_gradient_checkpointing and hasattr(model, "gradient_checkpointing_enable"):
+        model.gradient_checkpointing_enable()
+    return model

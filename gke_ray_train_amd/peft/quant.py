@@ -1,0 +1,129 @@
+"""NF4 (4-bit NormalFloat) frozen linear layer for QLoRA.
+
+Reference role: ``BitsAndBytesConfig(load_in_4bit=True, bnb_4bit_quant_type="nf4",
+bnb_4bit_compute_dtype=bfloat16, bnb_4bit_use_double_quant=USE_NESTED_QUANT)``
+(ray-jobs/fine_tune_llama_ray.py:215-227). Weights are quantised once on the GPU by the HIP
+kernel (blocks of 64, fp32 absmax); every forward AND backward dequantises into a transient
+bf16 weight (never stored for autograd, so the base model costs ~0.53 bytes/param resident) and
+runs the hipBLASLt GEMM. ``double_quant`` additionally stores the absmax vector as 8-bit codes
+with one fp32 scale per 256 blocks (bitsandbytes' nested quantisation) and expands it on device.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+
+
+@dataclass
+class BitsAndBytesConfig:
+    load_in_4bit: bool = True
+    bnb_4bit_quant_type: str = "nf4"
+    bnb_4bit_compute_dtype: torch.dtype = torch.bfloat16
+    bnb_4bit_use_double_quant: bool = False
+    blocksize: int = 64
+
+    def __post_init__(self):
+        if isinstance(self.bnb_4bit_compute_dtype, str):
+            self.bnb_4bit_compute_dtype = getattr(torch, self.bnb_4bit_compute_dtype)
+        if self.bnb_4bit_quant_type != "nf4":
+            raise ValueError("only nf4 is implemented")
+
+
+class _NF4Matmul(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, layer):
+        w = layer.dequantize()
+        ctx.layer = layer
+        return F.linear(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        w = ctx.layer.dequantize()  # recomputed: the bf16 weight is never kept alive for autograd
+        return dy @ w, None
+
+
+class NF4Linear(nn.Module):
+    def __init__(self, in_features: int, out_features: int, compute_dtype=torch.bfloat16, blocksize: int = 64,
+                 double_quant: bool = False, device=None, slices=None):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.compute_dtype = compute_dtype
+        self.blocksize = blocksize
+        self.double_quant = double_quant
+        n = in_features * out_features
+        self.register_buffer("qweight", torch.zeros(n // 2, dtype=torch.uint8, device=device))
+        nb = n // blocksize
+        if double_quant:
+            self.register_buffer("absmax_q", torch.zeros(nb, dtype=torch.uint8, device=device))
+            self.register_buffer("absmax_scale", torch.zeros((nb + 255) // 256, dtype=torch.float32, device=device))
+            self.register_buffer("absmax_offset", torch.zeros(1, dtype=torch.float32, device=device))
+        else:
+            self.register_buffer("absmax", torch.zeros(nb, dtype=torch.float32, device=device))
+        if slices is not None:
+            self.slices = list(slices)
+
+    @classmethod
+    @torch.no_grad()
+    def from_linear(cls, lin: nn.Linear, cfg: BitsAndBytesConfig) -> "NF4Linear":
+        w = lin.weight.detach()
+        m = cls(lin.in_features, lin.out_features, cfg.bnb_4bit_compute_dtype, cfg.blocksize,
+                cfg.bnb_4bit_use_double_quant, device=w.device, slices=getattr(lin, "slices", None))
+        q, a = ops.nf4_quantize(w.contiguous().view(-1), cfg.blocksize)
+        m.qweight.copy_(q)
+        if cfg.bnb_4bit_use_double_quant:
+            off = a.mean()
+            c = a - off
+            blocks = F.pad(c, (0, (-c.numel()) % 256)).view(-1, 256)
+            sc = blocks.abs().amax(1).clamp_min(1e-12)
+            codes = torch.round(blocks / sc[:, None] * 127).clamp(-127, 127).to(torch.int16) + 128
+            m.absmax_q.copy_(codes.view(-1)[: a.numel()].to(torch.uint8))
+            m.absmax_scale.copy_(sc)
+            m.absmax_offset.fill_(float(off))
+        else:
+            m.absmax.copy_(a)
+        return m
+
+    def _absmax(self) -> torch.Tensor:
+        if not self.double_quant:
+            return self.absmax
+        nb = self.absmax_q.numel()
+        codes = self.absmax_q.to(torch.float32) - 128.0
+        sc = self.absmax_scale.repeat_interleave(256)[:nb]
+        return codes / 127.0 * sc + self.absmax_offset
+
+    def dequantize(self) -> torch.Tensor:
+        n = self.in_features * self.out_features
+        w = ops.nf4_dequantize(self.qweight, self._absmax().contiguous(), n, self.blocksize, self.compute_dtype)
+        return w.view(self.out_features, self.in_features)
+
+    @property
+    def weight(self):  # read-only dequantised view (merge_and_unload, inspection)
+        return self.dequantize()
+
+    def forward(self, x):
+        if x.dtype != self.compute_dtype:
+            x = x.to(self.compute_dtype)
+        if torch.is_grad_enabled() and x.requires_grad:
+            return _NF4Matmul.apply(x, self)
+        return F.linear(x, self.dequantize())
+
+
+def quantize_model_(model: nn.Module, cfg: BitsAndBytesConfig, skip=("lm_head",)) -> nn.Module:
+    """Replace every nn.Linear (except ``skip``) by an NF4Linear, in place."""
+    for name, mod in list(model.named_modules()):
+        for cname, child in list(mod.named_children()):
+            full = f"{name}.{cname}" if name else cname
+            if isinstance(child, nn.Linear) and not any(full.endswith(s) for s in skip):
+                setattr(mod, cname, NF4Linear.from_linear(child, cfg))
+                del child
+    for p in model.parameters():
+        p.requires_grad_(False)
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+    return model
