@@ -304,6 +304,21 @@ class LlamaForCausalLM(nn.Module):
         return missing, unexpected
 
 
+def _generate(self, input_ids, **kw):
+    """KV-cache greedy / sampling decode (models/generation.py)."""
+    from .generation import generate
+    return generate(self, input_ids, **kw)
+
+
+def _save_pretrained(self, path, **kw):
+    from .hub import save_pretrained
+    save_pretrained(self, path, **kw)
+
+
+LlamaForCausalLM.generate = _generate
+LlamaForCausalLM.save_pretrained = _save_pretrained
+
+
 def build_llama(name_or_cfg="llama2-7b", device=None, dtype=torch.bfloat16, seed: Optional[int] = 0, **overrides):
     cfg = name_or_cfg if isinstance(name_or_cfg, LlamaConfig) else get_config(name_or_cfg, **overrides)
     model = LlamaForCausalLM(cfg, device=device, dtype=dtype)

@@ -153,6 +153,10 @@ class PeftModel(nn.Module):
     def forward(self, *a, **k):
         return self.base_model(*a, **k)
 
+    def generate(self, *a, **k):
+        from ..models.generation import generate
+        return generate(self.base_model, *a, **k)
+
     def trainable_parameters(self):
         return [p for p in self.parameters() if p.requires_grad]
 

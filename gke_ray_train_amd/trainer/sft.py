@@ -1,0 +1,394 @@
+"""SFT trainer with HF-Trainer / TRL-SFTTrainer semantics on the framework's engines.
+
+Reference: ``SFTConfig(...)`` + ``SFTTrainer(model, args, train_dataset, eval_dataset,
+peft_config).train()`` inside ``train_loop_per_worker`` (ray-jobs/fine_tune_llama_ray.py:295-334)
+with every key of fine_tune_config.json: gradient accumulation with ``no_sync`` on
+non-boundary micro-steps, ``max_grad_norm`` clipping, the ``optim`` / ``lr_scheduler_type`` /
+``warmup_ratio`` / ``weight_decay`` choices, ``group_by_length``, ``packing``, ``logging_steps``
+(loss averaged across ranks), ``eval_steps``, ``save_steps`` -> ``checkpoint-<step>/`` (adapter or
+full weights, optimizer.pt, scheduler.pt, trainer_state.json, training_args.bin, rng_state_<rank>.pth),
+``save_total_limit``, ``report_to="tensorboard"`` (events under ``<output_dir>/runs/``), and the
+``train_result.metrics`` the reference prints (train_runtime, train_samples_per_second, ...).
+
+MI355X specifics: the model runs on the HIP ops; data parallelism is the flat-buffer RCCL DDP over
+the TRAINABLE parameters only (LoRA: 0.67 GB of fp32-equivalent grads per step instead of the
+whole model); clipping + AdamW are the two fused device passes; batches are right-padded to a
+multiple of 8 by the native collator and copied from pinned memory.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import math
+import os
+import random
+import shutil
+import socket
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Any, Dict, List, Optional, Union
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..ops import clip_grad_norm_, make_optimizer
+from ..parallel.ddp import DistributedDataParallel
+from .schedules import get_scheduler
+from .sft_data import LengthGroupedSampler, PadCollator, pack_sequences
+
+
+@dataclass
+class SFTConfig:
+    output_dir: str = "outputs"
+    num_train_epochs: float = 1.0
+    max_steps: int = -1
+    per_device_train_batch_size: int = 8
+    per_device_eval_batch_size: int = 8
+    gradient_accumulation_steps: int = 1
+    optim: str = "adamw_torch"
+    learning_rate: float = 5e-5
+    lr_scheduler_type: str = "linear"
+    warmup_ratio: float = 0.0
+    warmup_steps: int = 0
+    max_grad_norm: float = 1.0
+    weight_decay: float = 0.0
+    adam_beta1: float = 0.9
+    adam_beta2: float = 0.999
+    adam_epsilon: float = 1e-8
+    bf16: bool = False
+    fp16: bool = False
+    group_by_length: bool = False
+    max_seq_length: int = 1024
+    packing: bool = False
+    dataset_text_field: str = "text"
+    logging_steps: int = 500
+    logging_dir: Optional[str] = None
+    save_strategy: str = "steps"
+    save_steps: int = 500
+    save_total_limit: Optional[int] = None
+    report_to: Union[str, List[str]] = "none"
+    evaluation_strategy: Optional[str] = None
+    eval_strategy: str = "no"
+    eval_steps: Optional[int] = None
+    seed: int = 42
+    gradient_checkpointing: bool = False
+    dataloader_drop_last: bool = False
+    max_length: Optional[int] = None
+    master_weights: bool = False
+    disable_tqdm: bool = True
+
+    def __post_init__(self):
+        if self.evaluation_strategy is not None:  # deprecated alias used by the reference (:317)
+            self.eval_strategy = self.evaluation_strategy
+        if self.max_length:
+            self.max_seq_length = self.max_length
+        if self.eval_steps is None:
+            self.eval_steps = self.logging_steps
+        if self.fp16:
+            raise ValueError("fp16 is not supported on this stack; use bf16")
+
+    def to_dict(self):
+        return asdict(self)
+
+
+@dataclass
+class TrainOutput:
+    global_step: int
+    training_loss: float
+    metrics: Dict[str, float]
+
+
+def _world():
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def _rows(ds) -> List[Dict[str, Any]]:
+    if ds is None:
+        return []
+    if hasattr(ds, "take_all"):
+        return ds.take_all()
+    return [r for r in ds]
+
+
+class SFTTrainer:
+    def __init__(self, model, args: SFTConfig, train_dataset=None, eval_dataset=None, peft_config=None,
+                 processing_class=None, tokenizer=None, data_collator=None, callbacks=None, formatting_func=None):
+        self.args = args
+        self.rank, self.world = _world()
+        self.tokenizer = processing_class or tokenizer
+        if self.tokenizer is None:
+            from ..data.tokenizer import ByteTokenizer
+            self.tokenizer = ByteTokenizer(model.config.vocab_size)
+        if getattr(self.tokenizer, "pad_token", None) is None:
+            self.tokenizer.pad_token = self.tokenizer.eos_token
+        self.pad_id = self.tokenizer.pad_token_id if self.tokenizer.pad_token_id is not None else self.tokenizer.eos_token_id
+        if peft_config is not None:
+            from ..peft import get_peft_model
+            model = get_peft_model(model, peft_config)
+        self.model = model
+        if args.gradient_checkpointing:
+            inner = getattr(model, "base_model", model)
+            if hasattr(inner, "gradient_checkpointing_enable"):
+                inner.gradient_checkpointing_enable()
+        self.device = next(model.parameters()).device
+        self.callbacks = list(callbacks or [])
+        self.formatting_func = formatting_func
+        self.train_seqs = self._prepare(train_dataset)
+        self.eval_seqs = self._prepare(eval_dataset)
+        self.collator = data_collator or PadCollator(self.pad_id, 8, args.max_seq_length)
+        torch.manual_seed(args.seed)
+        random.seed(args.seed)
+        np.random.seed(args.seed)
+        self.engine = DistributedDataParallel(model, broadcast_params=True)
+        self.optimizer = make_optimizer(args.optim, self.engine.optimizer_param_groups(args.weight_decay),
+                                        lr=args.learning_rate, weight_decay=args.weight_decay,
+                                        betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
+                                        master_weights=args.master_weights)
+        self.scheduler = None
+        self.state = {"global_step": 0, "epoch": 0.0, "log_history": [], "best_metric": None,
+                      "best_model_checkpoint": None, "total_flos": 0.0}
+        self.tb = None
+        rt = args.report_to if isinstance(args.report_to, list) else [args.report_to]
+        if "tensorboard" in rt and self.rank == 0:
+            from .tb import SummaryWriter
+            ldir = args.logging_dir or os.path.join(args.output_dir, "runs",
+                                                    time.strftime("%b%d_%H-%M-%S") + "_" + socket.gethostname())
+            self.tb = SummaryWriter(ldir)
+
+    # ------------------------------------------------------------------ data
+    def _prepare(self, ds) -> List[List[int]]:
+        rows = _rows(ds)
+        if not rows:
+            return []
+        a = self.args
+        texts = []
+        for r in rows:
+            if self.formatting_func is not None:
+                texts.append(self.formatting_func(r))
+            elif isinstance(r, str):
+                texts.append(r)
+            else:
+                texts.append(r[a.dataset_text_field])
+        seqs = [self.tokenizer.encode(t)[: a.max_seq_length] for t in texts]
+        if a.packing:
+            seqs = pack_sequences(seqs, a.max_seq_length, self.tokenizer.eos_token_id)
+        return seqs
+
+    def _batches(self, seqs, bs, epoch, shuffle=True):
+        n = len(seqs)
+        if self.args.group_by_length and shuffle:
+            sampler = LengthGroupedSampler([len(s) for s in seqs], bs, self.world, self.rank, self.args.seed)
+            sampler.set_epoch(epoch)
+            idx = list(iter(sampler))
+        else:
+            order = list(range(n))
+            if shuffle:
+                g = random.Random(self.args.seed + epoch)
+                g.shuffle(order)
+            per = n // self.world if self.args.dataloader_drop_last else -(-n // self.world)
+            idx = [order[(self.rank + i * self.world) % n] for i in range(per)] if n else []
+        out = []
+        for i in range(0, len(idx), bs):
+            chunk = idx[i:i + bs]
+            if len(chunk) < bs and self.args.dataloader_drop_last:
+                break
+            out.append(self.collator([seqs[j] for j in chunk]))
+        return out
+
+    def _to_dev(self, b):
+        return {k: v.pin_memory().to(self.device, non_blocking=True) if self.device.type == "cuda" else v.to(self.device)
+                for k, v in b.items()}
+
+    # ------------------------------------------------------------------ train
+    def train(self, resume_from_checkpoint: Optional[str] = None) -> TrainOutput:
+        a = self.args
+        bs, accum = a.per_device_train_batch_size, a.gradient_accumulation_steps
+        micro_per_epoch = len(self._batches(self.train_seqs, bs, 0, shuffle=False))
+        steps_per_epoch = max(1, math.ceil(micro_per_epoch / accum))
+        total = a.max_steps if a.max_steps > 0 else math.ceil(a.num_train_epochs * steps_per_epoch)
+        warm = a.warmup_steps or math.ceil(a.warmup_ratio * total)
+        self.scheduler = get_scheduler(a.lr_scheduler_type, self.optimizer, warm, total)
+        start_step = 0
+        if resume_from_checkpoint:
+            start_step = self._load_checkpoint(resume_from_checkpoint)
+        self.model.train()
+        t0 = time.time()
+        tr_loss_sum = torch.zeros((), device=self.device)
+        log_loss = torch.zeros((), device=self.device)
+        log_count = 0
+        ntok = 0
+        nsamples = 0
+        step = start_step
+        epochs = math.ceil(total / steps_per_epoch)
+        done = False
+        for epoch in range(start_step // steps_per_epoch, epochs):
+            batches = self._batches(self.train_seqs, bs, epoch)
+            skip = (start_step - epoch * steps_per_epoch) * accum if epoch == start_step // steps_per_epoch else 0
+            nb = len(batches)
+            for mi in range(max(0, skip), nb):
+                boundary = ((mi + 1) % accum == 0) or (mi == nb - 1)
+                ntok += int(batches[mi]["attention_mask"].sum())  # CPU tensor: no device sync
+                b = self._to_dev(batches[mi])
+                with self.engine.no_sync(not boundary):
+                    out = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])
+                    loss = out["loss"] / accum
+                    loss.backward()
+                tr_loss_sum += loss.detach()
+                log_loss += loss.detach()
+                nsamples += b["input_ids"].shape[0]
+                if not boundary:
+                    continue
+                self.engine.finish_gradient_sync()
+                st = clip_grad_norm_(self.engine.grad_buffers(), a.max_grad_norm, prescale=1.0 / self.world)
+                self.optimizer.step(grad_scale=st)
+                self.scheduler.step()
+                self.engine.zero_grad()
+                step += 1
+                log_count += 1
+                self.state["global_step"] = step
+                self.state["epoch"] = epoch + (mi + 1) / nb
+                if a.logging_steps and step % a.logging_steps == 0:
+                    self._log({"loss": self._mean_across_ranks(log_loss / log_count), "grad_norm": float(st.norm),
+                               "learning_rate": self.scheduler.get_last_lr()[0], "epoch": round(self.state["epoch"], 4)})
+                    log_loss.zero_()
+                    log_count = 0
+                if a.eval_strategy == "steps" and self.eval_seqs and a.eval_steps and step % a.eval_steps == 0:
+                    self.evaluate()
+                if a.save_strategy == "steps" and a.save_steps and step % a.save_steps == 0:
+                    self._save_checkpoint(step)
+                if step >= total:
+                    done = True
+                    break
+            if a.eval_strategy == "epoch" and self.eval_seqs:
+                self.evaluate()
+            if a.save_strategy == "epoch":
+                self._save_checkpoint(step)
+            if done:
+                break
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        rt = time.time() - t0
+        train_loss = self._mean_across_ranks(tr_loss_sum / max(1, step - start_step))
+        gsamples = nsamples * self.world
+        metrics = {"train_runtime": round(rt, 4), "train_samples_per_second": round(gsamples / rt, 3),
+                   "train_steps_per_second": round((step - start_step) / rt, 3),
+                   "total_flos": float(self.state["total_flos"]), "train_loss": train_loss,
+                   "train_tokens_per_second": round(ntok * self.world / rt, 1),
+                   "epoch": round(self.state["epoch"], 4)}
+        self.state["log_history"].append(dict(metrics, step=step))
+        for cb in self.callbacks:
+            if hasattr(cb, "on_train_end"):
+                cb.on_train_end(self, metrics)
+        if self.tb is not None:
+            self.tb.flush()
+        return TrainOutput(step, train_loss, metrics)
+
+    def _mean_across_ranks(self, t: torch.Tensor) -> float:
+        t = t.detach().float().reshape(1).clone()
+        if self.world > 1:
+            dist.all_reduce(t)
+            t /= self.world
+        return float(t.item())
+
+    def _log(self, logs: Dict[str, float]):
+        logs = dict(logs, step=self.state["global_step"])
+        self.state["log_history"].append(logs)
+        if self.rank == 0:
+            print({k: (round(v, 6) if isinstance(v, float) else v) for k, v in logs.items()}, flush=True)
+            if self.tb is not None:
+                for k, v in logs.items():
+                    if k not in ("step", "epoch") and isinstance(v, (int, float)):
+                        self.tb.add_scalar(f"train/{k}" if not k.startswith("eval_") else k.replace("eval_", "eval/"),
+                                           v, self.state["global_step"])
+        for cb in self.callbacks:
+            if hasattr(cb, "on_log"):
+                cb.on_log(self, logs)
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def evaluate(self) -> Dict[str, float]:
+        was = self.model.training
+        self.model.eval()
+        t0 = time.time()
+        tot = torch.zeros(2, device=self.device, dtype=torch.float64)
+        for b in self._batches(self.eval_seqs, self.args.per_device_eval_batch_size, 0, shuffle=False):
+            b = self._to_dev(b)
+            loss = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])["loss"]
+            n = (b["labels"][:, 1:] != -100).sum()
+            tot[0] += loss.double() * n
+            tot[1] += n
+        if self.world > 1:
+            dist.all_reduce(tot)
+        rt = time.time() - t0
+        m = {"eval_loss": float(tot[0] / tot[1].clamp_min(1)), "eval_runtime": round(rt, 4),
+             "eval_samples_per_second": round(len(self.eval_seqs) / max(rt, 1e-9), 3),
+             "epoch": round(self.state["epoch"], 4)}
+        self._log(m)
+        if was:
+            self.model.train()
+        return m
+
+    # ------------------------------------------------------------------ save / load
+    def _unwrapped(self):
+        return self.model
+
+    def save_model(self, output_dir: Optional[str] = None):
+        out = output_dir or self.args.output_dir
+        if self.rank == 0:
+            m = self._unwrapped()
+            if hasattr(m, "save_pretrained") and hasattr(m, "lora_modules"):
+                m.save_pretrained(out)
+            else:
+                from ..models.hub import save_pretrained
+                save_pretrained(m, out)
+            if hasattr(self.tokenizer, "save_pretrained"):
+                self.tokenizer.save_pretrained(out)
+
+    def _save_checkpoint(self, step: int):
+        a = self.args
+        d = os.path.join(a.output_dir, f"checkpoint-{step}")
+        if self.rank == 0:
+            os.makedirs(d, exist_ok=True)
+            self.save_model(d)
+            torch.save(self.optimizer.state_dict(), os.path.join(d, "optimizer.pt"))
+            torch.save(self.scheduler.state_dict(), os.path.join(d, "scheduler.pt"))
+            torch.save(a.to_dict(), os.path.join(d, "training_args.bin"))
+            st = dict(self.state, train_batch_size=a.per_device_train_batch_size, max_steps=a.max_steps,
+                      logging_steps=a.logging_steps, save_steps=a.save_steps, eval_steps=a.eval_steps)
+            with open(os.path.join(d, "trainer_state.json"), "w") as f:
+                json.dump(st, f, indent=2)
+        if self.world > 1:
+            dist.barrier()
+        os.makedirs(d, exist_ok=True)
+        rng = {"python": random.getstate(), "numpy": np.random.get_state(), "cpu": torch.get_rng_state()}
+        if torch.cuda.is_available():
+            rng["cuda"] = torch.cuda.get_rng_state_all()
+        torch.save(rng, os.path.join(d, f"rng_state_{self.rank}.pth"))
+        if self.world > 1:
+            dist.barrier()
+        if self.rank == 0 and a.save_total_limit:
+            ck = sorted(glob.glob(os.path.join(a.output_dir, "checkpoint-*")), key=lambda p: int(p.rsplit("-", 1)[1]))
+            for old in ck[:-a.save_total_limit]:
+                shutil.rmtree(old, ignore_errors=True)
+        for cb in self.callbacks:
+            if hasattr(cb, "on_save"):
+                cb.on_save(self, d)
+
+    def _load_checkpoint(self, d: str) -> int:
+        m = self._unwrapped()
+        if hasattr(m, "load_adapter") and os.path.exists(os.path.join(d, "adapter_model.safetensors")):
+            m.load_adapter(d)
+        else:
+            from ..models.hub import from_pretrained
+            loaded = from_pretrained(d, device=self.device, torch_dtype=next(m.parameters()).dtype)
+            m.load_state_dict(loaded.state_dict())
+        self.optimizer.load_state_dict(torch.load(os.path.join(d, "optimizer.pt"), map_location=self.device,
+                                                  weights_only=False))
+        self.scheduler.load_state_dict(torch.load(os.path.join(d, "scheduler.pt"), weights_only=False))
+        with open(os.path.join(d, "trainer_state.json")) as f:
+            st = json.load(f)
+        self.state.update(st)
+        return int(st["global_step"])
