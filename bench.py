@@ -1,16 +1,19 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Llama-2-7B bf16 full fine-tune, tokens/s for the whole node.
+"""Headline benchmark: Llama-2-7B bf16 fine-tune, tokens/s for the whole node.
 
 BASELINE.json metric: "tokens/sec (whole node) Llama-2-7B fine-tune at 1/2/4/8 MI355X".
-Config #2 "Llama-2 7B DDP bf16, 8 Ray workers on 8xMI355X (fine_tune_llama_ray.py path)":
-* model: Llama-2-7B architecture (6.74 B params), random init, bf16 params + bf16 grads,
-  fp32 AdamW moments (the reference full-FT path: torch_dtype=bfloat16 + paged_adamw_32bit,
+Default = config #2 "Llama-2 7B DDP bf16, 8 Ray workers on 8xMI355X (fine_tune_llama_ray.py path)":
+* model: Llama-2-7B architecture (6.74 B params), random init, bf16 params + bf16 grads, fp32
+  AdamW moments (the reference full-FT path: torch_dtype=bfloat16 + paged_adamw_32bit,
   reference ray-jobs/fine_tune_llama_ray.py:235-241, fine_tune_config.json:17);
-* data: synthetic Wikitext-2-shaped token batches, seq 1024 (MAX_SEQ_LENGTH), 8 sequences per
-  GPU per optimizer step (= the reference's PER_DEVICE_TRAIN_BATCH_SIZE 2 x
-  GRADIENT_ACCUMULATION_STEPS 4, fine_tune_config.json:13-14) — weak scaling;
-* step: forward + backward + DDP gradient all-reduce (RCCL, bucketed, overlapped) + global
-  grad-norm clip (MAX_GRAD_NORM 0.3) + fused AdamW. Nothing is skipped inside the timed region.
+* data: synthetic Wikitext-2-shaped token stream (Zipf ids) streamed by the framework's loader
+  (native window gather -> pinned host ring -> async H2D), seq 1024 (MAX_SEQ_LENGTH), 8 sequences
+  per GPU per optimizer step (= PER_DEVICE_TRAIN_BATCH_SIZE 2 x GRADIENT_ACCUMULATION_STEPS 4,
+  fine_tune_config.json:13-14) — weak scaling;
+* step: forward + backward + gradient sync (RCCL, bucketed, overlapped) + global grad-norm clip
+  (MAX_GRAD_NORM 0.3) + fused AdamW. Nothing is skipped inside the timed region.
+Other BASELINE configs: ``--parallel fsdp`` (#3), ``--peft lora|qlora`` (#4),
+``--model llama3-70b --parallel fsdp --offload`` (#5).
 
 Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
 bench.py --gpus N``. Rank 0 prints ONE JSON line.
@@ -35,16 +38,56 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="llama2-7b")
-    ap.add_argument("--batch", type=int, default=8, help="sequences per GPU per step")
+    ap.add_argument("--batch", type=int, default=8, help="sequences per GPU per optimizer step")
     ap.add_argument("--micro-batch", type=int, default=0, help="micro-batch (grad accumulation); 0 = batch")
     ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--parallel", default="ddp", choices=["ddp", "fsdp"])
+    ap.add_argument("--offload", action="store_true", help="FSDP: optimizer states in pinned host memory")
+    ap.add_argument("--peft", default="none", choices=["none", "lora", "qlora"])
+    ap.add_argument("--lora-r", type=int, default=64)
     ap.add_argument("--bucket-mb", type=float, default=0.0, help="DDP bucket size (0 = planner)")
     ap.add_argument("--max-grad-norm", type=float, default=0.3)
     ap.add_argument("--lr", type=float, default=2e-5)
     ap.add_argument("--checkpointing", action="store_true", help="activation checkpointing")
+    ap.add_argument("--data", default="loader", choices=["loader", "static"])
     ap.add_argument("--profile-dir", default="", help="write a torch.profiler trace here")
     ap.add_argument("--device", default="cuda")
     return ap.parse_args()
+
+
+def build(a, cfg, dev, dtype, world):
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.models.llama import LlamaForCausalLM, RMSNorm
+    from gke_ray_train_amd.ops import FusedAdamW
+    if a.parallel == "fsdp":
+        from gke_ray_train_amd.parallel.fsdp import FullyShardedDataParallel
+        std = cfg.initializer_range
+        model = LlamaForCausalLM(cfg, device="meta", dtype=dtype)
+
+        def init(m):
+            with torch.no_grad():
+                if isinstance(m, (torch.nn.Linear, torch.nn.Embedding)):
+                    m.weight.normal_(0.0, std)
+                elif isinstance(m, RMSNorm):
+                    m.weight.fill_(1.0)
+        if a.checkpointing:
+            model.gradient_checkpointing_enable()
+        eng = FullyShardedDataParallel(model, param_init_fn=init, device=dev, cpu_offload=a.offload)
+        opt = eng.build_optimizer(lr=a.lr)
+        return model, eng, eng, opt
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    model = build_llama(cfg, device=dev, dtype=dtype, seed=1234)
+    if a.checkpointing:
+        model.gradient_checkpointing_enable()
+    fwd = model
+    if a.peft != "none":
+        from gke_ray_train_amd.peft import BitsAndBytesConfig, LoraConfig, get_peft_model, quantize_model_
+        if a.peft == "qlora":
+            quantize_model_(model, BitsAndBytesConfig(bnb_4bit_compute_dtype=dtype))
+        fwd = get_peft_model(model, LoraConfig(r=a.lora_r, lora_alpha=16, lora_dropout=0.1))
+    eng = DistributedDataParallel(fwd, bucket_cap_mb=a.bucket_mb or None)
+    opt = FusedAdamW(eng.optimizer_param_groups(weight_decay=0.0), lr=a.lr)
+    return fwd, eng, fwd, opt
 
 
 def main():
@@ -61,43 +104,57 @@ def main():
     if world > 1:
         dist.init_process_group("gloo" if cpu else "nccl", device_id=None if cpu else dev)
 
-    from gke_ray_train_amd.models import build_llama, get_config
-    from gke_ray_train_amd.parallel import DistributedDataParallel
-    from gke_ray_train_amd.ops import FusedAdamW, clip_grad_norm_
+    from gke_ray_train_amd.data import TokenBatchLoader, synthetic_tokens
+    from gke_ray_train_amd.models import get_config
+    from gke_ray_train_amd.ops import clip_grad_norm_
 
     torch.manual_seed(1234)
     dtype = torch.float32 if cpu else torch.bfloat16
     cfg = get_config(a.model)
-    model = build_llama(cfg, device=dev, dtype=dtype, seed=1234)
-    if a.checkpointing:
-        model.gradient_checkpointing_enable()
+    model, eng, call, opt = build(a, cfg, dev, dtype, world)
     model.train()
-    ddp = DistributedDataParallel(model, bucket_cap_mb=a.bucket_mb or None)
-    opt = FusedAdamW(ddp.optimizer_param_groups(weight_decay=0.0), lr=a.lr, betas=(0.9, 0.999), eps=1e-8)
 
     mb = a.micro_batch or a.batch
     assert a.batch % mb == 0
     accum = a.batch // mb
-    g = torch.Generator(device=dev)
-    g.manual_seed(rank + 17)
-    # synthetic Wikitext-2-shaped batches (pre-generated, fixed shapes; random token ids)
-    nbuf = 4
-    batches = [torch.randint(0, cfg.vocab_size, (mb, a.seq), device=dev, generator=g) for _ in range(nbuf * accum)]
+    total_micro = (a.warmup + a.steps) * accum
+    if a.data == "loader":
+        toks = synthetic_tokens(max(total_micro * mb * a.seq * world + a.seq + 2, 1 << 20), cfg.vocab_size, seed=7)
+        loader = TokenBatchLoader(toks, a.seq, mb, device=dev, rank=rank, world=world, shuffle=True, seed=3,
+                                  stride=a.seq)
+        it = iter(loader)
 
-    def step(i):
+        def next_batch(_i):
+            return next(it)[0]
+    else:
+        g = torch.Generator(device=dev)
+        g.manual_seed(rank + 17)
+        batches = [torch.randint(0, cfg.vocab_size, (mb, a.seq), device=dev, generator=g) for _ in range(4 * accum)]
+
+        def next_batch(i):
+            return batches[i % len(batches)]
+
+    fsdp = a.parallel == "fsdp"
+    counter = [0]
+
+    def step():
         for j in range(accum):
-            ids = batches[(i * accum + j) % len(batches)]
-            with ddp.no_sync(j < accum - 1):
-                loss = model(ids, labels=ids)["loss"] / accum
+            ids = next_batch(counter[0])
+            counter[0] += 1
+            with eng.no_sync(j < accum - 1):
+                loss = call(ids, labels=ids)["loss"] / accum
                 loss.backward()
-        ddp.finish_gradient_sync()
-        st = clip_grad_norm_(ddp.grad_buffers(), a.max_grad_norm, prescale=1.0 / ddp.world_size)
+        eng.finish_gradient_sync()
+        if fsdp:
+            st = eng.clip_grad_norm_(a.max_grad_norm)
+        else:
+            st = clip_grad_norm_(eng.grad_buffers(), a.max_grad_norm, prescale=1.0 / eng.world_size)
         opt.step(grad_scale=st)
-        ddp.zero_grad()
+        eng.zero_grad()
         return loss
 
-    for i in range(a.warmup):
-        loss = step(i)
+    for _ in range(a.warmup):
+        loss = step()
     if not cpu:
         torch.cuda.synchronize()
     if world > 1:
@@ -110,8 +167,8 @@ def main():
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
         prof.__enter__()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        loss = step(a.warmup + i)
+    for _ in range(a.steps):
+        loss = step()
     if not cpu:
         torch.cuda.synchronize()
     if world > 1:
@@ -134,7 +191,11 @@ def main():
     tokens_per_step = a.batch * a.seq * world
     tps = tokens_per_step / (elapsed / a.steps)
     fpt = cfg.flops_per_token(a.seq)
+    if a.peft != "none":
+        fpt = fpt * 2.0 / 3.0  # frozen base: no weight-gradient GEMMs (adapter FLOPs are negligible)
     mfu = tps / world * fpt / 2.5e15
+    par = f"{'fsdp' if fsdp else 'dp'}{world}" + ("+offload" if a.offload else "") + \
+        ("" if a.peft == "none" else f"+{a.peft}")
     if rank == 0:
         out = {
             "metric": "tokens/sec (whole node) Llama-2-7B fine-tune",
@@ -148,10 +209,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if not cpu else "fp32",
-            "data": "synthetic (random token ids, Wikitext-2-shaped; random-init weights)",
-            "config": {"model": cfg.name, "global_batch": a.batch * world, "seq_len": a.seq,
-                       "parallelism": f"dp{world}", "micro_batch": mb, "grad_accum": accum,
-                       "optimizer": "fused AdamW fp32 states", "max_grad_norm": a.max_grad_norm},
+            "data": "synthetic Wikitext-2-shaped token stream (Zipf ids) via the streaming loader; random-init weights",
+            "config": {"model": cfg.name, "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": par,
+                       "micro_batch": mb, "grad_accum": accum, "optimizer": "fused AdamW fp32 states",
+                       "max_grad_norm": a.max_grad_norm, "activation_checkpointing": a.checkpointing},
             "samples_per_sec": round(tps / a.seq, 2),
             "mfu_bf16_dense": round(mfu, 4),
             "loss": round(float(loss.item()) * accum, 4),

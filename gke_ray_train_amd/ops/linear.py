@@ -19,12 +19,19 @@ import torch.nn.functional as F
 
 
 class GradSlot:
-    __slots__ = ("view", "fresh", "notify")
+    """A parameter's slot in a flat gradient buffer.
+
+    ``direct`` marks that the backward GEMM wrote this step's contribution itself. Torch still
+    fires the parameter's post-accumulate-grad hook for that input (with no gradient), so the
+    engines' hooks consume the flag and skip that event instead of counting the parameter twice.
+    """
+    __slots__ = ("view", "fresh", "notify", "direct")
 
     def __init__(self, view: torch.Tensor, notify):
         self.view = view
         self.fresh = True
         self.notify = notify
+        self.direct = False
 
     def write(self, fn_out, fn_acc):
         if self.fresh:
@@ -32,6 +39,13 @@ class GradSlot:
             self.fresh = False
         else:
             fn_acc(self.view)
+        self.direct = True
+
+    def consume_direct(self) -> bool:
+        if self.direct:
+            self.direct = False
+            return True
+        return False
 
 
 class _DirectGradLinear(torch.autograd.Function):

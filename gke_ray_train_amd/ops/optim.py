@@ -142,9 +142,93 @@ class FusedAdamW(torch.optim.Optimizer):
         return loss
 
 
+class OffloadedAdamW(FusedAdamW):
+    """AdamW whose fp32 moments live in pinned HOST memory and stream through the GPU kernel.
+
+    For FSDP + CPU offload (BASELINE config #5): per step each chunk of (m, v) is copied H2D on a
+    side stream, updated by the same fused HIP AdamW kernel together with the HBM-resident
+    parameter / gradient shard, and copied back D2H, with chunk i+1's upload and chunk i-1's
+    download overlapping chunk i's update (two device staging slots). HBM holds only
+    2 x chunk x 8 bytes of optimizer state instead of 8 bytes per parameter.
+    """
+
+    def __init__(self, params, chunk_elems: int = 1 << 26, **kw):
+        super().__init__(params, **kw)
+        self.chunk = int(chunk_elems)
+        self._stage = None
+        self._copy_stream = None
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: Optional[GradClipState] = None):
+        for gi, group in enumerate(self.param_groups):
+            lr = group["lr"]
+            b1, b2 = group["betas"]
+            eps, wd = group["eps"], group["weight_decay"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if not p.is_cuda:
+                    raise RuntimeError("OffloadedAdamW streams states to a GPU parameter")
+                st = self.state[p]
+                n = p.numel()
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros(n, dtype=torch.float32).pin_memory()
+                    st["exp_avg_sq"] = torch.zeros(n, dtype=torch.float32).pin_memory()
+                st["step"] += 1
+                step = float(st["step"])
+                hb = self._hyper_buf(p.device, (gi,))
+                hb.copy_(torch.tensor([lr, b1, b2, eps, wd, 1.0 - b1 ** step, 1.0 - b2 ** step, 1.0]), non_blocking=True)
+                self._stream_update(p, st, hb, grad_scale)
+
+    def _stream_update(self, p, st, hb, grad_scale):
+        C = _native.kernels()
+        dev = p.device
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(dev)
+            self._stage = [(torch.empty(self.chunk, device=dev), torch.empty(self.chunk, device=dev)) for _ in range(2)]
+        cs, comp = self._copy_stream, torch.cuda.current_stream(dev)
+        pf, gf = p.data.view(-1), p.grad.view(-1)
+        m_h, v_h = st["exp_avg"], st["exp_avg_sq"]
+        n = pf.numel()
+        chunks = [(s, min(n, s + self.chunk)) for s in range(0, n, self.chunk)]
+        up_done = [torch.cuda.Event() for _ in chunks]
+        upd_done = [torch.cuda.Event() for _ in chunks]
+
+        def upload(i):
+            s, e = chunks[i]
+            mb, vb = self._stage[i % 2]
+            with torch.cuda.stream(cs):
+                if i >= 2:
+                    cs.wait_event(upd_done[i - 2])  # slot reuse: previous user's update done
+                mb[: e - s].copy_(m_h[s:e], non_blocking=True)
+                vb[: e - s].copy_(v_h[s:e], non_blocking=True)
+                up_done[i].record(cs)
+
+        if chunks:
+            upload(0)
+        for i, (s, e) in enumerate(chunks):
+            if i + 1 < len(chunks):
+                upload(i + 1)
+            comp.wait_event(up_done[i])
+            mb, vb = self._stage[i % 2]
+            C.adamw(pf[s:e], gf[s:e], mb[: e - s], vb[: e - s], None, hb,
+                    None if grad_scale is None else grad_scale.buf)
+            upd_done[i].record(comp)
+            with torch.cuda.stream(cs):
+                cs.wait_event(upd_done[i])
+                m_h[s:e].copy_(mb[: e - s], non_blocking=True)
+                v_h[s:e].copy_(vb[: e - s], non_blocking=True)
+        comp.wait_stream(cs)
+
+
 def make_optimizer(name: str, params, lr: float, weight_decay: float, betas=(0.9, 0.999), eps=1e-8,
-                   master_weights=False):
+                   master_weights=False, offload: bool = False):
+    """Optimizer by HF ``optim`` name. ``offload=True`` keeps AdamW moments in pinned host memory
+    (OffloadedAdamW) — only worthwhile when HBM cannot hold them (e.g. 70B on one node)."""
     name = (name or "adamw_torch").lower()
+    if offload and name.startswith(("adamw", "paged_adamw", "fused_adamw")):
+        return OffloadedAdamW(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
     if name in ("adamw", "adamw_torch", "adamw_hf", "adamw_32bit", "paged_adamw_32bit", "adamw_torch_fused",
                 "fused_adamw", "paged_adamw_8bit", "adamw_8bit"):
         return FusedAdamW(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,

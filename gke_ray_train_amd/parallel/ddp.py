@@ -165,6 +165,8 @@ class DistributedDataParallel(nn.Module):
         def hook(p):
             # AccumulateGrad path (params not written by a direct-grad GEMM, or CPU fallbacks)
             sl = self._slots[p]
+            if sl.consume_direct():  # the GEMM already wrote and announced this gradient
+                return
             view = sl.view
             if p.grad is not view and p.grad.data_ptr() != view.data_ptr():
                 with torch.no_grad():
@@ -186,6 +188,8 @@ class DistributedDataParallel(nn.Module):
         if not self._sync or self.world_size == 1:
             return
         b.ready += 1
+        if b.ready > len(b.params):  # a parameter announced twice would launch a bucket early
+            raise RuntimeError("DDP bucket readiness over-counted (gradient announced twice)")
         if b.ready == len(b.params):
             self._launch(g, b)
 

@@ -1,0 +1,519 @@
+"""Fully-sharded data parallelism (ZeRO-3 style) over RCCL, with optional optimizer-state offload.
+
+Not in the reference (its only strategy is DDP); required by BASELINE.json configs #3 (Llama-2-7B
+FSDP full-shard bf16) and #5 (Llama-3-70B FSDP full-shard + CPU offload). SURVEY §2.4, §7.5.
+
+Design for 8 x MI355X on xGMI:
+* a *unit* = one transformer block (``LlamaDecoderLayer`` / ``EncoderLayer``) plus a root unit
+  (embeddings, LM head). Each unit's weight MATRICES live as one padded flat bf16 buffer split
+  into ``world`` contiguous shards; rank r keeps shard r in a single rank-local shard store, so
+  the optimizer updates all of a rank's parameters with ONE fused AdamW launch;
+* 1-D parameters (norm weights, biases: <0.01 % of a Llama) are replicated and all-reduced once
+  per step (no per-layer latency-bound micro-collectives, no weight decay on them — HF rule);
+* forward: a unit's all-gather (``all_gather_into_tensor`` = one RCCL collective per unit,
+  ~400 MB for a 7B block at 8 ranks, well into the multi-ring bandwidth regime) is issued one
+  unit AHEAD on RCCL's stream while the current unit computes; after the unit runs, its full
+  buffer is released (``reshard_after_forward``);
+* backward: an identity autograd node on each unit's output re-gathers the unit (prefetching the
+  previous one) right before its backward kernels; weight gradients are written by the GEMMs
+  straight into the unit's full gradient buffer (ops/linear.py slots), and when the last one
+  lands the buffer is reduce-scattered (SUM; the 1/world average is folded into the optimizer)
+  into this rank's gradient shard and freed;
+* ``cpu_offload=True``: fp32 Adam moments live in pinned host memory and are streamed through the
+  GPU AdamW kernel in chunks on a side stream (H2D of chunk i+1 / D2H of chunk i-1 overlap the
+  update of chunk i); parameters and gradients stay in HBM.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..ops.linear import GradSlot
+
+DEFAULT_UNITS = ("LlamaDecoderLayer", "EncoderLayer")
+_ALIGN = 64
+
+
+class _BwdGather(torch.autograd.Function):
+    """Identity on a unit's output; its backward fires right before the unit's backward kernels."""
+
+    @staticmethod
+    def forward(ctx, fsdp, unit, *xs):
+        ctx.fsdp, ctx.unit = fsdp, unit
+        return xs if len(xs) > 1 else xs[0]
+
+    @staticmethod
+    def backward(ctx, *gs):
+        ctx.fsdp._pre_backward(ctx.unit)
+        return (None, None) + gs
+
+
+class _Unit:
+    def __init__(self, idx, module, items, world):
+        self.idx = idx
+        self.module = module
+        self.params = [p for _, p in items]
+        self.names = [n for n, _ in items]
+        self.shapes = [p.shape for p in self.params]
+        self.numels = [p.numel() for p in self.params]
+        self.offsets = []
+        off = 0
+        for n in self.numels:
+            self.offsets.append(off)
+            off += (n + _ALIGN - 1) // _ALIGN * _ALIGN
+        per = (off + world - 1) // world
+        per = (per + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.shard_numel = per
+        self.total = per * world
+        self.full: Optional[torch.Tensor] = None
+        self.gather_work = None
+        self.grad_full: Optional[torch.Tensor] = None
+        self.ready = 0
+        self.rs_work = None
+        self.rs_out: Optional[torch.Tensor] = None
+        self.in_backward = False
+        self.slots: Dict[int, GradSlot] = {}
+
+
+class FullyShardedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, process_group=None, unit_types=DEFAULT_UNITS, reshard_after_forward=True,
+                 cpu_offload: bool = False, sync_module_states: bool = True, param_init_fn=None, device=None,
+                 offload_chunk_elems: int = 1 << 26):
+        super().__init__()
+        self.module = module
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        self.reshard_after_forward = reshard_after_forward
+        self.cpu_offload = cpu_offload
+        self.offload_chunk = offload_chunk_elems
+        self._sync = True
+        self.gloo = dist.is_initialized() and dist.get_backend(process_group) == "gloo"
+        first = next(module.parameters())
+        self.device = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if first.device.type == "meta" else first.device)
+        # ---------------------------------------------------------------- partition parameters
+        unit_mods = [m for m in module.modules() if type(m).__name__ in unit_types]
+        owner = {}
+        for ui, m in enumerate(unit_mods):
+            for n, p in m.named_parameters():
+                owner.setdefault(id(p), ui)
+        seen = set()
+        per_unit: List[List[tuple]] = [[] for _ in range(len(unit_mods) + 1)]
+        self.replicated: List[tuple] = []
+        for n, p in module.named_parameters():
+            if id(p) in seen or not p.requires_grad:
+                continue
+            seen.add(id(p))
+            if p.dim() < 2:
+                self.replicated.append((n, p))
+            else:
+                per_unit[owner.get(id(p), len(unit_mods))].append((n, p))
+        mods = unit_mods + [module]
+        self.units = [_Unit(i, mods[i], items, self.world) for i, items in enumerate(per_unit) if items]
+        self.dtype = next((p.dtype for u in self.units for p in u.params), torch.bfloat16)
+        if self.dtype == torch.float32 and first.device.type != "meta":
+            self.dtype = first.dtype
+        # ---------------------------------------------------------------- shard stores
+        self._replaced = {}
+        tot = sum(u.shard_numel for u in self.units)
+        self.shard_store = torch.zeros(tot, dtype=self.dtype, device=self.device)
+        self.grad_store = torch.zeros(tot, dtype=self.dtype, device=self.device)
+        off = 0
+        for u in self.units:
+            u.shard = self.shard_store[off:off + u.shard_numel]
+            u.shard_grad = self.grad_store[off:off + u.shard_numel]
+            off += u.shard_numel
+            self._materialize_and_shard(u, param_init_fn, sync_module_states)
+        # replicated (1-D) params: one flat buffer, all-reduced once per step
+        self.replicated = [(n, self._replaced.get(id(p), p)) for n, p in self.replicated]
+        for m in module.modules():
+            own = [(n, p) for n, p in m.named_parameters(recurse=False) if p.device.type == "meta"]
+            for n, p in own:
+                newp = nn.Parameter(torch.empty(p.shape, dtype=self.dtype, device=self.device),
+                                    requires_grad=p.requires_grad)
+                setattr(m, n, newp)
+                self._replaced[id(p)] = newp
+            if own and param_init_fn is not None:
+                param_init_fn(m)
+        self.replicated = [(n, self._replaced.get(id(p), p)) for n, p in self.replicated]
+        rn = sum(p.numel() for _, p in self.replicated)
+        self.rep_flat = torch.zeros(max(rn, 1), dtype=self.dtype, device=self.device)
+        self.rep_grad = torch.zeros(max(rn, 1), dtype=self.dtype, device=self.device)
+        o = 0
+        with torch.no_grad():
+            for _, p in self.replicated:
+                self.rep_flat[o:o + p.numel()].copy_(p.data.view(-1))
+                p.data = self.rep_flat[o:o + p.numel()].view_as(p)
+                p.grad = self.rep_grad[o:o + p.numel()].view_as(p)
+                o += p.numel()
+        if sync_module_states and self.world > 1 and rn:
+            dist.broadcast(self.rep_flat, 0, group=process_group)
+        self._rep_hooks = [p.register_post_accumulate_grad_hook(self._rep_hook) for _, p in self.replicated]
+        self._rep_fresh = True
+        # ---------------------------------------------------------------- hooks
+        self._order: List[_Unit] = []
+        for u in self.units:
+            self._attach_slots(u)
+        for u in self.units:
+            if u.module is not module:
+                u.module.register_forward_pre_hook(self._make_pre_fwd(u))
+                u.module.register_forward_hook(self._make_post_fwd(u))
+        self._root_unit = next((u for u in self.units if u.module is module), None)
+        self._offload_state = None
+
+    # ================================================================ sharding helpers
+    @torch.no_grad()
+    def _materialize_and_shard(self, u: _Unit, init_fn, sync):
+        if any(p.device.type == "meta" for p in u.params):
+            ids = {id(p) for p in u.params}
+            mods = list(u.module.modules()) if u.module is not self.module else list(self.module.modules())
+            repl = {}
+            for m in mods:
+                own = [(n, p) for n, p in m.named_parameters(recurse=False) if id(p) in ids or
+                       (u.module is not self.module and p.device.type == "meta")]
+                if not own:
+                    continue
+                for n, p in own:
+                    newp = nn.Parameter(torch.empty(p.shape, dtype=self.dtype, device=self.device),
+                                        requires_grad=p.requires_grad)
+                    setattr(m, n, newp)
+                    repl[id(p)] = newp
+                if init_fn is not None:
+                    init_fn(m)
+            u.params = [repl.get(id(p), p) for p in u.params]
+            self._replaced.update(repl)
+        full = torch.zeros(u.total, dtype=self.dtype, device=self.device)
+        for p, o, n in zip(u.params, u.offsets, u.numels):
+            full[o:o + n].copy_(p.data.reshape(-1))
+        if sync and self.world > 1:
+            dist.broadcast(full, 0, group=self.pg)
+        u.shard.copy_(full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel])
+        if self.world == 1:
+            self._bind(u, u.shard)  # single rank: the shard IS the full buffer, never freed
+        else:
+            self._unbind(u)
+        del full
+
+    def _bind(self, u: _Unit, full: torch.Tensor):
+        u.full = full
+        for p, o, n, s in zip(u.params, u.offsets, u.numels, u.shapes):
+            p.data = full[o:o + n].view(s)
+
+    def _unbind(self, u: _Unit):
+        if self.world == 1:
+            return
+        u.full = None
+        for p in u.params:
+            p.data = torch.empty(0, dtype=self.dtype, device=self.device)
+
+    # ================================================================ all-gather
+    def _issue_gather(self, u: _Unit):
+        if u.full is not None or u.gather_work is not None or self.world == 1:
+            return
+        buf = torch.empty(u.total, dtype=self.dtype, device=self.device)
+        if self.gloo:
+            parts = list(buf.chunk(self.world))
+            u.gather_work = dist.all_gather(parts, u.shard, group=self.pg, async_op=True)
+        else:
+            u.gather_work = dist.all_gather_into_tensor(buf, u.shard, group=self.pg, async_op=True)
+        u._pending_buf = buf
+
+    def _wait_gather(self, u: _Unit):
+        if self.world == 1:
+            return
+        if u.full is None and u.gather_work is None:
+            self._issue_gather(u)
+        if u.gather_work is not None:
+            u.gather_work.wait()
+            u.gather_work = None
+            self._bind(u, u._pending_buf)
+            u._pending_buf = None
+
+    def _next(self, u: _Unit, step: int) -> Optional[_Unit]:
+        seq = [x for x in self.units if x.module is not self.module]
+        if u.module is self.module or u not in seq:
+            return None
+        i = seq.index(u) + step
+        return seq[i] if 0 <= i < len(seq) else None
+
+    def _make_pre_fwd(self, u: _Unit):
+        def hook(mod, args):
+            self._wait_gather(u)
+            nxt = self._next(u, +1)
+            if nxt is not None and not u.in_backward:
+                self._issue_gather(nxt)
+        return hook
+
+    def _make_post_fwd(self, u: _Unit):
+        def hook(mod, args, out):
+            if torch.is_grad_enabled() and self.module.training:
+                if not u.in_backward:
+                    if self.reshard_after_forward:
+                        self._unbind(u)
+                    tensors = out if isinstance(out, tuple) else (out,)
+                    idx = [i for i, t in enumerate(tensors) if isinstance(t, torch.Tensor) and t.requires_grad]
+                    if idx:
+                        wrapped = _BwdGather.apply(self, u, *[tensors[i] for i in idx])
+                        wrapped = wrapped if isinstance(wrapped, tuple) else (wrapped,)
+                        lst = list(tensors)
+                        for i, w in zip(idx, wrapped):
+                            lst[i] = w
+                        return tuple(lst) if isinstance(out, tuple) else lst[0]
+            elif self.reshard_after_forward and not u.in_backward:
+                self._unbind(u)
+            return out
+        return hook
+
+    # ================================================================ backward
+    def _pre_backward(self, u: _Unit):
+        u.in_backward = True
+        self._wait_gather(u)
+        prev = self._next(u, -1)
+        if prev is not None:
+            self._issue_gather(prev)
+        self._alloc_grads(u)
+
+    def _alloc_grads(self, u: _Unit):
+        if u.grad_full is not None:
+            return
+        g = torch.empty(u.total, dtype=self.dtype, device=self.device)
+        g.zero_()  # alignment gaps must not inject garbage into the reduction
+        u.grad_full = g
+        u.ready = 0
+        for p, o, n, s in zip(u.params, u.offsets, u.numels, u.shapes):
+            sl = u.slots[id(p)]
+            sl.view = g[o:o + n].view(s)
+            sl.fresh = True
+            p.grad = None
+
+    def _attach_slots(self, u: _Unit):
+        # Slots exist from construction on, so the forward takes the same (direct-grad) code path
+        # in the original pass and in an activation-checkpoint recompute.
+        for p in u.params:
+            sl = GradSlot(torch.empty(0, dtype=self.dtype, device=self.device), self._param_ready)
+            p._grt_slot = sl
+            p._grt_unit = u
+            u.slots[id(p)] = sl
+            p._grt_fsdp_hook = p.register_post_accumulate_grad_hook(self._acc_hook)
+
+    def _acc_hook(self, p):
+        # AccumulateGrad path (params not written by a direct-grad GEMM): fold into the slot
+        u = getattr(p, "_grt_unit", None)
+        if u is None:
+            return
+        sl = u.slots[id(p)]
+        if sl.consume_direct():  # the GEMM already wrote and announced this gradient
+            return
+        if p.grad is not None and p.grad.data_ptr() != sl.view.data_ptr():
+            with torch.no_grad():
+                sl.view.copy_(p.grad) if sl.fresh else sl.view.add_(p.grad)
+        sl.fresh = False
+        p.grad = None
+        self._param_ready(p)
+
+    def _param_ready(self, p):
+        u = p._grt_unit
+        sl = u.slots[id(p)]
+        sl.fresh = False
+        p.grad = None
+        u.ready += 1
+        if u.ready == len(u.params):
+            self._reduce_scatter(u)
+
+    def _reduce_scatter(self, u: _Unit):
+        g = u.grad_full
+        if self.world == 1:
+            if self._accumulating(u):
+                u.shard_grad.add_(g)
+            else:
+                u.shard_grad.copy_(g)
+        else:
+            if self.gloo:
+                dist.all_reduce(g, group=self.pg)
+                part = g[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel]
+                if self._accumulating(u):
+                    u.shard_grad.add_(part)
+                else:
+                    u.shard_grad.copy_(part)
+            else:
+                out = u.shard_grad if not self._accumulating(u) else torch.empty_like(u.shard_grad)
+                u.rs_work = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+                u.rs_out = out if out is not u.shard_grad else None
+                u._rs_src = g
+        u.grad_full = None
+        u.in_backward = False
+        u.ready = 0
+        u.acc_started = True
+        if u.module is not self.module:
+            self._unbind(u)
+
+    def _accumulating(self, u):
+        return getattr(u, "acc_started", False)
+
+    # ================================================================ replicated params
+    def _rep_hook(self, p):
+        pass
+
+    # ================================================================ public API
+    @contextlib.contextmanager
+    def no_sync(self, enabled: bool = True):
+        prev = self._sync
+        self._sync = not enabled
+        try:
+            yield
+        finally:
+            self._sync = prev
+
+    def forward(self, *args, **kwargs):
+        if self._root_unit is not None:
+            self._wait_gather(self._root_unit)
+            if self.module.training and torch.is_grad_enabled():
+                self._alloc_grads(self._root_unit)
+        first = next((x for x in self.units if x.module is not self.module), None)
+        if first is not None:
+            self._issue_gather(first)
+        return self.module(*args, **kwargs)
+
+    def finish_gradient_sync(self):
+        """Complete reduce-scatters and the replicated-param all-reduce of this step."""
+        for u in self.units:
+            if u.grad_full is not None:  # unit whose grads never all arrived (unused params)
+                for p in u.params:
+                    sl = u.slots[id(p)]
+                    if sl.fresh:
+                        sl.view.zero_()
+                        sl.fresh = False
+                u.ready = len(u.params) - 1
+                self._param_ready(u.params[-1]) if u.params else None
+        for u in self.units:
+            if u.rs_work is not None:
+                u.rs_work.wait()
+                u.rs_work = None
+                if u.rs_out is not None:
+                    u.shard_grad.add_(u.rs_out)
+                    u.rs_out = None
+                u._rs_src = None
+        if self.world > 1 and self.replicated and self._sync:
+            dist.all_reduce(self.rep_grad, group=self.pg)
+        if self._root_unit is not None and self.world > 1:
+            self._unbind(self._root_unit)
+
+    def zero_grad(self, set_to_none: bool = True):
+        for u in self.units:
+            u.acc_started = False
+        self.grad_store.zero_()
+        self.rep_grad.zero_()
+        o = 0
+        for _, p in self.replicated:  # a caller may have set .grad = None: re-attach the views
+            p.grad = self.rep_grad[o:o + p.numel()].view_as(p)
+            o += p.numel()
+
+    def grad_buffers(self) -> List[torch.Tensor]:
+        """Gradient shards (the global norm is completed by an all-reduce inside clip_grad_norm_)."""
+        return [self.grad_store, self.rep_grad]
+
+    @property
+    def world_size(self) -> int:
+        return self.world
+
+    def build_optimizer(self, lr: float, weight_decay: float = 0.0, betas=(0.9, 0.999), eps=1e-8):
+        """Fused AdamW over this rank's shards; with ``cpu_offload`` the moments live in pinned host
+        memory and stream through the GPU kernel (ops.optim.OffloadedAdamW)."""
+        from ..ops.optim import FusedAdamW, OffloadedAdamW
+        groups = self.optimizer_param_groups(weight_decay)
+        if self.cpu_offload and self.device.type == "cuda":
+            return OffloadedAdamW(groups, chunk_elems=self.offload_chunk, lr=lr, betas=betas, eps=eps)
+        return FusedAdamW(groups, lr=lr, betas=betas, eps=eps)
+
+    def optimizer_param_groups(self, weight_decay: float = 0.0):
+        sp = nn.Parameter(self.shard_store, requires_grad=False)
+        sp.grad = self.grad_store
+        rp = nn.Parameter(self.rep_flat, requires_grad=False)
+        rp.grad = self.rep_grad
+        return [{"params": [sp], "weight_decay": weight_decay}, {"params": [rp], "weight_decay": 0.0}]
+
+    def clip_grad_norm_(self, max_norm: float):
+        """Global grad norm over shards (sum of squares all-reduced), average folded in."""
+        from ..ops import clip_grad_norm_ as _clip
+        st = _clip([self.grad_store], 0.0, prescale=1.0)
+        ss_shard = st.buf[0] ** 2
+        st2 = _clip([self.rep_grad], 0.0, prescale=1.0)
+        ss_rep = st2.buf[0] ** 2
+        if self.world > 1:
+            dist.all_reduce(ss_shard, group=self.pg)
+        total = (ss_shard + ss_rep).sqrt() / self.world
+        coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(total)
+        st.buf[0] = total
+        st.buf[1] = coef / self.world
+        return st
+
+    @torch.no_grad()
+    def full_state_dict(self) -> Dict[str, torch.Tensor]:
+        """Gathered (unsharded) state dict on every rank, module parameter names."""
+        out = {}
+        for u in self.units:
+            self._wait_gather(u)
+            for n, p in zip(u.names, u.params):
+                out[n] = p.detach().clone()
+            if u.module is not self.module or self.world > 1:
+                self._unbind(u)
+        for n, p in self.replicated:
+            out[n] = p.detach().clone()
+        for n, b in self.module.named_buffers():
+            out[n] = b.detach().clone()
+        return out
+
+    @torch.no_grad()
+    def full_grad_dict(self) -> Dict[str, torch.Tensor]:
+        """Unsharded gradients (sum over ranks), module parameter names — tests / debugging."""
+        out = {}
+        for u in self.units:
+            if self.world > 1:
+                parts = [torch.empty_like(u.shard_grad) for _ in range(self.world)]
+                dist.all_gather(parts, u.shard_grad.contiguous(), group=self.pg)
+                full = torch.cat(parts)
+            else:
+                full = u.shard_grad
+            for n, o, k, s in zip(u.names, u.offsets, u.numels, u.shapes):
+                out[n] = full[o:o + k].view(s).clone()
+        o = 0
+        for n, p in self.replicated:
+            out[n] = self.rep_grad[o:o + p.numel()].view_as(p).clone()
+            o += p.numel()
+        return out
+
+    @torch.no_grad()
+    def load_full_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True):
+        """Load an unsharded state dict (module names): every rank keeps only its own shard."""
+        missing = []
+        for u in self.units:
+            full = torch.zeros(u.total, dtype=self.dtype, device=self.device)
+            for n, o, k in zip(u.names, u.offsets, u.numels):
+                if n in sd:
+                    full[o:o + k].copy_(sd[n].reshape(-1))
+                else:
+                    missing.append(n)
+            u.shard.copy_(full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel])
+        for n, p in self.replicated:
+            if n in sd:
+                p.data.copy_(sd[n].view_as(p))
+            else:
+                missing.append(n)
+        if strict and missing:
+            raise KeyError(f"missing keys in state dict: {missing[:8]}")
+
+    def sharded_state_dict(self) -> Dict[str, torch.Tensor]:
+        return {"shard_store": self.shard_store.detach().clone(), "rep_flat": self.rep_flat.detach().clone(),
+                "rank": torch.tensor(self.rank), "world": torch.tensor(self.world)}
+
+    @torch.no_grad()
+    def load_sharded_state_dict(self, sd):
+        assert int(sd["world"]) == self.world and int(sd["rank"]) == self.rank, "resharding is not supported"
+        self.shard_store.copy_(sd["shard_store"])
+        self.rep_flat.copy_(sd["rep_flat"])
