@@ -438,6 +438,10 @@ def _count_gpus() -> int:
     env = os.environ.get("GRT_NUM_GPUS")
     if env is not None:
         return int(env)
+    from ..cluster.head import read_current_cluster
+    cur = read_current_cluster()  # a `grt start --head` cluster caps the GPUs this driver may use
+    if cur is not None and cur.get("num_gpus") is not None:
+        return int(cur["num_gpus"])
     try:
         import torch
         return torch.cuda.device_count()

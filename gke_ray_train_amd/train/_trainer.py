@@ -117,7 +117,7 @@ class DataParallelTrainer:
         b = getattr(self.backend_config, "backend", None)
         if b is None:
             import torch
-            b = "nccl" if (self.scaling.use_gpu and torch.cuda.is_available()) else "gloo"
+            b = "nccl" if (self.scaling.use_gpu and torch.cuda.device_count() > 0) else "gloo"
         return b
 
     def fit(self) -> Result:

@@ -155,13 +155,17 @@ def load_config(path=None, overrides=None):
     with open(path) as f:
         cfg = json.load(f)
     cfg.update(overrides or {})
+    # the reference writes under its /mnt/pvc bucket mount: "pvc/..." resolves to the cluster storage
+    pvc = os.environ.get("GRT_PVC") or os.environ.get("GRT_STORAGE_PATH")
+    if pvc and str(cfg.get("OUTPUT_DIR_BASE", "")).startswith("pvc/"):
+        cfg["OUTPUT_DIR_BASE"] = os.path.join(pvc, cfg["OUTPUT_DIR_BASE"][4:])
     return cfg
 
 
 def main(config=None, num_workers=None, use_gpu=None):
     cfg = config or load_config()
     if use_gpu is None:
-        use_gpu = torch.cuda.is_available()
+        use_gpu = torch.cuda.device_count() > 0  # counting does not initialise HIP in the driver
     if num_workers is None:
         n_nodes = int(os.getenv("NUM_NODES", "1"))
         n_gpu = int(os.getenv("NUM_GPUS_PER_NODE", str(torch.cuda.device_count() if use_gpu else 1)))

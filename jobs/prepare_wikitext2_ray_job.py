@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from gke_ray_train_amd import runtime as rt  # noqa: E402
 
-PVC = os.environ.get("GRT_PVC", os.path.abspath("pvc"))
+PVC = os.environ.get("GRT_PVC") or os.environ.get("GRT_STORAGE_PATH") or os.path.abspath("pvc")
 
 
 @rt.remote(num_cpus=1)

@@ -29,7 +29,7 @@ from gke_ray_train_amd import train  # noqa: E402
 from gke_ray_train_amd.train import Checkpoint, CheckpointConfig, RunConfig, ScalingConfig  # noqa: E402
 from gke_ray_train_amd.train.torch import TorchConfig, TorchTrainer  # noqa: E402
 
-PVC = os.environ.get("GRT_PVC", os.path.abspath("pvc"))
+PVC = os.environ.get("GRT_PVC") or os.environ.get("GRT_STORAGE_PATH") or os.path.abspath("pvc")
 
 
 def warmup_cosine(total_steps: int, warmup_ratio: float, min_lr_ratio: float):
@@ -190,7 +190,7 @@ def main(argv=None):
     ap.add_argument("--data-scale", type=float, default=1.0)
     ap.add_argument("--max-windows", type=int, default=None, help="override test_run's 16,000-window subset")
     a = ap.parse_args(argv)
-    use_gpu = not a.cpu and torch.cuda.is_available()
+    use_gpu = not a.cpu and torch.cuda.device_count() > 0
     workers = a.workers or (torch.cuda.device_count() if use_gpu else 2)
     cfg = build_config(a)
     trainer = TorchTrainer(
