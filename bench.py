@@ -21,6 +21,7 @@ bench.py --gpus N``. Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -51,6 +52,8 @@ def parse():
     ap.add_argument("--checkpointing", action="store_true", help="activation checkpointing")
     ap.add_argument("--data", default="loader", choices=["loader", "static"])
     ap.add_argument("--profile-dir", default="", help="write a torch.profiler trace here")
+    ap.add_argument("--metrics-jsonl", default="", help="per-step metrics (phase breakdown, MFU, HBM) -> JSONL; "
+                    "adds one host sync per step, so it is off for the headline number")
     ap.add_argument("--device", default="cuda")
     return ap.parse_args()
 
@@ -136,21 +139,43 @@ def main():
 
     fsdp = a.parallel == "fsdp"
     counter = [0]
+    from gke_ray_train_amd.observability import StepMeter
+    meter = None
+    if a.metrics_jsonl:
+        fpt_m = cfg.flops_per_token(a.seq) * (2.0 / 3.0 if a.peft != "none" else 1.0)
+        meter = StepMeter(a.batch * a.seq * world, fpt_m, n_gpus=world, samples_per_step=a.batch * world,
+                          jsonl=a.metrics_jsonl, rank=rank, device=dev)
+    nullctx = contextlib.nullcontext
+
+    def ph(name):
+        return meter.phase(name) if meter is not None else nullctx()
 
     def step():
         for j in range(accum):
             ids = next_batch(counter[0])
             counter[0] += 1
             with eng.no_sync(j < accum - 1):
-                loss = call(ids, labels=ids)["loss"] / accum
-                loss.backward()
-        eng.finish_gradient_sync()
-        if fsdp:
-            st = eng.clip_grad_norm_(a.max_grad_norm)
-        else:
-            st = clip_grad_norm_(eng.grad_buffers(), a.max_grad_norm, prescale=1.0 / eng.world_size)
-        opt.step(grad_scale=st)
-        eng.zero_grad()
+                with ph("forward"):
+                    loss = call(ids, labels=ids)["loss"] / accum
+                with ph("backward"):
+                    loss.backward()
+        with ph("grad_sync"):
+            eng.finish_gradient_sync()
+        with ph("optimizer"):
+            if fsdp:
+                st = eng.clip_grad_norm_(a.max_grad_norm)
+            else:
+                st = clip_grad_norm_(eng.grad_buffers(), a.max_grad_norm, prescale=1.0 / eng.world_size)
+            opt.step(grad_scale=st)
+            eng.zero_grad()
+        return loss
+
+    def timed_step(i):
+        if meter is None:
+            return step()
+        with meter.step(i):
+            loss = step()
+        meter.log(i, loss=loss * accum)
         return loss
 
     for _ in range(a.warmup):
@@ -167,8 +192,8 @@ def main():
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
         prof.__enter__()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        loss = step()
+    for i in range(a.steps):
+        loss = timed_step(i)
     if not cpu:
         torch.cuda.synchronize()
     if world > 1:

@@ -32,6 +32,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from ..observability import roctx
+from ..observability.metrics import MI355X_PEAK_BF16_DENSE
 from ..ops import clip_grad_norm_, make_optimizer
 from ..parallel.ddp import DistributedDataParallel
 from .schedules import get_scheduler
@@ -129,6 +131,7 @@ class SFTTrainer:
             from ..peft import get_peft_model
             model = get_peft_model(model, peft_config)
         self.model = model
+        self.peft_config = peft_config
         if args.gradient_checkpointing:
             inner = getattr(model, "base_model", model)
             if hasattr(inner, "gradient_checkpointing_enable"):
@@ -221,6 +224,13 @@ class SFTTrainer:
         log_count = 0
         ntok = 0
         nsamples = 0
+        t_log, ntok_log = t0, 0
+        cfg = getattr(getattr(self.model, "base_model", self.model), "config", None)
+        fpt = 0.0
+        if cfg is not None and hasattr(cfg, "flops_per_token"):
+            fpt = cfg.flops_per_token(a.max_seq_length)
+            if self.peft_config is not None:
+                fpt *= 2.0 / 3.0  # frozen base weights: no weight-gradient GEMMs
         step = start_step
         epochs = math.ceil(total / steps_per_epoch)
         done = False
@@ -233,17 +243,21 @@ class SFTTrainer:
                 ntok += int(batches[mi]["attention_mask"].sum())  # CPU tensor: no device sync
                 b = self._to_dev(batches[mi])
                 with self.engine.no_sync(not boundary):
-                    out = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])
-                    loss = out["loss"] / accum
-                    loss.backward()
+                    with roctx.range("forward"):
+                        out = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])
+                        loss = out["loss"] / accum
+                    with roctx.range("backward"):
+                        loss.backward()
                 tr_loss_sum += loss.detach()
                 log_loss += loss.detach()
                 nsamples += b["input_ids"].shape[0]
                 if not boundary:
                     continue
-                self.engine.finish_gradient_sync()
-                st = clip_grad_norm_(self.engine.grad_buffers(), a.max_grad_norm, prescale=1.0 / self.world)
-                self.optimizer.step(grad_scale=st)
+                with roctx.range("grad_sync"):
+                    self.engine.finish_gradient_sync()
+                with roctx.range("optimizer"):
+                    st = clip_grad_norm_(self.engine.grad_buffers(), a.max_grad_norm, prescale=1.0 / self.world)
+                    self.optimizer.step(grad_scale=st)
                 self.scheduler.step()
                 self.engine.zero_grad()
                 step += 1
@@ -251,8 +265,15 @@ class SFTTrainer:
                 self.state["global_step"] = step
                 self.state["epoch"] = epoch + (mi + 1) / nb
                 if a.logging_steps and step % a.logging_steps == 0:
-                    self._log({"loss": self._mean_across_ranks(log_loss / log_count), "grad_norm": float(st.norm),
-                               "learning_rate": self.scheduler.get_last_lr()[0], "epoch": round(self.state["epoch"], 4)})
+                    logs = {"loss": self._mean_across_ranks(log_loss / log_count), "grad_norm": float(st.norm),
+                            "learning_rate": self.scheduler.get_last_lr()[0], "epoch": round(self.state["epoch"], 4)}
+                    now = time.time()  # the loss all-reduce above already synchronised the stream
+                    dt = max(now - t_log, 1e-9)
+                    logs["tokens_per_sec"] = round((ntok - ntok_log) * self.world / dt, 1)
+                    if fpt:
+                        logs["mfu"] = round((ntok - ntok_log) / dt * fpt / MI355X_PEAK_BF16_DENSE, 4)
+                    t_log, ntok_log = now, ntok
+                    self._log(logs)
                     log_loss.zero_()
                     log_count = 0
                 if a.eval_strategy == "steps" and self.eval_seqs and a.eval_steps and step % a.eval_steps == 0:
@@ -298,6 +319,9 @@ class SFTTrainer:
         self.state["log_history"].append(logs)
         if self.rank == 0:
             print({k: (round(v, 6) if isinstance(v, float) else v) for k, v in logs.items()}, flush=True)
+            os.makedirs(self.args.output_dir, exist_ok=True)
+            with open(os.path.join(self.args.output_dir, "metrics.jsonl"), "a") as f:
+                f.write(json.dumps(dict(logs, time=time.time())) + "\n")
             if self.tb is not None:
                 for k, v in logs.items():
                     if k not in ("step", "epoch") and isinstance(v, (int, float)):
