@@ -418,6 +418,28 @@ Tensor nf4_dequantize(const Tensor& q, const Tensor& absmax, int64_t n, int64_t 
   return w;
 }
 
+// ------------------------------------------------------------------ weight-gradient GEMM
+// out[P][Q] (+)= x[R][P]^T @ y[R][Q]  (dW = dY^T X); returns false when the shape is unsupported
+bool gemm_wgrad(const Tensor& x, const Tensor& y, const Tensor& out, bool accumulate, int64_t mode) {
+  TORCH_CHECK(x.dim() == 2 && y.dim() == 2 && out.dim() == 2, "gemm_wgrad: 2-D operands");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 &&
+                  out.scalar_type() == at::kBFloat16, "gemm_wgrad: bf16 operands");
+  TORCH_CHECK(x.is_cuda() && y.is_cuda() && out.is_cuda(), "gemm_wgrad: device tensors");
+  const int64_t R = x.size(0), P = x.size(1), Q = y.size(1);
+  TORCH_CHECK(y.size(0) == R && out.size(0) == P && out.size(1) == Q, "gemm_wgrad: shape mismatch");
+  if (x.stride(1) != 1 || y.stride(1) != 1 || out.stride(1) != 1) return false;
+  if (x.stride(0) % 8 || y.stride(0) % 8 || out.stride(0) % 8) return false;
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&x, &y, &out})
+    if (reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) return false;
+  if (P > INT32_MAX || Q > INT32_MAX || R > INT32_MAX || !grt::gemm_tt_supported((int)P, (int)Q, (int)R))
+    return false;
+  c10::OptionalDeviceGuard g(x.device());
+  grt::GemmTTParams p{x.data_ptr(), y.data_ptr(), out.data_ptr(), (int)P, (int)Q, (int)R,
+                      x.stride(0), y.stride(0), out.stride(0), accumulate ? 1 : 0};
+  grt::gemm_tt(p, cur_stream(x), (int)mode);
+  return true;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -446,4 +468,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
+  m.def("gemm_wgrad", &gemm_wgrad, py::arg("x"), py::arg("y"), py::arg("out"), py::arg("accumulate"),
+        py::arg("mode") = 0);
 }

@@ -107,4 +107,17 @@ void nf4_quantize(DType dt, const void* w, uint8_t* q, float* absmax, int64_t n,
 void nf4_dequantize(DType dt, const uint8_t* q, const float* absmax, void* w, int64_t n,
                     int blocksize, hipStream_t s);
 
+// ---------------- weight-gradient GEMM (gemm.hip) ----------------
+// C[P][Q] (+)= sum_r X[r][p] * Y[r][q]; X [R][P], Y [R][Q], C [P][Q] row-major bf16.
+struct GemmTTParams {
+  const void* x;  // bf16
+  const void* y;  // bf16
+  void* c;        // bf16
+  int P, Q, R;
+  int64_t ldx, ldy, ldc;
+  int beta;  // 1: C += result (gradient accumulation), 0: C = result
+};
+bool gemm_tt_supported(int P, int Q, int R);
+void gemm_tt(const GemmTTParams& p, hipStream_t stream, int mode = 0);  // mode != 0: diagnostics
+
 }  // namespace grt

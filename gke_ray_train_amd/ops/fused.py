@@ -12,6 +12,7 @@ import torch
 
 from .. import _native
 from . import _ref
+from .linear import wgrad
 
 
 def _gpu(t: torch.Tensor) -> bool:
@@ -302,10 +303,10 @@ class _LMHeadCE(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             slot = getattr(weight, "_grt_slot", None)
             if slot is not None:   # GEMM writes dW straight into the DDP bucket (ops/linear.py)
-                slot.write(lambda v: torch.mm(dlogits.t(), hidden, out=v), lambda v: v.addmm_(dlogits.t(), hidden))
+                slot.write(lambda v: wgrad(dlogits, hidden, v, False), lambda v: wgrad(dlogits, hidden, v, True))
                 slot.notify(weight)
             else:
-                dw = dlogits.t() @ hidden
+                dw = wgrad(dlogits, hidden)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dlogits.sum(0)
         return dh, dw, db, None, None

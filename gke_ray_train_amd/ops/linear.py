@@ -13,6 +13,8 @@ The engine attaches ``param._grt_slot = GradSlot(view, notify)``; without it thi
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -48,6 +50,32 @@ class GradSlot:
         return False
 
 
+_WGRAD_NATIVE = os.environ.get("GRT_WGRAD_GEMM", "1") != "0"
+
+
+def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor = None, accumulate: bool = False) -> torch.Tensor:
+    """dW = dy2^T @ x2 ([M,N]^T [M,K] -> [N,K]), written into / accumulated onto ``out``.
+
+    bf16 on MI355X runs the hand-written MFMA kernel (csrc/kernels/gemm.hip) when the shape tiles
+    (N, K multiples of 256, M of 64); anything else goes to hipBLASLt through torch.
+    """
+    dy2 = dy2.reshape(-1, dy2.shape[-1])
+    x2 = x2.reshape(-1, x2.shape[-1])
+    if out is None:
+        out = torch.empty(dy2.shape[1], x2.shape[1], device=dy2.device, dtype=dy2.dtype)
+        accumulate = False
+    if _WGRAD_NATIVE and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 \
+            and out.dtype == torch.bfloat16:
+        from .. import _native
+        if _native.kernels().gemm_wgrad(dy2, x2, out, accumulate):
+            return out
+    if accumulate:
+        out.addmm_(dy2.t(), x2)
+    else:
+        torch.mm(dy2.t(), x2, out=out)
+    return out
+
+
 class _DirectGradLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
@@ -67,10 +95,10 @@ class _DirectGradLinear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             slot = getattr(w, "_grt_slot", None)
             if slot is not None:
-                slot.write(lambda v: torch.mm(dy2.t(), x2, out=v), lambda v: v.addmm_(dy2.t(), x2))
+                slot.write(lambda v: wgrad(dy2, x2, v, False), lambda v: wgrad(dy2, x2, v, True))
                 slot.notify(w)
             else:
-                dw = dy2.t() @ x2
+                dw = wgrad(dy2, x2)
         if ctx.has_b:
             b_needs = ctx.needs_input_grad[2]
             if b_needs:

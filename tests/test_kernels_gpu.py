@@ -288,3 +288,40 @@ def test_llama_tiny_matches_reference_math():
         a, b = g_native[n].cpu(), p.grad
         rel = (a - b).norm() / (b.norm() + 1e-8)
         assert rel < 0.08, f"{n}: rel grad err {rel:.3f}"
+
+
+@pytest.mark.parametrize("R,P,Q,strided", [(64, 256, 256, False), (1024, 768, 512, False), (2048, 512, 1280, True),
+                                          (8192, 256, 256, False), (96, 512, 256, False)])
+def test_gemm_wgrad(R, P, Q, strided):
+    mode = 0
+    """Hand-written MFMA wgrad GEMM vs an fp32 reference, overwrite and accumulate (beta=1)."""
+    C = _C()
+    g = torch.Generator(device="cuda").manual_seed(R + P + Q)
+    xs = torch.randn(R, P + (64 if strided else 0), device="cuda", generator=g).bfloat16()
+    ys = torch.randn(R, Q + (128 if strided else 0), device="cuda", generator=g).bfloat16()
+    x, y = xs[:, :P], ys[:, :Q]
+    ref = x.float().t() @ y.float()
+    out = torch.full((P, Q), float("nan"), device="cuda", dtype=torch.bfloat16)
+    if R % 64:
+        assert not C.gemm_wgrad(x, y, out, False, mode)
+        return
+    assert C.gemm_wgrad(x, y, out, False, mode)
+    tol = 2e-2 * ref.abs().max().item() + 1e-2
+    assert (out.float() - ref).abs().max().item() < tol
+    base = torch.randn(P, Q, device="cuda", generator=g).bfloat16()
+    out2 = base.clone()
+    assert C.gemm_wgrad(x, y, out2, True, mode)
+    assert (out2.float() - (ref + base.float())).abs().max().item() < tol
+    # tiles that do not divide are refused (the caller falls back to hipBLASLt)
+    assert not C.gemm_wgrad(x[:, : P - 8], y, torch.empty(P - 8, Q, device="cuda", dtype=torch.bfloat16), False)
+
+
+def test_wgrad_helper_fallback_and_native():
+    from gke_ray_train_amd.ops.linear import wgrad
+    dy = torch.randn(512, 384, device="cuda").bfloat16()   # 384 is not a multiple of 256 -> hipBLASLt
+    x = torch.randn(512, 512, device="cuda").bfloat16()
+    ref = dy.float().t() @ x.float()
+    assert (wgrad(dy, x).float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()
+    dy = torch.randn(512, 512, device="cuda").bfloat16()
+    ref = dy.float().t() @ x.float()
+    assert (wgrad(dy, x).float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()

@@ -31,6 +31,11 @@ def timeit(fn, iters=20, warmup=5):
 def gemms(T=8192, d=4096, f=11008, V=32000):
     out = []
     dev = "cuda"
+    try:
+        from gke_ray_train_amd import _native
+        C = _native.kernels()
+    except Exception:
+        C = None
     shapes = {
         "qkv_fwd": (T, d, 3 * d), "o_fwd": (T, d, d), "gate_up_fwd": (T, d, 2 * f), "down_fwd": (T, f, d),
         "lm_head_fwd": (T, d, V),
@@ -47,6 +52,18 @@ def gemms(T=8192, d=4096, f=11008, V=32000):
         out.append(dict(op=f"gemm_{name.replace('fwd', 'dgrad')}", ms=t * 1e3, tflops=fl / t / 1e12))
         t = timeit(lambda: torch.mm(dy.t(), x, out=dw))
         out.append(dict(op=f"gemm_{name.replace('fwd', 'wgrad')}", ms=t * 1e3, tflops=fl / t / 1e12))
+        if C is not None and C.gemm_wgrad(dy, x, dw, False):
+            ref = dw.float()
+            torch.mm(dy.t(), x, out=dw)
+            err = (ref - dw.float()).abs().max().item() / dw.float().abs().max().item()
+            t = timeit(lambda: C.gemm_wgrad(dy, x, dw, False))
+            out.append(dict(op=f"gemm_{name.replace('fwd', 'wgrad')}_grt", ms=t * 1e3, tflops=fl / t / 1e12,
+                            rel_err=err))
+            if os.environ.get("GRT_GEMM_DIAG"):
+                for mode in (1, 2, 3, 4, 5, 6):
+                    t = timeit(lambda: C.gemm_wgrad(dy, x, dw, False, mode))
+                    out.append(dict(op=f"gemm_{name.replace('fwd', 'wgrad')}_grt_mode{mode}", ms=t * 1e3,
+                                    tflops=fl / t / 1e12))
     return out
 
 
