@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--metrics-jsonl", default="", help="per-step metrics (phase breakdown, MFU, HBM) -> JSONL; "
                     "adds one host sync per step, so it is off for the headline number")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--backend", default="", help="process-group backend (default: nccl = RCCL on GPU, gloo on CPU)")
     return ap.parse_args()
 
 
@@ -102,10 +103,13 @@ def main():
     if cpu:
         dev = torch.device("cpu")
     else:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # one rank per GPU; ranks beyond the visible GPUs share them (rehearsal with --backend gloo)
+        idx = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     if world > 1:
-        dist.init_process_group("gloo" if cpu else "nccl", device_id=None if cpu else dev)
+        backend = a.backend or ("gloo" if cpu else "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     from gke_ray_train_amd.data import TokenBatchLoader, synthetic_tokens
     from gke_ray_train_amd.models import get_config
