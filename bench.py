@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--peft", default="none", choices=["none", "lora", "qlora"])
     ap.add_argument("--lora-r", type=int, default=64)
     ap.add_argument("--bucket-mb", type=float, default=0.0, help="DDP bucket size (0 = planner)")
+    ap.add_argument("--zero", default="auto", choices=["auto", "on", "off"],
+                    help="DDP sharded optimizer (reduce-scatter + 1/N AdamW + overlapped all-gather); "
+                         "auto = on when world > 1")
     ap.add_argument("--max-grad-norm", type=float, default=0.3)
     ap.add_argument("--lr", type=float, default=2e-5)
     ap.add_argument("--checkpointing", action="store_true", help="activation checkpointing")
@@ -89,7 +92,8 @@ def build(a, cfg, dev, dtype, world):
         if a.peft == "qlora":
             quantize_model_(model, BitsAndBytesConfig(bnb_4bit_compute_dtype=dtype))
         fwd = get_peft_model(model, LoraConfig(r=a.lora_r, lora_alpha=16, lora_dropout=0.1))
-    eng = DistributedDataParallel(fwd, bucket_cap_mb=a.bucket_mb or None)
+    zero = a.zero == "on" or (a.zero == "auto" and world > 1)
+    eng = DistributedDataParallel(fwd, bucket_cap_mb=a.bucket_mb or None, shard_optimizer=zero)
     opt = FusedAdamW(eng.optimizer_param_groups(weight_decay=0.0), lr=a.lr)
     return fwd, eng, fwd, opt
 
@@ -113,7 +117,6 @@ def main():
 
     from gke_ray_train_amd.data import TokenBatchLoader, synthetic_tokens
     from gke_ray_train_amd.models import get_config
-    from gke_ray_train_amd.ops import clip_grad_norm_
 
     torch.manual_seed(1234)
     dtype = torch.float32 if cpu else torch.bfloat16
@@ -166,11 +169,10 @@ def main():
         with ph("grad_sync"):
             eng.finish_gradient_sync()
         with ph("optimizer"):
-            if fsdp:
-                st = eng.clip_grad_norm_(a.max_grad_norm)
-            else:
-                st = clip_grad_norm_(eng.grad_buffers(), a.max_grad_norm, prescale=1.0 / eng.world_size)
+            st = eng.clip_grad_norm_(a.max_grad_norm)  # global norm of the averaged gradient, on device
             opt.step(grad_scale=st)
+            if not fsdp:
+                eng.after_optimizer_step()  # ZeRO: async all-gather of the updated shards
             eng.zero_grad()
         return loss
 
@@ -184,6 +186,8 @@ def main():
 
     for _ in range(a.warmup):
         loss = step()
+    if not fsdp:
+        eng.wait_params()
     if not cpu:
         torch.cuda.synchronize()
     if world > 1:
@@ -198,6 +202,8 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = timed_step(i)
+    if not fsdp:
+        eng.wait_params()  # the last step's parameter all-gather belongs to the timed work
     if not cpu:
         torch.cuda.synchronize()
     if world > 1:
@@ -223,7 +229,8 @@ def main():
     if a.peft != "none":
         fpt = fpt * 2.0 / 3.0  # frozen base: no weight-gradient GEMMs (adapter FLOPs are negligible)
     mfu = tps / world * fpt / 2.5e15
-    par = f"{'fsdp' if fsdp else 'dp'}{world}" + ("+offload" if a.offload else "") + \
+    par = f"{'fsdp' if fsdp else 'dp'}{world}" + ("+zero1" if getattr(eng, "zero", False) else "") + \
+        ("+offload" if a.offload else "") + \
         ("" if a.peft == "none" else f"+{a.peft}")
     if rank == 0:
         out = {

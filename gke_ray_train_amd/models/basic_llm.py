@@ -158,7 +158,7 @@ class BasicLLM(nn.Module):
         x = ops.dropout(x, self.dropout_p, self.training)
         for layer in self.transformer_decoder.layers:
             x = layer(x, B, S)
-        return ops.lm_head_cross_entropy(x, self.fc_out.weight, targets.reshape(-1), bias=self.fc_out.bias)
+        return self.fc_out(x, labels=targets.reshape(-1))
 
 
 class _ScaleAddPE(torch.autograd.Function):

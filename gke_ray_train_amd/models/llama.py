@@ -162,6 +162,12 @@ class RMSNorm(nn.Module):
         self.weight = nn.Parameter(torch.ones(d, device=device, dtype=dtype))
         self.eps = eps
 
+    def forward(self, x, residual=None):
+        """rms_norm(x) or, with ``residual``, the fused (norm(x + residual), x + residual)."""
+        if residual is None:
+            return ops.rms_norm(x, self.weight, self.eps)
+        return ops.add_rms_norm(x, residual, self.weight, self.eps)
+
 
 class LlamaDecoderLayer(nn.Module):
     def __init__(self, cfg: LlamaConfig, device=None, dtype=None):
@@ -250,7 +256,7 @@ class LlamaForCausalLM(nn.Module):
                     h, residual = ckpt.checkpoint(layer, h, residual, B, S, cos, sin, use_reentrant=False)
             else:
                 h, residual = layer(h, residual, B, S, cos, sin)
-        x, _ = ops.add_rms_norm(h, residual, self.model.norm.weight, self.model.norm.eps)
+        x, _ = self.model.norm(h, residual)
         return x
 
     def forward(self, input_ids, labels=None, attention_mask=None, return_logits=None):
@@ -263,7 +269,7 @@ class LlamaForCausalLM(nn.Module):
             shifted[:, :-1] = labels[:, 1:]
             if attention_mask is not None:
                 shifted[:, :-1].masked_fill_(attention_mask[:, 1:] == 0, -100)
-            out["loss"] = ops.lm_head_cross_entropy(x, self.lm_head.weight, shifted.view(-1))
+            out["loss"] = self.lm_head(x, labels=shifted.view(-1))
         if labels is None or return_logits:
             out["logits"] = self.lm_head(x).view(B, S, -1)
         return out

@@ -113,7 +113,15 @@ def linear(x, weight, bias=None):
 
 
 class Linear(nn.Linear):
-    """nn.Linear (same parameters / state_dict) routed through ``ops.linear``."""
+    """nn.Linear (same parameters / state_dict) routed through ``ops.linear``.
 
-    def forward(self, x):
+    ``layer(x, labels=t)`` is the fused LM-head + cross-entropy (``ops.lm_head_cross_entropy``)
+    instead of logits; going through ``__call__`` keeps module hooks (e.g. the ZeRO parameter
+    gather wait of parallel/ddp.py) firing for the head's weight.
+    """
+
+    def forward(self, x, labels=None, ignore_index: int = -100):
+        if labels is not None:
+            from .fused import lm_head_cross_entropy
+            return lm_head_cross_entropy(x, self.weight, labels, bias=self.bias, ignore_index=ignore_index)
         return linear(x, self.weight, self.bias)

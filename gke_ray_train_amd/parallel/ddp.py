@@ -16,7 +16,13 @@ MI355X design (not a translation of torch's C++ Reducer):
   bucket's transfer is exposed after the last backward kernel;
 * buffers are not re-broadcast every step (the reference BasicLLM paid an 8 MiB PE-buffer
   broadcast per forward, SURVEY §2.7 C03); parameters are broadcast once at construction;
-* ``no_sync()`` for gradient accumulation (GRADIENT_ACCUMULATION_STEPS, fine_tune_config.json:14).
+* ``no_sync()`` for gradient accumulation (GRADIENT_ACCUMULATION_STEPS, fine_tune_config.json:14);
+* ``shard_optimizer=True`` (ZeRO-1/2, world > 1): each bucket is REDUCE-SCATTERED during backward
+  (half the bytes of an all-reduce on the critical path) into a contiguous per-rank gradient shard,
+  the fused AdamW updates only this rank's 1/world of the parameters (optimizer state and its HBM
+  traffic shrink by world), and the updated shards are ALL-GATHERED back into the flat parameter
+  buffer asynchronously, bucket by bucket in forward order, each bucket waited for by a forward
+  pre-hook of the first module that uses it — the gather overlaps the next step's forward.
 """
 from __future__ import annotations
 
@@ -45,6 +51,8 @@ class _Bucket:
     params: List[nn.Parameter] = field(default_factory=list)
     ready: int = 0
     work: Optional[object] = None
+    shard_off: int = 0        # ZeRO: offset of this bucket's chunk in the rank's shard buffers
+    ag_work: Optional[object] = None
 
 
 @dataclass
@@ -57,9 +65,12 @@ class _FlatGroup:
     grad: torch.Tensor
     offsets: List[int]
     buckets: List[_Bucket]
+    shard_param: Optional[torch.Tensor] = None   # ZeRO: this rank's parameter shard (contiguous)
+    shard_grad: Optional[torch.Tensor] = None
 
 
 class DistributedDataParallel(nn.Module):
+
     """nn.Module wrapper like torch DDP (``.module``, ``module.``-prefixed state_dict); the wrapped
     module's parameters become views into flat buffers and stay usable by any optimizer.
 
@@ -67,15 +78,18 @@ class DistributedDataParallel(nn.Module):
     breaks on one GPU because Ray's prepare_model does not wrap then; this wrapper is applied at
     every world size so that access always works.
     """
+    UNIT_TYPES = ("LlamaDecoderLayer", "EncoderLayer")
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  broadcast_params: bool = True, grad_dtype: Optional[torch.dtype] = None,
-                 split_decay: bool = True):
+                 split_decay: bool = True, shard_optimizer: bool = False):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world_size > 1 else 0
+        self.zero = bool(shard_optimizer) and self.world_size > 1
+        self.gloo = self.world_size > 1 and dist.get_backend(process_group) == "gloo"
         self._sync = True
         self._hooks = []
         self._grad_view = {}
@@ -123,14 +137,25 @@ class DistributedDataParallel(nn.Module):
                     if id(p) in self._direct:
                         p._grt_slot = sl
         self._register_hooks()
+        if self.zero:
+            self._setup_shards()
 
     # ------------------------------------------------------------------ layout
     def _flatten(self, items, dtype, decay, grad_dtype) -> _FlatGroup:
         align = 64  # elements: keeps every view 128-byte aligned for 16-byte vector kernels
-        offsets, off = [], 0
+        # ZeRO: every bucket spans a multiple of align * world so it splits into equal aligned chunks
+        bucket_align = align * (self.world_size if self.zero else 1)
+        elt = torch.tensor([], dtype=grad_dtype).element_size()
+        offsets, spans, off, cur_start = [], [], 0, 0
         for _, p in items:
+            if off > cur_start and (off - cur_start) * elt >= self.bucket_bytes:
+                off = (off + bucket_align - 1) // bucket_align * bucket_align
+                spans.append((cur_start, off))
+                cur_start = off
             offsets.append(off)
             off += (p.numel() + align - 1) // align * align
+        off = (off + bucket_align - 1) // bucket_align * bucket_align
+        spans.append((cur_start, off))
         dev = items[0][1].device
         flat = torch.zeros(off, dtype=dtype, device=dev)
         grad = torch.zeros(off, dtype=grad_dtype, device=dev)
@@ -142,18 +167,61 @@ class DistributedDataParallel(nn.Module):
                 p.grad = grad[o:o + p.numel()].view_as(p)
                 self._grad_view[p] = p.grad
                 params.append(p)
-        # buckets over the contiguous reverse-order layout
-        buckets: List[_Bucket] = []
-        elt = torch.tensor([], dtype=grad_dtype).element_size()
-        cur = None
+        buckets = [_Bucket(start=a, end=b) for a, b in spans]
+        bi = 0
         for p, o in zip(params, offsets):
-            n_el = (p.numel() + align - 1) // align * align
-            if cur is None or (cur.end - cur.start) * elt >= self.bucket_bytes:
-                cur = _Bucket(start=o, end=o)
-                buckets.append(cur)
-            cur.params.append(p)
-            cur.end = o + n_el
+            while o >= buckets[bi].end:
+                bi += 1
+            buckets[bi].params.append(p)
+        buckets = [b for b in buckets if b.params]
         return _FlatGroup(dtype, decay, params, [n for n, _ in items], flat, grad, offsets, buckets)
+
+    def _setup_shards(self):
+        """ZeRO: contiguous per-rank shard buffers (bucket chunks back to back) + forward pre-hooks."""
+        W, r = self.world_size, self.rank
+        for g in self.groups:
+            tot = 0
+            for b in g.buckets:
+                b.shard_off = tot
+                tot += (b.end - b.start) // W
+            g.shard_param = torch.empty(tot, dtype=g.flat.dtype, device=g.flat.device)
+            g.shard_grad = torch.zeros(tot, dtype=g.grad.dtype, device=g.grad.device)
+            with torch.no_grad():
+                for b in g.buckets:
+                    c = (b.end - b.start) // W
+                    g.shard_param[b.shard_off:b.shard_off + c].copy_(g.flat[b.start + r * c:b.start + (r + 1) * c])
+        # Which module's forward pre-hook waits for a bucket: the enclosing transformer layer for
+        # parameters inside one (layers read their norm weights directly, not via submodule calls),
+        # else the parameter's own module (embedding, final norm, LM head).
+        owner = {}
+        for g in self.groups:
+            for b in g.buckets:
+                for p in b.params:
+                    owner[id(p)] = b
+        waits = {}
+        claimed = set()
+        for m in self.module.modules():
+            if type(m).__name__ in self.UNIT_TYPES:
+                for p in m.parameters():
+                    if id(p) in owner and id(p) not in claimed:
+                        claimed.add(id(p))
+                        waits.setdefault(m, {})[id(owner[id(p)])] = owner[id(p)]
+        for m in self.module.modules():
+            for p in m.parameters(recurse=False):
+                if id(p) in owner and id(p) not in claimed:
+                    claimed.add(id(p))
+                    waits.setdefault(m, {})[id(owner[id(p)])] = owner[id(p)]
+        for m, bs in waits.items():
+            self._hooks.append(m.register_forward_pre_hook(self._make_gather_wait(list(bs.values()))))
+
+    @staticmethod
+    def _make_gather_wait(buckets):
+        def hook(mod, args):
+            for b in buckets:
+                if b.ag_work is not None:
+                    b.ag_work.wait()
+                    b.ag_work = None
+        return hook
 
     def _register_hooks(self):
         for g in self.groups:
@@ -194,8 +262,14 @@ class DistributedDataParallel(nn.Module):
             self._launch(g, b)
 
     def _launch(self, g: _FlatGroup, b: _Bucket):
-        if b.work is None:
+        if b.work is not None:
+            return
+        if not self.zero or self.gloo:  # gloo has no reduce-scatter: all-reduce, keep our chunk later
             b.work = dist.all_reduce(g.grad[b.start:b.end], op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+        else:
+            c = (b.end - b.start) // self.world_size
+            b.work = dist.reduce_scatter_tensor(g.shard_grad[b.shard_off:b.shard_off + c], g.grad[b.start:b.end],
+                                                op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
 
     # ------------------------------------------------------------------ public API
     @contextlib.contextmanager
@@ -209,6 +283,7 @@ class DistributedDataParallel(nn.Module):
 
     def finish_gradient_sync(self):
         """Wait for every bucket's all-reduce (launching any whose params got no gradient)."""
+        self.wait_params()  # ZeRO: a bucket no forward module waited for (unused parameters)
         stale = [p for p, sl in self._slots.items() if sl.fresh]
         if stale:  # parameters that got no gradient this step: their slots hold last step's data
             torch._foreach_zero_([self._slots[p].view for p in stale])
@@ -226,9 +301,54 @@ class DistributedDataParallel(nn.Module):
                 b.work.wait()
                 b.work = None
                 b.ready = 0
+                if self.zero and self.gloo:
+                    c = (b.end - b.start) // self.world_size
+                    lo = b.start + self.rank * c
+                    g.shard_grad[b.shard_off:b.shard_off + c].copy_(g.grad[lo:lo + c])
 
     def grad_buffers(self) -> List[torch.Tensor]:
+        """Gradient buffers the optimizer consumes (ZeRO: this rank's reduced shards)."""
+        if self.zero:
+            return [g.shard_grad for g in self.groups]
         return [g.grad for g in self.groups]
+
+    def clip_grad_norm_(self, max_norm: float):
+        """Global grad norm of the AVERAGED gradient and the clip coefficient (device scalars, no
+        host sync); the 1/world averaging is folded into the coefficient consumed by FusedAdamW."""
+        from ..ops import clip_grad_norm_ as _clip
+        W = self.world_size
+        if not self.zero:
+            return _clip(self.grad_buffers(), max_norm, prescale=1.0 / W)
+        st = _clip(self.grad_buffers(), 0.0, prescale=1.0)
+        ss = (st.buf[0] ** 2).reshape(1)
+        dist.all_reduce(ss, group=self.pg)
+        total = ss[0].sqrt() / W
+        coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(total)
+        st.buf[0] = total
+        st.buf[1] = coef / W
+        return st
+
+    def after_optimizer_step(self):
+        """ZeRO: start the all-gather of the updated shards, forward order; forward pre-hooks wait."""
+        if not self.zero:
+            return
+        W = self.world_size
+        for g in self.groups:
+            for b in reversed(g.buckets):  # buckets are in backward order; forward needs the last first
+                c = (b.end - b.start) // W
+                src = g.shard_param[b.shard_off:b.shard_off + c]
+                if self.gloo:
+                    b.ag_work = dist.all_gather(list(g.flat[b.start:b.end].chunk(W)), src, group=self.pg,
+                                                async_op=True)
+                else:
+                    b.ag_work = dist.all_gather_into_tensor(g.flat[b.start:b.end], src, group=self.pg, async_op=True)
+
+    def wait_params(self):
+        for g in self.groups:
+            for b in g.buckets:
+                if b.ag_work is not None:
+                    b.ag_work.wait()
+                    b.ag_work = None
 
     def zero_grad(self, set_to_none: bool = True):
         """Mark every gradient slot fresh: the next write overwrites (GEMM beta = 0 / copy)."""
@@ -237,11 +357,12 @@ class DistributedDataParallel(nn.Module):
             p.grad = None
 
     def optimizer_param_groups(self, weight_decay: float = 0.0):
-        """One flat Parameter per (dtype, decay) group; its .grad is the flat gradient buffer."""
+        """One flat Parameter per (dtype, decay) group; its .grad is the flat gradient buffer
+        (ZeRO: this rank's contiguous parameter / gradient shard)."""
         out = []
         for g in self.groups:
-            fp = nn.Parameter(g.flat, requires_grad=False)
-            fp.grad = g.grad
+            fp = nn.Parameter(g.shard_param if self.zero else g.flat, requires_grad=False)
+            fp.grad = g.shard_grad if self.zero else g.grad
             out.append({"params": [fp], "weight_decay": weight_decay if g.decay else 0.0})
         return out
 

@@ -77,3 +77,63 @@ def test_ddp_matches_single_process(accum):
         (m(micro[j], labels=micro[j])["loss"] / (world * accum)).backward()
     for n, p in m.named_parameters():
         assert torch.allclose(p.grad, g0[n], atol=1e-5, rtol=1e-4), f"{n}: max {(p.grad - g0[n]).abs().max()}"
+
+
+def _zero_worker(rank, world, port, q, zero):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gke_ray_train_amd.models import build_llama
+        from gke_ray_train_amd.ops import FusedAdamW
+        from gke_ray_train_amd.parallel import DistributedDataParallel
+        m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=3)
+        ddp = DistributedDataParallel(m, bucket_cap_mb=0.1, shard_optimizer=zero)
+        assert ddp.zero == zero
+        opt = FusedAdamW(ddp.optimizer_param_groups(0.1), lr=3e-3)
+        if zero:  # the optimizer holds only this rank's shard
+            n_opt = sum(p.numel() for gp in opt.param_groups for p in gp["params"])
+            assert n_opt * world <= sum(g.flat.numel() for g in ddp.groups) + 1
+        g = torch.Generator().manual_seed(1)
+        norms = []
+        for step in range(3):
+            ids = torch.randint(0, 512, (world * 2, 32), generator=g).view(world, 2, 32)[rank]
+            loss = ddp(ids, labels=ids)["loss"]
+            loss.backward()
+            ddp.finish_gradient_sync()
+            st = ddp.clip_grad_norm_(0.5)
+            norms.append(float(st.buf[0]))
+            opt.step(grad_scale=st)
+            ddp.after_optimizer_step()
+            ddp.zero_grad()
+        ddp.wait_params()
+        q.put((rank, {n: p.detach().numpy().copy() for n, p in m.named_parameters()}, norms))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zero_sharded_optimizer_matches_ddp():
+    """ZeRO-1/2 mode (reduce-scatter + sharded AdamW + async all-gather) == plain DDP, 3 steps."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    out = {}
+    for zero in (False, True):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_zero_worker, args=(r, world, port, q, zero)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = {}
+        for _ in range(world):
+            r, prm, norms = q.get(timeout=300)
+            res[r] = (prm, norms)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        for n in res[0][0]:
+            assert (res[0][0][n] == res[1][0][n]).all(), f"zero={zero}: ranks diverged on {n}"
+        out[zero] = res[0]
+    (p_ref, n_ref), (p_zero, n_zero) = out[False], out[True]
+    assert max(abs(a - b) for a, b in zip(n_ref, n_zero)) < 1e-4 * max(n_ref), (n_ref, n_zero)
+    for n in p_ref:
+        d = abs(p_ref[n] - p_zero[n]).max()
+        assert d < 1e-5, f"{n}: {d}"

@@ -86,3 +86,58 @@ def test_two_ranks_on_one_gpu_match_single_process(engine, accum):
             scale = np.abs(ref).max() + 1e-6
             assert np.abs(got - ref).max() / scale < 0.05, f"{engine} rank {r} {n}"
         assert np.array_equal(res[0][n], res[1][n]) or engine == "fsdp", f"ranks disagree on {n}"
+
+
+def _opt_worker(rank, world, port, q, zero):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gke_ray_train_amd.models import build_llama
+        from gke_ray_train_amd.ops import FusedAdamW
+        from gke_ray_train_amd.parallel import DistributedDataParallel
+        m = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=7)
+        eng = DistributedDataParallel(m, bucket_cap_mb=0.25, shard_optimizer=zero)
+        opt = FusedAdamW(eng.optimizer_param_groups(0.0), lr=1e-3)
+        ids = _batch(world, 2).view(2, world, -1, 128)[:, rank].cuda()
+        for step in range(2):
+            loss = eng(ids[step], labels=ids[step])["loss"]
+            loss.backward()
+            eng.finish_gradient_sync()
+            opt.step(grad_scale=eng.clip_grad_norm_(1.0))
+            eng.after_optimizer_step()
+            eng.zero_grad()
+        eng.wait_params()
+        q.put((rank, {n: p.detach().float().cpu().numpy() for n, p in m.named_parameters()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_zero_matches_plain_ddp_two_ranks_on_one_gpu():
+    """Sharded-optimizer DDP (reduce-scatter, 1/world AdamW, async all-gather waited by forward
+    pre-hooks) takes the same two optimizer steps as plain DDP (same reduced gradients; only the
+    grad-norm summation order differs -> agreement to bf16 rounding)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    out = {}
+    for zero in (False, True):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_opt_worker, args=(r, world, port, q, zero)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = {}
+        try:
+            for _ in range(world):
+                r, prm = q.get(timeout=300)
+                res[r] = prm
+        finally:
+            for p in procs:
+                p.join(timeout=60)
+        assert all(p.exitcode == 0 for p in procs)
+        for n in res[0]:
+            assert np.array_equal(res[0][n], res[1][n]), f"zero={zero}: ranks disagree on {n}"
+        out[zero] = res[0]
+    for n, ref in out[False].items():
+        got = out[True][n]
+        assert np.all(np.abs(got - ref) <= 1e-2 * np.abs(ref) + 1e-5), f"{n}: {np.abs(got - ref).max()}"
