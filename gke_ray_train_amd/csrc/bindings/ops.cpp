@@ -4,6 +4,9 @@
 // besides the torch caching allocator, no synchronisation) and checks shapes/strides on the
 // host BEFORE launch so a hand-written kernel never sees operands its grid does not expect.
 #include <torch/extension.h>
+
+#include <algorithm>
+#include <cmath>
 #include <c10/hip/HIPStream.h>
 #include <c10/core/DeviceGuard.h>
 
@@ -352,15 +355,29 @@ grt::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, c
     TORCH_CHECK(seqlens_k->scalar_type() == at::kInt && seqlens_k->numel() == q.size(0), "seqlens_k int32 [B]");
     p.seqlens_k = seqlens_k->data_ptr<int32_t>();
   }
+  p.drop_seed = 0;
+  p.drop_thresh = 0;
+  p.drop_scale = 1.f;
   return p;
 }
 
+void set_dropout(grt::AttnParams& p, double dropout_p, int64_t seed) {
+  TORCH_CHECK(dropout_p >= 0.0 && dropout_p < 1.0, "attention dropout p must be in [0, 1)");
+  if (dropout_p <= 0.0) return;
+  p.drop_seed = (uint32_t)(seed & 0xffffffffLL);
+  p.drop_thresh = (uint32_t)std::min(4294967295.0, std::ceil(dropout_p * 4294967296.0));
+  if (p.drop_thresh == 0) p.drop_thresh = 1;
+  p.drop_scale = (float)(1.0 / (1.0 - dropout_p));
+}
+
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& out,
-                             double scale, bool causal, const optional<Tensor>& seqlens_k) {
+                             double scale, bool causal, const optional<Tensor>& seqlens_k, double dropout_p,
+                             int64_t seed) {
   c10::OptionalDeviceGuard g(q.device());
   Tensor o = out.has_value() ? *out : at::empty(q.sizes(), q.options());
   auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
   auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k);
+  set_dropout(p, dropout_p, seed);
   grt::attn_fwd(p, cur_stream(q));
   return {o, lse};
 }
@@ -368,11 +385,12 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
 std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                              Tensor& lse, const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
                              const optional<Tensor>& dv_out, double scale, bool causal,
-                             const optional<Tensor>& seqlens_k) {
+                             const optional<Tensor>& seqlens_k, double dropout_p, int64_t seed) {
   c10::OptionalDeviceGuard g(q.device());
   check_bshd(dout, "dout");
   TORCH_CHECK(dout.sizes() == q.sizes(), "dout shape");
   auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k);
+  set_dropout(p, dropout_p, seed);
   Tensor dq = dq_out.has_value() ? *dq_out : at::empty(q.sizes(), q.options());
   Tensor dk = dk_out.has_value() ? *dk_out : at::empty(k.sizes(), k.options());
   Tensor dv = dv_out.has_value() ? *dv_out : at::empty(v.sizes(), v.options());
@@ -464,8 +482,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("clip_finalize", &clip_finalize);
   m.def("adamw", &adamw);
   m.def("scale_", &scale_);
-  m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("scale"),
+        py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
+        py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"), py::arg("causal"),
+        py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("gemm_wgrad", &gemm_wgrad, py::arg("x"), py::arg("y"), py::arg("out"), py::arg("accumulate"),

@@ -88,6 +88,11 @@ struct AttnParams {
   float scale;
   int causal;
   const int32_t* seqlens_k;   // optional per-batch valid key length (right padding), may be null
+  // attention-probability dropout (0 = off): element (b*Hq + hq, q, k) is kept iff
+  // attn_dropout_hash(seed, bh, q, k) >= drop_thresh (= p * 2^32); kept values scaled by drop_scale
+  uint32_t drop_seed;
+  uint32_t drop_thresh;
+  float drop_scale;
 };
 void attn_fwd(const AttnParams& p, hipStream_t s);
 struct AttnBwdParams {

@@ -66,6 +66,22 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& x, int base) {
 }
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
+// Counter-based dropout hash (must match ops/_ref.attn_dropout_keep bit for bit): murmur3 fmix32
+// of the (batch*head, query, key) coordinates mixed with the per-call seed. Stateless, so the
+// forward and both backward kernels regenerate the same mask without storing it.
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t attn_dropout_hash(uint32_t seed, uint32_t bh, uint32_t q, uint32_t k) {
+  uint32_t h = seed ^ (bh * 0x9E3779B1u);
+  h = fmix32(h ^ (q * 0x85EBCA77u));
+  return fmix32(h ^ (k * 0xC2B2AE3Du));
+}
+__device__ __forceinline__ float drop_factor(const AttnParams& p, uint32_t bh, int q, int k) {
+  return attn_dropout_hash(p.drop_seed, bh, (uint32_t)q, (uint32_t)k) >= p.drop_thresh ? p.drop_scale : 0.f;
+}
+
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
@@ -75,6 +91,7 @@ constexpr float kLn2 = 0.6931471805599453f;
 constexpr int FBM = 128, FBN = 64, FNT = 256;
 constexpr int kTileBytes = FBN * D * 2;  // 16 KiB
 
+template <bool DROP>
 __global__ __launch_bounds__(FNT, 2) void attn_fwd_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // K[2], V[2]
   auto Kl = [&](int buf) -> char* { return smem + buf * kTileBytes; };
@@ -184,8 +201,8 @@ __global__ __launch_bounds__(FNT, 2) void attn_fwd_kernel(const AttnParams p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float e = fast_exp2(s[n][r] - msub);
-          s[n][r] = e;
-          rs += e;
+          rs += e;  // the softmax normaliser uses the undropped probabilities
+          s[n][r] = DROP ? e * drop_factor(p, (uint32_t)bh, myq, kb + n * 32 + acc_row(r, h)) : e;
         }
       l = l * alpha + rs;
       m = mn;
@@ -262,6 +279,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p
 // the MFMA lane; K and V fragments stay in VGPRs for the whole sweep over the group's query heads
 // x 32-row query tiles (Q / dO tiles double-buffered in LDS, one barrier per tile). No atomics:
 // dK and dV are complete in registers at the end.
+template <bool DROP>
 __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdParams P) {
   const AttnParams& p = P.f;
   constexpr int QB = BBM * D * 2;
@@ -371,8 +389,15 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
           const int q = qt + 8 * gg + 4 * h + j;
           float pv = fast_exp2(s[r] * c - ls[j]);
           if (need_mask && (mykey >= sk || q >= p.Sq || (p.causal && mykey > q + off))) pv = 0.f;
-          s[r] = pv;
-          dp[r] = pv * (dp[r] - de[j]);
+          if (DROP) {
+            const uint32_t bhq = (uint32_t)(b * p.Hq + hkv * grp + it / nqt);
+            const float z = drop_factor(p, bhq, q, mykey);
+            s[r] = pv * z;                   // dV uses the dropped probabilities
+            dp[r] = pv * (dp[r] * z - de[j]);
+          } else {
+            s[r] = pv;
+            dp[r] = pv * (dp[r] - de[j]);
+          }
         }
       }
 #pragma unroll
@@ -417,6 +442,7 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
 // 64 keys double-buffered in LDS). S^T = K Q^T and dP^T = V dO^T are recomputed, dS^T stays in
 // registers and feeds dQ^T += K^T dS^T as the B operand (K^T by transposed reads of the same K
 // tile). lse and delta are lane-local. No atomics, dQ written once in bf16.
+template <bool DROP>
 __global__ __launch_bounds__(FNT, 2) void attn_bwd_dq_kernel(const AttnBwdParams P) {
   const AttnParams& p = P.f;
   __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // K[2], V[2]
@@ -509,11 +535,12 @@ __global__ __launch_bounds__(FNT, 2) void attn_bwd_dq_kernel(const AttnBwdParams
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float pv = fast_exp2(s[r] * c - lse2);
+          const int key = kb + n * 32 + acc_row(r, h);
           if (need_mask) {
-            const int key = kb + n * 32 + acc_row(r, h);
             if (key >= sk || (p.causal && key > myq + off)) pv = 0.f;
           }
-          s[r] = pv * (dp[r] - dlt);
+          const float z = DROP ? drop_factor(p, (uint32_t)bh, myq, key) : 1.f;
+          s[r] = pv * (dp[r] * z - dlt);
         }
 #pragma unroll
         for (int st = 0; st < 2; ++st) {
@@ -551,7 +578,8 @@ __global__ __launch_bounds__(FNT, 2) void attn_bwd_dq_kernel(const AttnBwdParams
 void attn_fwd(const AttnParams& p, hipStream_t s) {
   const int nqb = (p.Sq + FBM - 1) / FBM;
   const dim3 grid((unsigned)(nqb * p.B * p.Hq));
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(FNT), 0, s, p);
+  if (p.drop_thresh) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(FNT), 0, s, p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(FNT), 0, s, p);
 }
 
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
@@ -563,9 +591,15 @@ void attn_bwd(const AttnBwdParams& p, hipStream_t s) {
   const int64_t rows = (int64_t)p.f.B * p.f.Hq * p.f.Sq;
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
   const int nkb = (p.f.Sk + BBN - 1) / BBN;
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((unsigned)(nkb * p.f.B * p.f.Hkv)), dim3(BNT), 0, s, p);
   const int nqb = (p.f.Sq + FBM - 1) / FBM;
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((unsigned)(nqb * p.f.B * p.f.Hq)), dim3(FNT), 0, s, p);
+  const dim3 g1((unsigned)(nkb * p.f.B * p.f.Hkv)), g2((unsigned)(nqb * p.f.B * p.f.Hq));
+  if (p.f.drop_thresh) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(BNT), 0, s, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(FNT), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(BNT), 0, s, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(FNT), 0, s, p);
+  }
 }
 
 }  // namespace grt

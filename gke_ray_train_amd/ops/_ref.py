@@ -70,8 +70,33 @@ def apply_rope(x, cos, sin, pos=None):
     return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1).to(x.dtype)
 
 
-def attention(q, k, v, causal=True, scale=None, seqlens_k=None):
-    """q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] -> o [B,Sq,Hq,D]; math in fp32."""
+_M32 = 0xFFFFFFFF
+
+
+def _fmix32(h):
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    return h ^ (h >> 16)
+
+
+def attn_dropout_keep(seed: int, B: int, H: int, Sq: int, Sk: int, p: float, device=None) -> torch.Tensor:
+    """[B, H, Sq, Sk] bool keep-mask of the attention-probability dropout, bit-identical to the
+    counter hash of csrc/kernels/attention.hip (element (b*H + h, q, k))."""
+    thresh = min(_M32, math.ceil(p * 2 ** 32))
+    bh = torch.arange(B * H, device=device, dtype=torch.int64).view(B, H, 1, 1)
+    q = torch.arange(Sq, device=device, dtype=torch.int64).view(1, 1, Sq, 1)
+    k = torch.arange(Sk, device=device, dtype=torch.int64).view(1, 1, 1, Sk)
+    h = (seed & _M32) ^ ((bh * 0x9E3779B1) & _M32)
+    h = _fmix32(h ^ ((q * 0x85EBCA77) & _M32))
+    h = _fmix32(h ^ ((k * 0xC2B2AE3D) & _M32))
+    return h >= thresh
+
+
+def attention(q, k, v, causal=True, scale=None, seqlens_k=None, dropout_p=0.0, seed=0):
+    """q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] -> o [B,Sq,Hq,D]; math in fp32 (explicit matmul/softmax —
+    no SDPA backend dispatch). ``dropout_p`` drops attention probabilities with the kernel's mask."""
     B, Sq, Hq, D = q.shape
     Sk, Hkv = k.shape[1], k.shape[2]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
@@ -91,6 +116,9 @@ def attention(q, k, v, causal=True, scale=None, seqlens_k=None):
     s = s.masked_fill(mask, float("-inf"))
     p = torch.softmax(s, dim=-1)
     p = torch.nan_to_num(p, nan=0.0)
+    if dropout_p > 0.0:
+        keep = attn_dropout_keep(seed, B, Hq, Sq, Sk, dropout_p, device=q.device)
+        p = p * keep.to(p.dtype) / (1.0 - dropout_p)
     o = torch.matmul(p, vf).transpose(1, 2)
     return o.to(q.dtype)
 

@@ -166,30 +166,43 @@ def dropout(x, p, training=True, seed=None):
 # ----------------------------------------------------------------------------- attention
 class _FlashAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, causal, scale, seqlens_k):
+    def forward(ctx, q, k, v, causal, scale, seqlens_k, dropout_p, seed):
         C = _native.kernels()
-        o, lse = C.attn_fwd(q, k, v, None, scale, causal, seqlens_k)
+        o, lse = C.attn_fwd(q, k, v, None, scale, causal, seqlens_k, dropout_p, seed)
         ctx.save_for_backward(q, k, v, o, lse, seqlens_k)
-        ctx.causal, ctx.scale = causal, scale
+        ctx.causal, ctx.scale, ctx.dropout_p, ctx.seed = causal, scale, dropout_p, seed
         return o
 
     @staticmethod
     def backward(ctx, do):
         q, k, v, o, lse, seqlens_k = ctx.saved_tensors
         dq, dk, dv = _native.kernels().attn_bwd(do.contiguous(), q, k, v, o, lse, None, None, None,
-                                                ctx.scale, ctx.causal, seqlens_k)
-        return dq, dk, dv, None, None, None
+                                                ctx.scale, ctx.causal, seqlens_k, ctx.dropout_p, ctx.seed)
+        return dq, dk, dv, None, None, None, None, None
 
 
-def flash_attention(q, k, v, causal=True, scale=None, seqlens_k=None):
-    """q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] (any batch/seq/head strides) -> o [B,Sq,Hq,D]."""
+def _dropout_seed() -> int:
+    # drawn from torch's CPU generator (torch.manual_seed reproducible, no device sync)
+    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+
+
+def flash_attention(q, k, v, causal=True, scale=None, seqlens_k=None, dropout_p=0.0, seed=None):
+    """q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] (any batch/seq/head strides) -> o [B,Sq,Hq,D].
+
+    ``dropout_p`` > 0 drops attention probabilities (nn.MultiheadAttention / SDPA semantics:
+    softmax normaliser over all keys, kept probabilities scaled by 1/(1-p)); the mask is a
+    stateless counter hash of (seed, batch*head, query, key), regenerated in the backward.
+    """
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if dropout_p > 0.0 and seed is None:
+        seed = _dropout_seed()
+    seed = 0 if seed is None else int(seed)
     if _gpu(q) and q.dtype == torch.bfloat16 and q.shape[-1] == 128:
-        return _FlashAttn.apply(q, k, v, causal, scale, seqlens_k)
+        return _FlashAttn.apply(q, k, v, causal, scale, seqlens_k, float(dropout_p), seed)
     if _gpu(q):
         _warn_once(f"flash_attention: no gfx950 kernel for dtype={q.dtype} head_dim={q.shape[-1]}; "
                    "using the fp32 math path")
-    return _ref.attention(q, k, v, causal=causal, scale=scale, seqlens_k=seqlens_k)
+    return _ref.attention(q, k, v, causal=causal, scale=scale, seqlens_k=seqlens_k, dropout_p=dropout_p, seed=seed)
 
 
 _warned = set()

@@ -206,7 +206,7 @@ def test_nf4_roundtrip():
     assert rel < 0.15
 
 
-def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False):
+def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False, dropout_p=0.0):
     from gke_ray_train_amd import ops
     from gke_ray_train_amd.ops import _ref
     torch.manual_seed(8)
@@ -224,11 +224,11 @@ def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False):
         k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
         v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     sl = None if seqlens is None else torch.tensor(seqlens, device=DEV, dtype=torch.int32)
-    o = ops.flash_attention(q, k, v, causal=causal, seqlens_k=sl)
+    o = ops.flash_attention(q, k, v, causal=causal, seqlens_k=sl, dropout_p=dropout_p, seed=1234)
     do = torch.randn_like(o)
     (o.float() * do.float()).sum().backward()
     qr, kr, vr = (t.detach().float().requires_grad_() for t in (q, k, v))
-    orf = _ref.attention(qr, kr, vr, causal=causal, seqlens_k=sl)
+    orf = _ref.attention(qr, kr, vr, causal=causal, seqlens_k=sl, dropout_p=dropout_p, seed=1234)
     (orf * do.float()).sum().backward()
     valid = torch.ones(B, Sq, dtype=torch.bool, device=DEV)
     _close(o, orf, 2e-2, 2e-2, "attn o")
@@ -244,6 +244,8 @@ def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False):
     dict(B=1, Sq=64, Sk=192, Hq=2, Hkv=1, causal=True),
     dict(B=2, Sq=256, Sk=256, Hq=4, Hkv=2, causal=True, strided=True),
     dict(B=2, Sq=160, Sk=160, Hq=2, Hkv=2, causal=False, seqlens=[160, 77]),
+    dict(B=2, Sq=256, Sk=256, Hq=4, Hkv=2, causal=True, dropout_p=0.1),
+    dict(B=1, Sq=200, Sk=200, Hq=2, Hkv=2, causal=True, dropout_p=0.3),
 ])
 def test_flash_attention(case):
     _attn_case(**case)

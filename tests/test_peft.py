@@ -82,3 +82,20 @@ def test_double_quant_close_to_single():
     ids = torch.randint(0, 512, (1, 16))
     a, b = m1(ids)["logits"], m2(ids)["logits"]
     assert (a - b).norm() / a.norm() < 0.02
+
+
+def test_attention_dropout_reference_mask_statistics():
+    """CPU reference of the kernel's counter-hash dropout: keep-rate ~ 1-p, deterministic in the
+    seed, different across seeds, and the expectation of dropped attention equals no dropout."""
+    import torch
+    from gke_ray_train_amd.ops import _ref
+    keep = _ref.attn_dropout_keep(7, 2, 3, 64, 64, 0.25)
+    assert abs(keep.float().mean().item() - 0.75) < 0.02
+    assert torch.equal(keep, _ref.attn_dropout_keep(7, 2, 3, 64, 64, 0.25))
+    assert not torch.equal(keep, _ref.attn_dropout_keep(8, 2, 3, 64, 64, 0.25))
+    q = torch.randn(1, 32, 2, 16)
+    k = torch.randn(1, 32, 2, 16)
+    v = torch.randn(1, 32, 2, 16)
+    base = _ref.attention(q, k, v, causal=True)
+    avg = torch.stack([_ref.attention(q, k, v, causal=True, dropout_p=0.2, seed=s) for s in range(400)]).mean(0)
+    assert (avg - base).abs().max().item() < 0.15
