@@ -54,13 +54,18 @@ def save_pretrained(model: LlamaForCausalLM, path: str, max_shard_bytes: int = 5
                    "do_sample": False}, f, indent=2)
 
 
+def config_from_hf_dict(d: dict, name: Optional[str] = None) -> LlamaConfig:
+    fields = LlamaConfig.__dataclass_fields__
+    kw = {k: v for k, v in d.items() if k in fields}
+    if name is not None:
+        kw["name"] = name
+    return LlamaConfig(**kw)
+
+
 def load_config(path: str) -> LlamaConfig:
     with open(os.path.join(path, "config.json")) as f:
         d = json.load(f)
-    fields = LlamaConfig.__dataclass_fields__
-    kw = {k: v for k, v in d.items() if k in fields}
-    kw["name"] = os.path.basename(os.path.normpath(path))
-    return LlamaConfig(**kw)
+    return config_from_hf_dict(d, os.path.basename(os.path.normpath(path)))
 
 
 def from_pretrained(name_or_path: str, device=None, torch_dtype=torch.bfloat16, random_init_seed: Optional[int] = 0,

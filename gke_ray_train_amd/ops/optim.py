@@ -152,6 +152,8 @@ class OffloadedAdamW(FusedAdamW):
     2 x chunk x 8 bytes of optimizer state instead of 8 bytes per parameter.
     """
 
+    _host_states = True  # checkpoint loaders keep exp_avg / exp_avg_sq in pinned host memory
+
     def __init__(self, params, chunk_elems: int = 1 << 26, **kw):
         super().__init__(params, **kw)
         self.chunk = int(chunk_elems)
