@@ -319,8 +319,28 @@ class DataIterator:
                         local_shuffle_seed)
 
     def iter_torch_batches(self, batch_size: int = 256, dtypes=None, device="auto", collate_fn=None,
-                           drop_last: bool = False, **kw):
-        return _torch_batches(self.iter_batches(batch_size, drop_last=drop_last, **kw), dtypes, device, collate_fn)
+                           drop_last: bool = False, producer_process: bool = False, **kw):
+        """``producer_process=True`` runs the shard's read -> map -> batch pipeline in a separate
+        process that streams fixed-schema numeric batches through the native shared-memory ring
+        (runtime/shm_ring.py), keeping host-side data work off the training process."""
+        if producer_process:
+            batches = _process_batches(lambda: self.iter_batches(batch_size, drop_last=drop_last, **kw), batch_size)
+        else:
+            batches = self.iter_batches(batch_size, drop_last=drop_last, **kw)
+        return _torch_batches(batches, dtypes, device, collate_fn)
+
+
+def _process_batches(factory, batch_size: int):
+    """Batches of ``factory()`` produced in another process through an ShmRing (numeric fields
+    with fixed trailing shapes); falls back to in-process iteration otherwise."""
+    from ..runtime.shm_ring import RingBatchStream
+    probe = next(iter(factory()), None)
+    if probe is None:
+        return iter(())
+    if any(v.dtype == object for v in probe.values()):
+        return factory()
+    schema = {k: (v.dtype.str, (max(batch_size, v.shape[0]),) + tuple(v.shape[1:])) for k, v in probe.items()}
+    return iter(RingBatchStream(factory, schema))
 
 
 def _batches(blocks: Iterable[Block], batch_size, batch_format, drop_last, shuffle_buf=None, seed=None):

@@ -90,3 +90,18 @@ def test_pipeline_ops():
     tr, te = ds2.train_test_split(0.2)
     assert tr.count() == 40 and te.count() == 10
     assert len(ds2.split(3)) == 3
+
+
+def test_streaming_split_producer_process_matches_in_process():
+    """iter_torch_batches(producer_process=True): the shard's batches come from a producer process
+    through the native shared-memory ring and equal the in-process iteration."""
+    import numpy as np
+    from gke_ray_train_amd.data.pipeline import Dataset
+    ds = Dataset.from_numpy(np.arange(4000, dtype=np.int64).reshape(1000, 4)).map_batches(
+        lambda b: {"x": b["data"] * 2, "y": b["data"].sum(1)})
+    it = ds.streaming_split(2)[1]
+    a = list(it.iter_torch_batches(batch_size=64, device="cpu"))
+    b = list(it.iter_torch_batches(batch_size=64, device="cpu", producer_process=True))
+    assert len(a) == len(b) > 3
+    for u, v in zip(a, b):
+        assert (u["x"] == v["x"]).all() and (u["y"] == v["y"]).all()
