@@ -151,10 +151,10 @@ def train_loop_per_worker(config: dict):
 
 
 def load_config(path=None, overrides=None):
+    """fine_tune_config.json (same 35 keys) validated / typed by utils.config.FineTuneConfig."""
+    from gke_ray_train_amd.utils.config import FineTuneConfig, load_json_config, to_dict
     path = path or os.path.join(os.path.dirname(os.path.abspath(__file__)), "fine_tune_config.json")
-    with open(path) as f:
-        cfg = json.load(f)
-    cfg.update(overrides or {})
+    cfg = to_dict(load_json_config(FineTuneConfig, path, overrides))
     # the reference writes under its /mnt/pvc bucket mount: "pvc/..." resolves to the cluster storage
     pvc = os.environ.get("GRT_PVC") or os.environ.get("GRT_STORAGE_PATH")
     if pvc and str(cfg.get("OUTPUT_DIR_BASE", "")).startswith("pvc/"):
@@ -182,4 +182,15 @@ def main(config=None, num_workers=None, use_gpu=None):
 
 
 if __name__ == "__main__":
-    main()
+    import argparse
+    from gke_ray_train_amd.utils.config import num_workers_from_env, parse_overrides
+    ap = argparse.ArgumentParser(description="Llama SFT (QLoRA / LoRA / full) through TorchTrainer")
+    ap.add_argument("--config", default=None, help="JSON config (default: jobs/fine_tune_config.json)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE", help="override a config key")
+    ap.add_argument("--num-workers", type=int, default=None,
+                    help="default: NUM_NODES x NUM_GPUS_PER_NODE (GPUs per node = visible MI355X count)")
+    ap.add_argument("--cpu", action="store_true", help="gloo CPU workers (plumbing runs)")
+    a = ap.parse_args()
+    cfg = load_config(a.config, parse_overrides(a.set))
+    nw = a.num_workers or (num_workers_from_env() if not a.cpu else 1)
+    main(cfg, num_workers=nw, use_gpu=False if a.cpu else None)

@@ -168,10 +168,14 @@ def build_config(a):
         "raw_data_path": os.path.join(a.pvc, "datasets", "wikitext-2-raw", "wiki.train.tokens"),
         "processed_data_dir": os.path.join(a.pvc, "datasets", "wikitext-2-processed"),
         "storage_path_base_on_fuse": os.path.join(a.pvc, "ray_llm_training_runs"),
-        "experiment_name_for_tb": a.name, "test_run": not a.full, "dtype": a.dtype,
-        "synthetic_scale": a.data_scale, "max_windows": a.max_windows,
+        "experiment_name_for_tb": a.name, "test_run": not a.full,
     }
     cfg.update(PRESETS[a.preset])
+    # the reference's 19 keys, typed and validated (utils/config.py); then the framework's extras
+    from gke_ray_train_amd.utils.config import BasicLLMTrainConfig, from_dict, parse_overrides, to_dict
+    cfg.update(parse_overrides(getattr(a, "set", None)))
+    cfg = to_dict(from_dict(BasicLLMTrainConfig, cfg, strict=True))
+    cfg.update({"dtype": a.dtype, "synthetic_scale": a.data_scale, "max_windows": a.max_windows})
     return cfg
 
 
@@ -189,6 +193,8 @@ def main(argv=None):
     ap.add_argument("--name", default="wikitext2_manualTB_v1")
     ap.add_argument("--data-scale", type=float, default=1.0)
     ap.add_argument("--max-windows", type=int, default=None, help="override test_run's 16,000-window subset")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="override a train_loop_config key (e.g. --set lr=1e-4)")
     a = ap.parse_args(argv)
     use_gpu = not a.cpu and torch.cuda.device_count() > 0
     workers = a.workers or (torch.cuda.device_count() if use_gpu else 2)
