@@ -28,7 +28,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
-BUILD = ROOT / "build" / "native"
+BUILD = ROOT / "build" / ("native-checked" if os.environ.get("GRT_KERNEL_CHECKS", "0") == "1" else "native")
 ARCH = os.environ.get("GRT_OFFLOAD_ARCH", "gfx950")
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 
@@ -63,6 +63,12 @@ def _headers():
     return sorted((CSRC / "include").glob("*.h"))
 
 
+def _check_flags():
+    """``GRT_KERNEL_CHECKS=1``: compile the device-side bounds checks (GRT_DEVICE_CHECK in
+    grt_common.h) into the kernels — a debugging build, slower; objects go to build/native-checked."""
+    return ["-DGRT_KERNEL_CHECKS=1"] if os.environ.get("GRT_KERNEL_CHECKS", "0") == "1" else []
+
+
 def build_kernels(force=False, jobs=8, verbose=False) -> Path:
     tdir, abi = _torch_paths()
     BUILD.mkdir(parents=True, exist_ok=True)
@@ -76,7 +82,7 @@ def build_kernels(force=False, jobs=8, verbose=False) -> Path:
         objs.append(obj)
         if force or _newer(obj, [src, *hdrs]):
             cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-                   "-munsafe-fp-atomics", *inc, "-c", str(src), "-o", str(obj)]
+                   "-munsafe-fp-atomics", *_check_flags(), *inc, "-c", str(src), "-o", str(obj)]
             tasks.append(cmd)
     pyinc = sysconfig.get_paths()["include"]
     bind_src = CSRC / "bindings" / "ops.cpp"

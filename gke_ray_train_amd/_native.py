@@ -29,6 +29,30 @@ def _load_ext(name: str, path: Path):
     return mod
 
 
+class _SyncChecked:
+    """``GRT_DEBUG_SYNC=1``: every native op is followed by a device synchronize, so an illegal
+    access / kernel fault is reported at the op that launched it (the HIP_LAUNCH_BLOCKING /
+    AMD_SERIALIZE_KERNEL debugging mode of SURVEY §5.2) instead of at a later sync point."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        fn = getattr(self._mod, name)
+        if not callable(fn):
+            return fn
+
+        def wrapped(*a, **k):
+            import torch
+            out = fn(*a, **k)
+            try:
+                torch.cuda.synchronize()
+            except RuntimeError as e:
+                raise RuntimeError(f"native op {name} failed on the device: {e}") from e
+            return out
+        return wrapped
+
+
 def kernels():
     """Return the ``_C`` extension module; raise with a clear message if unavailable."""
     global _C, _C_err
@@ -46,6 +70,8 @@ def kernels():
             if _C_err is None:
                 try:
                     _C = _load_ext("_C", so)
+                    if os.environ.get("GRT_DEBUG_SYNC", "0") == "1":
+                        _C = _SyncChecked(_C)
                 except Exception as e:
                     _C_err = e
     if _C is None:

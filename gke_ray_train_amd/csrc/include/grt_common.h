@@ -11,6 +11,18 @@ namespace grt {
 
 constexpr int kWave = 64;
 
+// Device-side bounds / invariant checks, compiled in only for the GRT_KERNEL_CHECKS=1 debugging
+// build (python -m gke_ray_train_amd._build with that env var): a failed check traps the wave so
+// the fault is reported at the offending kernel (rocprofv3 / dmesg) instead of corrupting memory.
+#if defined(GRT_KERNEL_CHECKS) && GRT_KERNEL_CHECKS
+#define GRT_DEVICE_CHECK(cond) \
+  do {                         \
+    if (!(cond)) __builtin_trap(); \
+  } while (0)
+#else
+#define GRT_DEVICE_CHECK(cond) ((void)0)
+#endif
+
 typedef __bf16 bf16;
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

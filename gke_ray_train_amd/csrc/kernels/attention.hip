@@ -104,6 +104,7 @@ __global__ __launch_bounds__(FNT, 2) void attn_fwd_kernel(const AttnParams p) {
   const int bh = blockIdx.x % BH;
   const int b = bh / p.Hq, hq = bh % p.Hq;
   const int hkv = hq / (p.Hq / p.Hkv);
+  GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && qblk >= 0);
   const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
   const int off = p.Sk - p.Sq;  // bottom-right aligned causal mask
   const int q0 = qblk * FBM, qw0 = q0 + w * 32;
@@ -296,6 +297,7 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
   const int bhk = blockIdx.x % (p.B * p.Hkv);
   const int b = bhk / p.Hkv, hkv = bhk % p.Hkv;
   const int grp = p.Hq / p.Hkv;
+  GRT_DEVICE_CHECK(kblk >= 0 && grp * p.Hkv == p.Hq);
   const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
   const int off = p.Sk - p.Sq;
   const int k0 = kblk * BBN;

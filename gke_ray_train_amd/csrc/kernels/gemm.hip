@@ -91,6 +91,7 @@ __global__ __launch_bounds__(GNT, 1) void gemm_tt_kernel(const GemmTTParams p) {
   const int grp = wg / per_group, first = grp * kGroupRows;
   const int gsize = min(nP - first, kGroupRows);
   const int tp = first + (wg % per_group) % gsize, tq = (wg % per_group) / gsize;
+  GRT_DEVICE_CHECK(tp < nP && tq < nQ && wg < nwg);
   const int p0 = tp * TP, q0 = tq * TQ;
 
   // ---- LDS ring: NSLOT slots x 32 KiB; slot k holds one 32-token half-step of four 128-column
