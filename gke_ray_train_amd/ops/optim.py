@@ -183,45 +183,58 @@ class OffloadedAdamW(FusedAdamW):
                 hb.copy_(torch.tensor([lr, b1, b2, eps, wd, 1.0 - b1 ** step, 1.0 - b2 ** step, 1.0]), non_blocking=True)
                 self._stream_update(p, st, hb, grad_scale)
 
+    NSLOT = 3
+
     def _stream_update(self, p, st, hb, grad_scale):
+        """H2D on one stream, D2H on another (the host link is full duplex), the update on the
+        compute stream; NSLOT device staging slots so chunk i+1 uploads and chunk i-1 downloads
+        while chunk i is updated."""
         C = _native.kernels()
         dev = p.device
         if self._copy_stream is None:
-            self._copy_stream = torch.cuda.Stream(dev)
-            self._stage = [(torch.empty(self.chunk, device=dev), torch.empty(self.chunk, device=dev)) for _ in range(2)]
-        cs, comp = self._copy_stream, torch.cuda.current_stream(dev)
+            self._copy_stream = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+            self._stage = [(torch.empty(self.chunk, device=dev), torch.empty(self.chunk, device=dev))
+                           for _ in range(self.NSLOT)]
+        up, down = self._copy_stream
+        comp = torch.cuda.current_stream(dev)
         pf, gf = p.data.view(-1), p.grad.view(-1)
         m_h, v_h = st["exp_avg"], st["exp_avg_sq"]
         n = pf.numel()
         chunks = [(s, min(n, s + self.chunk)) for s in range(0, n, self.chunk)]
         up_done = [torch.cuda.Event() for _ in chunks]
         upd_done = [torch.cuda.Event() for _ in chunks]
+        down_done = [torch.cuda.Event() for _ in chunks]
+        entry = torch.cuda.Event()
+        entry.record(comp)  # grads / params of this step are ready
 
         def upload(i):
             s, e = chunks[i]
-            mb, vb = self._stage[i % 2]
-            with torch.cuda.stream(cs):
-                if i >= 2:
-                    cs.wait_event(upd_done[i - 2])  # slot reuse: previous user's update done
+            mb, vb = self._stage[i % self.NSLOT]
+            with torch.cuda.stream(up):
+                up.wait_event(entry)
+                if i >= self.NSLOT:
+                    up.wait_event(down_done[i - self.NSLOT])  # slot free: its previous chunk is home
                 mb[: e - s].copy_(m_h[s:e], non_blocking=True)
                 vb[: e - s].copy_(v_h[s:e], non_blocking=True)
-                up_done[i].record(cs)
+                up_done[i].record(up)
 
-        if chunks:
-            upload(0)
+        for i in range(min(self.NSLOT - 1, len(chunks))):
+            upload(i)
         for i, (s, e) in enumerate(chunks):
-            if i + 1 < len(chunks):
-                upload(i + 1)
+            if i + self.NSLOT - 1 < len(chunks):
+                upload(i + self.NSLOT - 1)
             comp.wait_event(up_done[i])
-            mb, vb = self._stage[i % 2]
+            mb, vb = self._stage[i % self.NSLOT]
             C.adamw(pf[s:e], gf[s:e], mb[: e - s], vb[: e - s], None, hb,
                     None if grad_scale is None else grad_scale.buf)
             upd_done[i].record(comp)
-            with torch.cuda.stream(cs):
-                cs.wait_event(upd_done[i])
+            with torch.cuda.stream(down):
+                down.wait_event(upd_done[i])
                 m_h[s:e].copy_(mb[: e - s], non_blocking=True)
                 v_h[s:e].copy_(vb[: e - s], non_blocking=True)
-        comp.wait_stream(cs)
+                down_done[i].record(down)
+        comp.wait_stream(down)  # host states complete before the next step reads them
+        comp.wait_stream(up)
 
 
 def make_optimizer(name: str, params, lr: float, weight_decay: float, betas=(0.9, 0.999), eps=1e-8,
