@@ -131,5 +131,7 @@ if __name__ == "__main__":
         res += attention(B=8, S=1024, H=32, Hkv=8)
     if a.what in ("all", "mem"):
         res += memops()
+    if a.what == "normbwd":  # A/B of the rmsnorm backward grid (env is read once per process)
+        res += [r for r in memops() if r["op"] == "rmsnorm_bwd"]
     for r in res:
         print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in r.items()}))
