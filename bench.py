@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--metrics-jsonl", default="", help="per-step metrics (phase breakdown, MFU, HBM) -> JSONL; "
                     "adds one host sync per step, so it is off for the headline number")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--no-tuned-gemm", action="store_true", help="library-default GEMM solutions (A/B)")
     ap.add_argument("--backend", default="", help="process-group backend (default: nccl = RCCL on GPU, gloo on CPU)")
     return ap.parse_args()
 
@@ -120,6 +121,10 @@ def main():
 
     torch.manual_seed(1234)
     dtype = torch.float32 if cpu else torch.bfloat16
+    tuned = False
+    if not cpu and not a.no_tuned_gemm:
+        from gke_ray_train_amd.ops.gemm_tuning import enable_tuned_gemms
+        tuned = enable_tuned_gemms()
     cfg = get_config(a.model)
     model, eng, call, opt = build(a, cfg, dev, dtype, world)
     model.train()
@@ -248,7 +253,8 @@ def main():
             "data": "synthetic Wikitext-2-shaped token stream (Zipf ids) via the streaming loader; random-init weights",
             "config": {"model": cfg.name, "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": par,
                        "micro_batch": mb, "grad_accum": accum, "optimizer": "fused AdamW fp32 states",
-                       "max_grad_norm": a.max_grad_norm, "activation_checkpointing": a.checkpointing},
+                       "max_grad_norm": a.max_grad_norm, "activation_checkpointing": a.checkpointing,
+                       "library_gemms": "offline-tuned" if tuned else "default"},
             "samples_per_sec": round(tps / a.seq, 2),
             "mfu_bf16_dense": round(mfu, 4),
             "loss": round(float(loss.item()) * accum, 4),

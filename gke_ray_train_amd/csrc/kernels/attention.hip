@@ -24,6 +24,8 @@
 //     (256-byte row segments, the full-rate shape of MI355X_MICROARCH.md §Global float atomics).
 //   All LDS tiles use the dual row-read / transposed-read XOR image of cdna_hip_programming.md
 //   T10 (b), conflict-free for both the ds_read_b128 row reads and the tr_b16 reads.
+#include <stdlib.h>
+
 #include "grt_common.h"
 #include "grt_kernels.h"
 
@@ -278,17 +280,20 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p
 
 // dK / dV kernel: one workgroup = 128 keys of one (batch, kv head), 32 keys per wave with the key on
 // the MFMA lane; K and V fragments stay in VGPRs for the whole sweep over the group's query heads
-// x 32-row query tiles (Q / dO tiles double-buffered in LDS, one barrier per tile). No atomics:
-// dK and dV are complete in registers at the end.
-template <bool DROP>
+// x (32 * NQ)-row query tiles (Q / dO tiles double-buffered in LDS, one barrier per tile). No
+// atomics: dK and dV are complete in registers at the end. NQ = 2 gives every wave four independent
+// MFMA accumulation chains per tile (S and dP for two 32-row halves) and halves the barriers.
+template <bool DROP, int NQ>
 __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdParams P) {
   const AttnParams& p = P.f;
-  constexpr int QB = BBM * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[4 * QB + 2 * 2 * BBM * 4];
+  constexpr int TM = BBM * NQ;           // query rows per tile
+  constexpr int QB = TM * D * 2;
+  constexpr int LD = TM * kChunks / BNT;  // 16-byte chunks per thread per operand
+  __shared__ __attribute__((aligned(16))) char smem[4 * QB + 2 * 2 * TM * 4];
   auto Ql = [&](int buf) -> char* { return smem + buf * QB; };
   auto dOl = [&](int buf) -> char* { return smem + (2 + buf) * QB; };
-  float* lsel = (float*)(smem + 4 * QB);  // [2][32]
-  float* dell = lsel + 2 * BBM;           // [2][32]
+  float* lsel = (float*)(smem + 4 * QB);  // [2][TM]
+  float* dell = lsel + 2 * TM;            // [2][TM]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int g = lane >> 4, l16 = lane & 15;
@@ -327,18 +332,18 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
   int qstart = 0;
   if (p.causal) qstart = max(0, k0 - off);
   qstart = (qstart / BBM) * BBM;
-  const int nqt = qstart < p.Sq ? (p.Sq - qstart + BBM - 1) / BBM : 0;
+  const int nqt = qstart < p.Sq ? (p.Sq - qstart + TM - 1) / TM : 0;
   const int total = (k0 < sk) ? nqt * grp : 0;
 
-  bf16x8 qreg[2], oreg[2];
+  bf16x8 qreg[LD], oreg[LD];
   float lse_r = 0.f, del_r = 0.f;
   auto load_q = [&](int it) {
     const int hq = hkv * grp + it / nqt;
-    const int qt = qstart + (it % nqt) * BBM;
+    const int qt = qstart + (it % nqt) * TM;
     const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + (int64_t)hq * p.q_hs;
     const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + (int64_t)hq * P.do_hs;
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < LD; ++r) {
       const int i = tid + BNT * r, row = i / kChunks, ch = i % kChunks, q = qt + row;
       if (q < p.Sq) {
         qreg[r] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)q * p.q_ss + ch * 8);
@@ -348,7 +353,7 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
         oreg[r] = bf16x8{};
       }
     }
-    if (tid < BBM) {
+    if (tid < TM) {
       const int q = qt + tid;
       const int64_t ri = ((int64_t)b * p.Hq + hq) * p.Sq + q;
       lse_r = q < p.Sq ? p.lse[ri] * kLog2e : INFINITY;
@@ -357,12 +362,12 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
   };
   auto store_q = [&](int buf) {
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < LD; ++r) {
       const int i = tid + BNT * r, row = i / kChunks, ch = i % kChunks;
       *reinterpret_cast<bf16x8*>(Ql(buf) + img_off(row, ch)) = qreg[r];
       *reinterpret_cast<bf16x8*>(dOl(buf) + img_off(row, ch)) = oreg[r];
     }
-    if (tid < BBM) { lsel[buf * BBM + tid] = lse_r; dell[buf * BBM + tid] = del_r; }
+    if (tid < TM) { lsel[buf * TM + tid] = lse_r; dell[buf * TM + tid] = del_r; }
   };
 
   if (total > 0) { load_q(0); store_q(0); }
@@ -370,52 +375,61 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
 
   for (int it = 0; it < total; ++it) {
     const int cur = it & 1;
-    const int qt = qstart + (it % nqt) * BBM;
+    const int qt = qstart + (it % nqt) * TM;
     if (it + 1 < total) load_q(it + 1);
-    const bool skip = p.causal && (kw0 > qt + BBM - 1 + off);   // all 32 keys after every q row
-    if (!skip) {
-      f32x16 s = f32x16{}, dp = f32x16{};
+    if (!(p.causal && (kw0 > qt + TM - 1 + off))) {  // else: all 32 keys after every row of the tile
+      f32x16 s[NQ], dp[NQ];
 #pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) {
-        s = mfma32(lds_row_read(Ql(cur), l32, 2 * ks + h), kf[ks], s);
-        dp = mfma32(lds_row_read(dOl(cur), l32, 2 * ks + h), vf[ks], dp);
-      }
-      const bool need_mask = (k0 + BBN > sk) || (p.causal && kw0 + 31 > qt + off) || (qt + BBM > p.Sq);
+      for (int n = 0; n < NQ; ++n) { s[n] = f32x16{}; dp[n] = f32x16{}; }
 #pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        const f32x4 ls = *reinterpret_cast<const f32x4*>(lsel + cur * BBM + 8 * gg + 4 * h);
-        const f32x4 de = *reinterpret_cast<const f32x4*>(dell + cur * BBM + 8 * gg + 4 * h);
+      for (int ks = 0; ks < D / 16; ++ks)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int r = 4 * gg + j;
-          const int q = qt + 8 * gg + 4 * h + j;
-          float pv = fast_exp2(s[r] * c - ls[j]);
-          if (need_mask && (mykey >= sk || q >= p.Sq || (p.causal && mykey > q + off))) pv = 0.f;
-          if (DROP) {
-            const uint32_t bhq = (uint32_t)(b * p.Hq + hkv * grp + it / nqt);
-            const float z = drop_factor(p, bhq, q, mykey);
-            s[r] = pv * z;                   // dV uses the dropped probabilities
-            dp[r] = pv * (dp[r] * z - de[j]);
-          } else {
-            s[r] = pv;
-            dp[r] = pv * (dp[r] - de[j]);
+        for (int n = 0; n < NQ; ++n) {
+          s[n] = mfma32(lds_row_read(Ql(cur), n * 32 + l32, 2 * ks + h), kf[ks], s[n]);
+          dp[n] = mfma32(lds_row_read(dOl(cur), n * 32 + l32, 2 * ks + h), vf[ks], dp[n]);
+        }
+#pragma unroll
+      for (int n = 0; n < NQ; ++n) {
+        const int qn = qt + n * 32;
+        const bool need_mask = (k0 + BBN > sk) || (p.causal && kw0 + 31 > qn + off) || (qn + 32 > p.Sq);
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          const f32x4 ls = *reinterpret_cast<const f32x4*>(lsel + cur * TM + n * 32 + 8 * gg + 4 * h);
+          const f32x4 de = *reinterpret_cast<const f32x4*>(dell + cur * TM + n * 32 + 8 * gg + 4 * h);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int r = 4 * gg + j;
+            const int q = qn + 8 * gg + 4 * h + j;
+            float pv = fast_exp2(s[n][r] * c - ls[j]);
+            if (need_mask && (mykey >= sk || q >= p.Sq || (p.causal && mykey > q + off))) pv = 0.f;
+            if (DROP) {
+              const uint32_t bhq = (uint32_t)(b * p.Hq + hkv * grp + it / nqt);
+              const float z = drop_factor(p, bhq, q, mykey);
+              s[n][r] = pv * z;                   // dV uses the dropped probabilities
+              dp[n][r] = pv * (dp[n][r] * z - de[j]);
+            } else {
+              s[n][r] = pv;
+              dp[n][r] = pv * (dp[n][r] - de[j]);
+            }
           }
         }
       }
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const bf16x8 pb = pack8(s, 8 * st);
-        const bf16x8 sb = pack8(dp, 8 * st);
-        const int kk = 16 * st + 4 * h;
+      for (int n = 0; n < NQ; ++n)
 #pragma unroll
-        for (int db = 0; db < 4; ++db) {
-          const int c0 = db * 32 + (g & 1) * 16;
-          const bf16x8 oa = cat(lds_tr_read(dOl(cur), kk, c0, l16), lds_tr_read(dOl(cur), kk + 8, c0, l16));
-          dv[db] = mfma32(oa, pb, dv[db]);
-          const bf16x8 qa = cat(lds_tr_read(Ql(cur), kk, c0, l16), lds_tr_read(Ql(cur), kk + 8, c0, l16));
-          dk[db] = mfma32(qa, sb, dk[db]);
+        for (int st = 0; st < 2; ++st) {
+          const bf16x8 pb = pack8(s[n], 8 * st);
+          const bf16x8 sb = pack8(dp[n], 8 * st);
+          const int kk = n * 32 + 16 * st + 4 * h;
+#pragma unroll
+          for (int db = 0; db < 4; ++db) {
+            const int c0 = db * 32 + (g & 1) * 16;
+            const bf16x8 oa = cat(lds_tr_read(dOl(cur), kk, c0, l16), lds_tr_read(dOl(cur), kk + 8, c0, l16));
+            dv[db] = mfma32(oa, pb, dv[db]);
+            const bf16x8 qa = cat(lds_tr_read(Ql(cur), kk, c0, l16), lds_tr_read(Ql(cur), kk + 8, c0, l16));
+            dk[db] = mfma32(qa, sb, dk[db]);
+          }
         }
-      }
     }
     if (it + 1 < total) store_q(cur ^ 1);
     __syncthreads();
@@ -595,11 +609,14 @@ void attn_bwd(const AttnBwdParams& p, hipStream_t s) {
   const int nkb = (p.f.Sk + BBN - 1) / BBN;
   const int nqb = (p.f.Sq + FBM - 1) / FBM;
   const dim3 g1((unsigned)(nkb * p.f.B * p.f.Hkv)), g2((unsigned)(nqb * p.f.B * p.f.Hq));
+  static const int nq = [] { const char* e = getenv("GRT_ATTN_BWD_NQ"); return e ? atoi(e) : 2; }();
   if (p.f.drop_thresh) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(BNT), 0, s, p);
+    if (nq == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 1>), g1, dim3(BNT), 0, s, p);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 2>), g1, dim3(BNT), 0, s, p);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(FNT), 0, s, p);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(BNT), 0, s, p);
+    if (nq == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 1>), g1, dim3(BNT), 0, s, p);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 2>), g1, dim3(BNT), 0, s, p);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(FNT), 0, s, p);
   }
 }
