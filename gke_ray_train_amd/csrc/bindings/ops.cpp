@@ -436,6 +436,42 @@ Tensor nf4_dequantize(const Tensor& q, const Tensor& absmax, int64_t n, int64_t 
   return w;
 }
 
+// ------------------------------------------------------------------ embedding
+Tensor embedding_fwd(const Tensor& ids, const Tensor& w) {
+  check_contig(ids, "ids");
+  check_contig(w, "weight");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && w.dim() == 2, "embedding: int64 ids, 2-D weight");
+  const int64_t d = w.size(1);
+  TORCH_CHECK(d % 8 == 0, "embedding: row width must be a multiple of 8");
+  c10::OptionalDeviceGuard g(w.device());
+  auto out = at::empty({ids.numel(), d}, w.options());
+  grt::embedding_fwd(dtype_of(w), ids.data_ptr<int64_t>(), w.data_ptr(), out.data_ptr(), ids.numel(), (int)d,
+                     w.size(0), cur_stream(w));
+  return out;
+}
+
+void embedding_bwd(const Tensor& dy, const Tensor& ids, const Tensor& dw, bool accumulate) {
+  check_contig(dy, "dy");
+  check_contig(dw, "dw");
+  TORCH_CHECK(ids.scalar_type() == at::kLong, "embedding_bwd: int64 ids");
+  TORCH_CHECK(dy.dim() == 2 && dw.dim() == 2 && dy.size(1) == dw.size(1) && dy.size(0) == ids.numel(),
+              "embedding_bwd: shapes");
+  TORCH_CHECK(dy.scalar_type() == dw.scalar_type(), "embedding_bwd: dtype");
+  c10::OptionalDeviceGuard g(dy.device());
+  const int64_t V = dw.size(0);
+  auto flat = ids.reshape({-1});
+  auto sorted = flat.sort();
+  auto vals = std::get<0>(sorted);
+  auto order = std::get<1>(sorted).contiguous();
+  // segment bounds of every vocabulary row by binary search: no unique() (its output size would
+  // force a device->host sync in the middle of the backward)
+  auto rows = at::arange(V, vals.options());
+  auto row_start = at::searchsorted(vals, rows, /*out_int32=*/true, /*right=*/false);
+  auto row_end = at::searchsorted(vals, rows, /*out_int32=*/true, /*right=*/true);
+  grt::embedding_bwd(dtype_of(dy), dy.data_ptr(), order.data_ptr<int64_t>(), row_start.data_ptr<int32_t>(),
+                     row_end.data_ptr<int32_t>(), dw.data_ptr(), V, (int)dy.size(1), accumulate, cur_stream(dy));
+}
+
 // ------------------------------------------------------------------ weight-gradient GEMM
 // out[P][Q] (+)= x[R][P]^T @ y[R][Q]  (dW = dY^T X); returns false when the shape is unsupported
 bool gemm_wgrad(const Tensor& x, const Tensor& y, const Tensor& out, bool accumulate, int64_t mode) {
@@ -489,6 +525,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
   m.def("gemm_wgrad", &gemm_wgrad, py::arg("x"), py::arg("y"), py::arg("out"), py::arg("accumulate"),
         py::arg("mode") = 0);
 }

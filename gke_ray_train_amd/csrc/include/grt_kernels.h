@@ -112,6 +112,15 @@ void nf4_quantize(DType dt, const void* w, uint8_t* q, float* absmax, int64_t n,
 void nf4_dequantize(DType dt, const uint8_t* q, const float* absmax, void* w, int64_t n,
                     int blocksize, hipStream_t s);
 
+// ---------------- token embedding (embedding.hip) ----------------
+// out[i] = w[ids[i]]; rows of d elements (d % 8 == 0 for bf16, % 4 for fp32)
+void embedding_fwd(DType dt, const int64_t* ids, const void* w, void* out, int64_t n, int d, int64_t V,
+                   hipStream_t s);
+// dW[v] (+)= sum_{k in [row_start[v], row_end[v])} dy[order[k]]; empty rows are zeroed (overwrite)
+// or untouched (accumulate).
+void embedding_bwd(DType dt, const void* dy, const int64_t* order, const int32_t* row_start, const int32_t* row_end,
+                   void* dw, int64_t V, int d, bool accumulate, hipStream_t s);
+
 // ---------------- weight-gradient GEMM (gemm.hip) ----------------
 // C[P][Q] (+)= sum_r X[r][p] * Y[r][q]; X [R][P], Y [R][Q], C [P][Q] row-major bf16.
 struct GemmTTParams {

@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import ops
-from ..ops.linear import Linear
+from ..ops.linear import Embedding, Linear
 
 
 @dataclass
@@ -121,7 +121,7 @@ class BasicLLM(nn.Module):
         super().__init__()
         self.config = BasicLLMConfig(vocab_size, embed_dim, num_heads, num_layers, hidden_dim, max_seq_len, dropout)
         self.embed_dim = embed_dim
-        self.token_embedding = nn.Embedding(vocab_size, embed_dim, device=device, dtype=dtype)
+        self.token_embedding = Embedding(vocab_size, embed_dim, device=device, dtype=dtype)
         self.positional_encoding = PositionalEncoding(embed_dim, max_seq_len)
         self.transformer_decoder = _Encoder(
             [EncoderLayer(embed_dim, num_heads, hidden_dim, dropout, device, dtype) for _ in range(num_layers)])

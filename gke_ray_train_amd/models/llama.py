@@ -28,7 +28,7 @@ import torch.nn as nn
 import torch.utils.checkpoint as ckpt
 
 from .. import ops
-from ..ops.linear import Linear
+from ..ops.linear import Embedding, Linear
 from ..ops import _ref
 
 
@@ -192,7 +192,7 @@ class LlamaDecoderLayer(nn.Module):
 class LlamaModel(nn.Module):
     def __init__(self, cfg: LlamaConfig, device=None, dtype=None):
         super().__init__()
-        self.embed_tokens = nn.Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
+        self.embed_tokens = Embedding(cfg.vocab_size, cfg.hidden_size, device=device, dtype=dtype)
         self.layers = nn.ModuleList([LlamaDecoderLayer(cfg, device, dtype) for _ in range(cfg.num_hidden_layers)])
         self.norm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, device, dtype)
 

@@ -51,6 +51,10 @@ class GradSlot:
 
 
 _WGRAD_NATIVE = os.environ.get("GRT_WGRAD_GEMM", "1") != "0"
+# Opt-in: the one-pass backward gives each vocabulary row to one wave, which serialises on the
+# hottest tokens of a Zipf-distributed batch (measured +6.5 ms per Llama-2-7B step vs torch's
+# partial-segment scheme, tools/gpu_emb_ab.sh); the forward gather and the uniform-id case are fine.
+_NATIVE_EMBEDDING = os.environ.get("GRT_NATIVE_EMBEDDING", "0") == "1"
 
 
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor = None, accumulate: bool = False) -> torch.Tensor:
@@ -125,3 +129,49 @@ class Linear(nn.Linear):
             from .fused import lm_head_cross_entropy
             return lm_head_cross_entropy(x, self.weight, labels, bias=self.bias, ignore_index=ignore_index)
         return linear(x, self.weight, self.bias)
+
+
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, w):
+        from .. import _native
+        ctx.save_for_backward(ids)
+        ctx.wshape = w.shape
+        ctx.w = w
+        return _native.kernels().embedding_fwd(ids.reshape(-1).contiguous(), w).view(*ids.shape, w.shape[1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        from .. import _native
+        (ids,) = ctx.saved_tensors
+        C = _native.kernels()
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        w = ctx.w
+        slot = getattr(w, "_grt_slot", None)
+        if slot is not None:  # write dW straight into the data-parallel gradient buffer
+            slot.write(lambda v: C.embedding_bwd(dy2, ids, v, False), lambda v: C.embedding_bwd(dy2, ids, v, True))
+            slot.notify(w)
+            return None, None
+        dw = torch.empty(ctx.wshape, device=dy.device, dtype=dy.dtype)
+        C.embedding_bwd(dy2, ids, dw, False)
+        return None, dw
+
+
+def embedding(ids, weight):
+    """Token embedding: HIP gather forward + one-pass segmented backward on MI355X (bf16/fp32)."""
+    if _NATIVE_EMBEDDING and weight.is_cuda and weight.dtype in (torch.bfloat16, torch.float32) \
+            and weight.shape[1] % 8 == 0:
+        if weight.requires_grad and torch.is_grad_enabled():
+            return _Embedding.apply(ids, weight)
+        from .. import _native
+        return _native.kernels().embedding_fwd(ids.reshape(-1).contiguous(), weight).view(*ids.shape, weight.shape[1])
+    return F.embedding(ids, weight)
+
+
+class Embedding(nn.Embedding):
+    """nn.Embedding (same parameter / state_dict) routed through ``ops.embedding``."""
+
+    def forward(self, ids):
+        if self.padding_idx is not None or self.max_norm is not None or self.sparse:
+            return super().forward(ids)
+        return embedding(ids, self.weight)

@@ -34,8 +34,18 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
-from ..ops.linear import GradSlot, Linear as _DirectLinear
+from ..ops.linear import Embedding as _DirectEmbedding, GradSlot, Linear as _DirectLinear
 from .comm import plan_bucket_bytes
+
+
+def shared_param_ids(module: nn.Module) -> set:
+    """ids of parameters owned by more than one module (tied embeddings): their gradient has two
+    producers, so they must not use the single-writer direct gradient slots."""
+    seen, shared = set(), set()
+    for m in module.modules():
+        for p in m.parameters(recurse=False):
+            (shared if id(p) in seen else seen).add(id(p))
+    return shared
 
 
 def _no_decay(name: str, p: torch.Tensor) -> bool:
@@ -97,11 +107,12 @@ class DistributedDataParallel(nn.Module):
         # weights whose backward GEMM writes straight into the flat gradient buffer
         self._direct = set()
         for m in module.modules():
-            if isinstance(m, _DirectLinear) and m.weight.requires_grad:
+            if isinstance(m, (_DirectLinear, _DirectEmbedding)) and m.weight.requires_grad:
                 self._direct.add(id(m.weight))
         lm_head = getattr(module, "lm_head", None)
         if isinstance(lm_head, nn.Linear) and lm_head.weight.requires_grad:
             self._direct.add(id(lm_head.weight))
+        self._direct -= shared_param_ids(module)  # tied weights: two writers -> AccumulateGrad path
         named = []
         seen = set()
         for n, p in module.named_parameters():

@@ -295,9 +295,14 @@ class FullyShardedDataParallel(nn.Module):
     def _attach_slots(self, u: _Unit):
         # Slots exist from construction on, so the forward takes the same (direct-grad) code path
         # in the original pass and in an activation-checkpoint recompute.
+        shared = getattr(self, "_shared_ids", None)
+        if shared is None:
+            from .ddp import shared_param_ids
+            shared = self._shared_ids = shared_param_ids(self.module)
         for p in u.params:
             sl = GradSlot(torch.empty(0, dtype=self.dtype, device=self.device), self._param_ready)
-            p._grt_slot = sl
+            if id(p) not in shared:  # tied weights keep the AccumulateGrad path (two producers)
+                p._grt_slot = sl
             p._grt_unit = u
             u.slots[id(p)] = sl
             p._grt_fsdp_hook = p.register_post_accumulate_grad_hook(self._acc_hook)

@@ -1,0 +1,6 @@
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -rf -x > gpurun_out/s6_gpu_tests.log 2>&1 || { echo "gpu tests rc=$?"; tail -30 gpurun_out/s6_gpu_tests.log; exit 1; }
+tail -2 gpurun_out/s6_gpu_tests.log
+timeout -k 10 400 python bench.py --steps 8 --warmup 2 > gpurun_out/s6_bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/s6_bench.log; exit 1; }
+tail -1 gpurun_out/s6_bench.log | cut -c1-220
