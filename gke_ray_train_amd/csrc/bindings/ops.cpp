@@ -239,6 +239,23 @@ Tensor dropout_bwd(const Tensor& dy, const Tensor& mask, double p) {
                    cur_stream(dy));
   return dx;
 }
+// mask-free variants: forward stores no mask; backward regenerates it and can accumulate into dx
+Tensor dropout_fwd_seeded(const Tensor& x, double p, int64_t seed, int64_t offset) {
+  check_contig(x, "x");
+  c10::OptionalDeviceGuard g(x.device());
+  auto y = at::empty_like(x);
+  grt::dropout_fwd(dtype_of(x), x.data_ptr(), y.data_ptr(), nullptr, x.numel(), (float)p, (uint64_t)seed,
+                   (uint64_t)offset, cur_stream(x));
+  return y;
+}
+void dropout_bwd_seeded(const Tensor& dy, const Tensor& dx, double p, int64_t seed, int64_t offset, bool accumulate) {
+  check_contig(dy, "dy");
+  check_contig(dx, "dx");
+  TORCH_CHECK(dy.numel() == dx.numel() && dy.scalar_type() == dx.scalar_type(), "dropout_bwd_seeded: shapes");
+  c10::OptionalDeviceGuard g(dy.device());
+  grt::dropout_bwd(dtype_of(dy), dy.data_ptr(), nullptr, dx.data_ptr(), dy.numel(), (float)p, cur_stream(dy),
+                   (uint64_t)seed, (uint64_t)offset, accumulate);
+}
 
 // ------------------------------------------------------------------ cross entropy
 std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore_index) {
@@ -511,6 +528,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scale_add_pe", &scale_add_pe);
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
+  m.def("dropout_fwd_seeded", &dropout_fwd_seeded);
+  m.def("dropout_bwd_seeded", &dropout_bwd_seeded);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("sumsq_blocks", &sumsq_blocks);

@@ -51,8 +51,10 @@ void scale_add_pe(DType dt, const void* emb, const float* pe, void* out, int64_t
 // Dropout with a counter-based hash RNG; mask bytes written for backward.
 void dropout_fwd(DType dt, const void* x, void* y, uint8_t* mask, int64_t n, float p, uint64_t seed,
                  uint64_t offset, hipStream_t s);
+// mask may be null in both: fwd then stores no mask, bwd regenerates keep(i) from (seed, offset);
+// bwd with accumulate adds into dx.
 void dropout_bwd(DType dt, const void* dy, const uint8_t* mask, void* dx, int64_t n, float p,
-                 hipStream_t s);
+                 hipStream_t s, uint64_t seed = 0, uint64_t offset = 0, bool accumulate = false);
 
 // ---------------- cross entropy (cross_entropy.hip) ----------------
 void cross_entropy_fwd(DType dt, const void* logits, int64_t ld, const int64_t* labels, float* loss,

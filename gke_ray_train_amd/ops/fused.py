@@ -151,15 +151,21 @@ class _Dropout(torch.autograd.Function):
 _dropout_counter = [0]
 
 
+def dropout_seed_offset(x):
+    """(seed, offset) for a counter-based dropout over ``x``: seed from the device generator, a
+    running element offset so successive calls draw disjoint counter ranges."""
+    seed = int(torch.cuda.default_generators[x.device.index or 0].initial_seed()) & 0xFFFFFF
+    off = _dropout_counter[0]
+    _dropout_counter[0] += x.numel()
+    return seed, off
+
+
 def dropout(x, p, training=True, seed=None):
     if not training or p == 0.0:
         return x
     if _gpu(x):
-        if seed is None:
-            seed = int(torch.cuda.default_generators[x.device.index or 0].initial_seed()) & 0xFFFFFF
-        off = _dropout_counter[0]
-        _dropout_counter[0] += x.numel()
-        return _Dropout.apply(x, p, seed, off)
+        s, off = dropout_seed_offset(x)
+        return _Dropout.apply(x, p, s if seed is None else seed, off)
     return torch.nn.functional.dropout(x, p, training=True)
 
 

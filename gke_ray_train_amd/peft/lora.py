@@ -6,10 +6,13 @@ target_modules=[q,k,v,o,gate,up,down]_proj)`` passed to SFTTrainer, then ``merge
 
 The model keeps q/k/v and gate/up as ONE fused base GEMM each. A LoRA wrapper over a fused
 projection holds one (A, B) pair per targeted HF sub-projection; the A matrices of all targeted
-slices are concatenated so the down-projection is ONE GEMM ``x @ A_cat^T`` ([tokens, r * k]), and
-the up-projection is one GEMM against a block-diagonal ``B`` assembled on the fly (k x r columns,
-< 5 % of the base GEMM's FLOPs at r = 64). The adapter output is added to the base output in one
-elementwise pass. Parameter names on disk follow HF PEFT
+slices are concatenated so the down-projection is ONE GEMM ``x @ A_cat^T`` ([tokens, r * k]).
+On MI355X the whole adapted projection is one autograd op (``_LoraFn``): each target's
+up-projection ``h_i @ B_i^T`` is accumulated into its column block of the base output by the GEMM
+epilogue (beta = 1, alpha = scaling), the input dropout is the counter-based kernel (no mask
+stored, regenerated in the backward) and the adapter's input gradient is added into the base dX
+by the dropout-backward kernel in place — no separate add kernels, no block-diagonal B, no
+autograd gradient accumulation. Parameter names on disk follow HF PEFT
 (``base_model.model.<module>.<proj>.lora_A.weight`` / ``lora_B.weight``).
 
 Documented deviation: one dropout mask per fused input (HF draws separate masks for q, k, v).
@@ -27,7 +30,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from .. import ops
+from .. import _native, ops
 from .quant import NF4Linear
 
 
@@ -51,6 +54,66 @@ class LoraConfig:
         d = asdict(self)
         d["peft_type"] = "LORA"
         return d
+
+
+def _base_weight(base: nn.Module) -> torch.Tensor:
+    return base.dequantize() if isinstance(base, NF4Linear) else base.weight
+
+
+class _LoraFn(torch.autograd.Function):
+    """y = base(x) + scaling * sum_i  B_i A_i dropout(x)  (placed at target i's output columns)."""
+
+    @staticmethod
+    def forward(ctx, x, base, spec, r, scaling, p, seed, offset, *ab):
+        k = len(spec)
+        As, Bs = ab[:k], ab[k:]
+        x2 = x.reshape(-1, x.shape[-1])
+        if x2.dtype != As[0].dtype:
+            x2 = x2.to(As[0].dtype)
+        x2 = x2.contiguous()
+        C = _native.kernels()
+        w = _base_weight(base)
+        bias = getattr(base, "bias", None)
+        y = F.linear(x2, w, bias)
+        del w
+        xd = C.dropout_fwd_seeded(x2, p, seed, offset) if p > 0 else x2
+        acat = torch.cat(As, 0) if k > 1 else As[0]
+        h = xd @ acat.t()                                   # [M, r * k]
+        for i, (off, n) in enumerate(spec):                 # GEMM epilogue accumulates into y
+            y[:, off:off + n].addmm_(h[:, i * r:(i + 1) * r], Bs[i].t(), alpha=scaling)
+        ctx.base, ctx.spec, ctx.r, ctx.scaling, ctx.p, ctx.seed, ctx.offset = base, spec, r, scaling, p, seed, offset
+        ctx.xshape = x.shape
+        ctx.save_for_backward(xd, h, acat, *Bs)
+        return y.view(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        xd, h, acat, *Bs = ctx.saved_tensors
+        spec, r, s = ctx.spec, ctx.r, ctx.scaling
+        C = _native.kernels()
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if dy2.dtype != acat.dtype:
+            dy2 = dy2.to(acat.dtype)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            w = _base_weight(ctx.base)
+            dx = dy2 @ w                                     # base dX (frozen weight)
+            del w
+        gs, dBs = [], []
+        for i, (off, n) in enumerate(spec):
+            dyi = dy2[:, off:off + n]
+            gs.append(dyi @ (Bs[i] * s))                     # dL/dh_i  [M, r]
+            dBs.append((dyi.t() @ h[:, i * r:(i + 1) * r]).mul_(s))
+        g = torch.cat(gs, 1) if len(gs) > 1 else gs[0]       # [M, r * k]
+        dacat = g.t() @ xd                                   # [r * k, in]
+        if dx is not None:
+            if ctx.p > 0:
+                C.dropout_bwd_seeded(g @ acat, dx, ctx.p, ctx.seed, ctx.offset, True)  # dx += drop'(g A)
+            else:
+                dx.addmm_(g, acat)
+            dx = dx.view(ctx.xshape)
+        dAs = [dacat[i * r:(i + 1) * r] for i in range(len(spec))]
+        return (dx, None, None, None, None, None, None, None, *dAs, *dBs)
 
 
 class LoraLinear(nn.Module):
@@ -78,6 +141,13 @@ class LoraLinear(nn.Module):
                            self.targets[0][2] == self.out_features)
 
     def forward(self, x):
+        if x.is_cuda:
+            p = self.dropout_p if self.training else 0.0
+            seed, offset = ops.fused.dropout_seed_offset(x) if p > 0 else (0, 0)
+            names = [t[0] for t in self.targets]
+            spec = [(off, n) for _, off, n in self.targets]
+            return _LoraFn.apply(x, self.base, spec, self.r, self.scaling, p, seed, offset,
+                                 *[self.lora_A[n] for n in names], *[self.lora_B[n] for n in names])
         y = self.base(x)
         xd = ops.dropout(x, self.dropout_p, self.training) if self.dropout_p > 0 else x
         names = [t[0] for t in self.targets]
