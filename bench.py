@@ -59,6 +59,8 @@ def parse():
                     "adds one host sync per step, so it is off for the headline number")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--no-tuned-gemm", action="store_true", help="library-default GEMM solutions (A/B)")
+    ap.add_argument("--ipc", action="store_true", help="latency-bound collectives (grad-norm all-reduce) over the "
+                    "xGMI IPC one-shot kernel instead of RCCL (GRT_IPC_COLLECTIVES=1)")
     ap.add_argument("--backend", default="", help="process-group backend (default: nccl = RCCL on GPU, gloo on CPU)")
     return ap.parse_args()
 
@@ -101,6 +103,8 @@ def build(a, cfg, dev, dtype, world):
 
 def main():
     a = parse()
+    if a.ipc:
+        os.environ["GRT_IPC_COLLECTIVES"] = "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -511,6 +511,82 @@ bool gemm_wgrad(const Tensor& x, const Tensor& y, const Tensor& out, bool accumu
   return true;
 }
 
+// ------------------------------------------------------------------ xGMI IPC collectives
+int64_t ipc_alloc(int64_t nbytes, bool fine_grained, int64_t device) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  return reinterpret_cast<int64_t>(grt::ipc_malloc(nbytes, fine_grained));
+}
+void ipc_free_ptr(int64_t p, int64_t device) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  grt::ipc_free(reinterpret_cast<void*>(p));
+}
+py::bytes ipc_handle(int64_t p, int64_t device) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  char h[grt::kIpcHandleBytes];
+  grt::ipc_get_handle(reinterpret_cast<void*>(p), h);
+  return py::bytes(h, grt::kIpcHandleBytes);
+}
+int64_t ipc_open(const py::bytes& handle, int64_t device) {
+  std::string h = handle;
+  TORCH_CHECK((int)h.size() == grt::kIpcHandleBytes, "ipc_open: handle must be ", grt::kIpcHandleBytes, " bytes");
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  return reinterpret_cast<int64_t>(grt::ipc_open_handle(h.data()));
+}
+void ipc_close(int64_t p, int64_t device) {
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  grt::ipc_close_handle(reinterpret_cast<void*>(p));
+}
+
+grt::IpcPeers make_peers(const std::vector<int64_t>& staging, const std::vector<int64_t>& result,
+                         const std::vector<int64_t>& signal, const Tensor& err, int64_t cap, int64_t rank,
+                         int64_t timeout_ticks) {
+  const int64_t W = (int64_t)staging.size();
+  TORCH_CHECK(W >= 1 && W <= grt::kIpcMaxRanks, "ipc: world size must be 1..", grt::kIpcMaxRanks);
+  TORCH_CHECK((int64_t)result.size() == W && (int64_t)signal.size() == W, "ipc: pointer lists differ in length");
+  TORCH_CHECK(rank >= 0 && rank < W, "ipc: bad rank");
+  check_contig(err, "err");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1, "ipc: err must be an int32 device tensor");
+  grt::IpcPeers p{};
+  for (int64_t i = 0; i < W; ++i) {
+    TORCH_CHECK(staging[i] && result[i] && signal[i], "ipc: null peer buffer");
+    p.staging[i] = reinterpret_cast<void*>(staging[i]);
+    p.result[i] = reinterpret_cast<void*>(result[i]);
+    p.signal[i] = reinterpret_cast<uint32_t*>(signal[i]);
+  }
+  p.err = reinterpret_cast<uint32_t*>(err.data_ptr());
+  p.cap = cap;
+  p.rank = (int)rank;
+  p.world = (int)W;
+  p.timeout_ticks = (uint64_t)timeout_ticks;
+  return p;
+}
+
+void ipc_allreduce(const std::vector<int64_t>& staging, const std::vector<int64_t>& result,
+                   const std::vector<int64_t>& signal, const Tensor& err, int64_t cap, int64_t rank, int64_t epoch,
+                   int64_t timeout_ticks, const Tensor& in, const Tensor& out, bool two_shot, double scale) {
+  const grt::IpcPeers p = make_peers(staging, result, signal, err, cap, rank, timeout_ticks);
+  check_contig(in, "in");
+  check_contig(out, "out");
+  TORCH_CHECK(in.device() == err.device() && out.device() == err.device(), "ipc: tensors on another device");
+  TORCH_CHECK(in.scalar_type() == out.scalar_type() && in.numel() == out.numel(), "ipc: in/out mismatch");
+  const int64_t nbytes = in.numel() * in.element_size();
+  TORCH_CHECK(nbytes % 16 == 0, "ipc: message must be a multiple of 16 bytes (pad it)");
+  TORCH_CHECK(nbytes <= cap, "ipc: message of ", nbytes, " bytes exceeds the buffer (", cap, ")");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(in.data_ptr()) % 16 == 0 &&
+              reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "ipc: 16-byte alignment required");
+  c10::OptionalDeviceGuard g(in.device());
+  grt::ipc_allreduce(p, (uint32_t)epoch, dtype_of(in), in.data_ptr(), out.data_ptr(), nbytes, two_shot, (float)scale,
+                     cur_stream(in));
+}
+
+void ipc_barrier(const std::vector<int64_t>& staging, const std::vector<int64_t>& result,
+                 const std::vector<int64_t>& signal, const Tensor& err, int64_t cap, int64_t rank, int64_t epoch,
+                 int64_t timeout_ticks) {
+  const grt::IpcPeers p = make_peers(staging, result, signal, err, cap, rank, timeout_ticks);
+  c10::OptionalDeviceGuard g(err.device());
+  grt::ipc_barrier(p, (uint32_t)epoch, cur_stream(err));
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -548,4 +624,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("gemm_wgrad", &gemm_wgrad, py::arg("x"), py::arg("y"), py::arg("out"), py::arg("accumulate"),
         py::arg("mode") = 0);
+  m.def("ipc_alloc", &ipc_alloc);
+  m.def("ipc_free", &ipc_free_ptr);
+  m.def("ipc_handle", &ipc_handle);
+  m.def("ipc_open", &ipc_open);
+  m.def("ipc_close", &ipc_close);
+  m.def("ipc_allreduce", &ipc_allreduce);
+  m.def("ipc_barrier", &ipc_barrier);
+  m.attr("IPC_MAX_RANKS") = grt::kIpcMaxRanks;
+  m.attr("IPC_SIGNAL_BYTES") = grt::kIpcSignalBytes;
 }

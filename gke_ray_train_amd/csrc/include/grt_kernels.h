@@ -136,4 +136,32 @@ struct GemmTTParams {
 bool gemm_tt_supported(int P, int Q, int R);
 void gemm_tt(const GemmTTParams& p, hipStream_t stream, int mode = 0);  // mode != 0: diagnostics
 
+// ---------------- xGMI peer-to-peer collectives (ipc_comm.hip) ----------------
+constexpr int kIpcMaxRanks = 8;
+constexpr int kIpcMaxBlocks = 64;
+constexpr int kIpcHandleBytes = 64;
+// Per-rank view of the communicator: every rank's staging / result / signal buffers (peer
+// entries are IPC-opened mappings), this rank's error word, bytes per parity buffer.
+struct IpcPeers {
+  void* staging[kIpcMaxRanks];
+  void* result[kIpcMaxRanks];
+  uint32_t* signal[kIpcMaxRanks];
+  uint32_t* err;
+  int64_t cap;
+  int rank, world;
+  uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
+};
+// signal buffer: [2 phases][kIpcMaxBlocks][kIpcMaxRanks] uint32
+constexpr int64_t kIpcSignalBytes = 2LL * kIpcMaxBlocks * kIpcMaxRanks * 4;
+int ipc_blocks_for(int64_t nbytes, bool two_shot);
+// out = scale * sum over ranks of in (nbytes a multiple of 16, <= cap); in == out allowed.
+void ipc_allreduce(const IpcPeers& peers, uint32_t epoch, DType dt, const void* in, void* out, int64_t nbytes,
+                   bool two_shot, float scale, hipStream_t s);
+void ipc_barrier(const IpcPeers& peers, uint32_t epoch, hipStream_t s);
+void* ipc_malloc(int64_t nbytes, bool fine_grained);
+void ipc_free(void* p);
+void ipc_get_handle(void* p, char out[kIpcHandleBytes]);
+void* ipc_open_handle(const char in[kIpcHandleBytes]);
+void ipc_close_handle(void* p);
+
 }  // namespace grt

@@ -76,3 +76,16 @@ def all_reduce_scalar(x: float, op=None, device=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device or ("cuda" if dist.get_backend() == "nccl" else "cpu"))
     dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def small_all_reduce(t: torch.Tensor, group=None) -> torch.Tensor:
+    """In-place SUM all-reduce of a small (latency-bound) tensor: over the xGMI IPC one-shot
+    kernel (``parallel/ipc.py``) when ``GRT_IPC_COLLECTIVES=1`` on a single-node RCCL group, else
+    through the process group. Grad-norm scalars, logged losses and metrics go through here."""
+    if group is None and t.is_cuda and t.dtype in (torch.float32, torch.bfloat16):
+        from .ipc import default_communicator
+        comm = default_communicator()
+        if comm is not None and t.numel() * t.element_size() <= comm.cap:
+            return comm.all_reduce(t)
+    dist.all_reduce(t, group=group)
+    return t

@@ -35,7 +35,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.linear import Embedding as _DirectEmbedding, GradSlot, Linear as _DirectLinear
-from .comm import plan_bucket_bytes
+from .comm import plan_bucket_bytes, small_all_reduce
 
 
 def shared_param_ids(module: nn.Module) -> set:
@@ -332,7 +332,7 @@ class DistributedDataParallel(nn.Module):
             return _clip(self.grad_buffers(), max_norm, prescale=1.0 / W)
         st = _clip(self.grad_buffers(), 0.0, prescale=1.0)
         ss = (st.buf[0] ** 2).reshape(1)
-        dist.all_reduce(ss, group=self.pg)
+        small_all_reduce(ss, group=self.pg)
         total = ss[0].sqrt() / W
         coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(total)
         st.buf[0] = total

@@ -34,6 +34,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from ..ops.linear import GradSlot
+from .comm import small_all_reduce
 
 DEFAULT_UNITS = ("LlamaDecoderLayer", "EncoderLayer")
 _ALIGN = 64
@@ -451,7 +452,7 @@ class FullyShardedDataParallel(nn.Module):
         st2 = _clip([self.rep_grad], 0.0, prescale=1.0)
         ss_rep = st2.buf[0] ** 2
         if self.world > 1:
-            dist.all_reduce(ss_shard, group=self.pg)
+            small_all_reduce(ss_shard, group=self.pg)
         total = (ss_shard + ss_rep).sqrt() / self.world
         coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(total)
         st.buf[0] = total

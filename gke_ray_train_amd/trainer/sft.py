@@ -35,6 +35,7 @@ import torch.distributed as dist
 from ..observability import roctx
 from ..observability.metrics import MI355X_PEAK_BF16_DENSE
 from ..ops import clip_grad_norm_, make_optimizer
+from ..parallel.comm import small_all_reduce
 from ..parallel.ddp import DistributedDataParallel
 from .schedules import get_scheduler
 from .sft_data import LengthGroupedSampler, PadCollator, pack_sequences
@@ -310,7 +311,7 @@ class SFTTrainer:
     def _mean_across_ranks(self, t: torch.Tensor) -> float:
         t = t.detach().float().reshape(1).clone()
         if self.world > 1:
-            dist.all_reduce(t)
+            small_all_reduce(t)
             t /= self.world
         return float(t.item())
 
