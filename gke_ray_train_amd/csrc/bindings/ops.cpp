@@ -336,9 +336,15 @@ void scale_(Tensor& x, double a, const optional<Tensor>& a_ptr) {
 void check_bshd(const Tensor& t, const char* name) {
   check_cuda(t, name);
   TORCH_CHECK(t.dim() == 4, name, " must be [B, S, H, D]");
-  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bf16");
-  TORCH_CHECK(t.size(3) == 128 && t.stride(3) == 1, name, ": head_dim must be 128 and contiguous");
-  TORCH_CHECK(t.stride(0) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(2) % 8 == 0 &&
+  TORCH_CHECK(t.stride(3) == 1, name, ": head_dim must be contiguous");
+  if (t.scalar_type() == at::kBFloat16) {
+    TORCH_CHECK(t.size(3) == 128, name, ": bf16 kernels need head_dim 128");
+  } else {
+    TORCH_CHECK(t.scalar_type() == at::kFloat, name, " must be bf16 or fp32");
+    TORCH_CHECK(grt::attn_f32_supported((int)t.size(3)), name, ": fp32 kernels need head_dim 64 or 128");
+  }
+  const int64_t vec = 16 / t.element_size();
+  TORCH_CHECK(t.stride(0) % vec == 0 && t.stride(1) % vec == 0 && t.stride(2) % vec == 0 &&
                   reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
               name, ": strides must keep 16-byte alignment");
 }
@@ -350,6 +356,9 @@ grt::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, c
   check_bshd(v, "v");
   check_bshd(o, "o");
   TORCH_CHECK(k.sizes() == v.sizes(), "k/v shape mismatch");
+  TORCH_CHECK(k.scalar_type() == q.scalar_type() && v.scalar_type() == q.scalar_type() &&
+                  o.scalar_type() == q.scalar_type(), "q/k/v/o dtype mismatch");
+  TORCH_CHECK(k.size(3) == q.size(3), "head_dim mismatch");
   TORCH_CHECK(q.size(0) == k.size(0) && o.sizes() == q.sizes(), "batch/out shape mismatch");
   TORCH_CHECK(q.size(2) % k.size(2) == 0, "Hq must be a multiple of Hkv");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() &&
@@ -395,7 +404,8 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
   auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k);
   set_dropout(p, dropout_p, seed);
-  grt::attn_fwd(p, cur_stream(q));
+  if (q.scalar_type() == at::kFloat) grt::attn_fwd_f32(p, cur_stream(q));
+  else grt::attn_fwd(p, cur_stream(q));
   return {o, lse};
 }
 
@@ -423,7 +433,10 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   bp.dk = dk.data_ptr(); bp.dk_bs = dk.stride(0); bp.dk_ss = dk.stride(1); bp.dk_hs = dk.stride(2);
   bp.dv = dv.data_ptr(); bp.dv_bs = dv.stride(0); bp.dv_ss = dv.stride(1); bp.dv_hs = dv.stride(2);
   bp.delta = ws.data_ptr<float>();
-  grt::attn_bwd(bp, cur_stream(q));
+  TORCH_CHECK(dout.scalar_type() == q.scalar_type() && dq.scalar_type() == q.scalar_type() &&
+                  dk.scalar_type() == q.scalar_type() && dv.scalar_type() == q.scalar_type(), "grad dtype mismatch");
+  if (q.scalar_type() == at::kFloat) grt::attn_bwd_f32(bp, cur_stream(q));
+  else grt::attn_bwd(bp, cur_stream(q));
   return {dq, dk, dv};
 }
 

@@ -107,6 +107,10 @@ struct AttnBwdParams {
 };
 void attn_bwd(const AttnBwdParams& p, hipStream_t s);
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int D);
+// exact-fp32 variants (attention_f32.hip): same params with fp32 tensors, head_dim 64 or 128
+bool attn_f32_supported(int head_dim);
+void attn_fwd_f32(const AttnParams& p, hipStream_t s);
+void attn_bwd_f32(const AttnBwdParams& p, hipStream_t s);
 
 // ---------------- 4-bit NormalFloat (nf4.hip) ----------------
 void nf4_quantize(DType dt, const void* w, uint8_t* q, float* absmax, int64_t n, int blocksize,

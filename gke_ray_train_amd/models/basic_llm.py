@@ -9,7 +9,7 @@ Same math and the SAME state_dict keys as the reference module (``token_embeddin
 ``positional_encoding.pe``, ``transformer_decoder.layers.{i}.self_attn.in_proj_weight`` …,
 ``fc_out.weight``), so ``model.pth`` files written by either load into the other. The compute
 path differs: post-LN is one fused residual+LayerNorm kernel per sub-block, GELU/dropout/CE are
-HIP kernels, attention is the flash kernel (bf16, with in-kernel attention-probability dropout)
+HIP kernels, attention is the flash kernel (fp32 or bf16, with in-kernel attention-probability dropout)
 and the PE is a non-synced on-device constant (no per-step DDP buffer broadcast).
 """
 from __future__ import annotations
@@ -82,8 +82,9 @@ class _MHA(nn.Module):
         qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias).view(B, S, 3, H, Dh)
         q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
         p = self.dropout if training else 0.0
-        # bf16 / Dh 128 on MI355X: the flash kernel with in-kernel probability dropout; otherwise
-        # the explicit fp32 math path with the same dropout mask (reference semantics, :82-86)
+        # on MI355X: the flash kernels with in-kernel probability dropout — exact fp32
+        # (attention_f32.hip, the reference's fp32 training) or bf16 (attention.hip); CPU: the
+        # explicit fp32 math path with the same dropout mask (reference semantics, :82-86)
         o = ops.flash_attention(q, k, v, causal=True, dropout_p=p)
         return self.out_proj(o.reshape(B * S, d))
 

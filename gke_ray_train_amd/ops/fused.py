@@ -203,7 +203,8 @@ def flash_attention(q, k, v, causal=True, scale=None, seqlens_k=None, dropout_p=
     if dropout_p > 0.0 and seed is None:
         seed = _dropout_seed()
     seed = 0 if seed is None else int(seed)
-    if _gpu(q) and q.dtype == torch.bfloat16 and q.shape[-1] == 128:
+    if _gpu(q) and ((q.dtype == torch.bfloat16 and q.shape[-1] == 128) or
+                    (q.dtype == torch.float32 and q.shape[-1] in (64, 128))):
         return _FlashAttn.apply(q, k, v, causal, scale, seqlens_k, float(dropout_p), seed)
     if _gpu(q):
         _warn_once(f"flash_attention: no gfx950 kernel for dtype={q.dtype} head_dim={q.shape[-1]}; "

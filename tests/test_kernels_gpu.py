@@ -206,23 +206,23 @@ def test_nf4_roundtrip():
     assert rel < 0.15
 
 
-def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False, dropout_p=0.0):
+def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False, dropout_p=0.0, dtype=torch.bfloat16,
+               D=128):
     from gke_ray_train_amd import ops
     from gke_ray_train_amd.ops import _ref
     torch.manual_seed(8)
-    D = 128
     if strided:
-        qkv = torch.randn(B, Sq, Hq + 2 * Hkv, D, device=DEV, dtype=torch.bfloat16)
+        qkv = torch.randn(B, Sq, Hq + 2 * Hkv, D, device=DEV, dtype=dtype)
         q = qkv[:, :, :Hq].detach().requires_grad_()
-        base = torch.randn(B, Sk, 2 * Hkv, D, device=DEV, dtype=torch.bfloat16)
+        base = torch.randn(B, Sk, 2 * Hkv, D, device=DEV, dtype=dtype)
         k = base[:, :, :Hkv]
         v = base[:, :, Hkv:]
         k = k.detach().requires_grad_()
         v = v.detach().requires_grad_()
     else:
-        q = torch.randn(B, Sq, Hq, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-        k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-        v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+        q = torch.randn(B, Sq, Hq, D, device=DEV, dtype=dtype, requires_grad=True)
+        k = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=dtype, requires_grad=True)
+        v = torch.randn(B, Sk, Hkv, D, device=DEV, dtype=dtype, requires_grad=True)
     sl = None if seqlens is None else torch.tensor(seqlens, device=DEV, dtype=torch.int32)
     o = ops.flash_attention(q, k, v, causal=causal, seqlens_k=sl, dropout_p=dropout_p, seed=1234)
     do = torch.randn_like(o)
@@ -231,10 +231,11 @@ def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False, dropout_
     orf = _ref.attention(qr, kr, vr, causal=causal, seqlens_k=sl, dropout_p=dropout_p, seed=1234)
     (orf * do.float()).sum().backward()
     valid = torch.ones(B, Sq, dtype=torch.bool, device=DEV)
-    _close(o, orf, 2e-2, 2e-2, "attn o")
-    _close(q.grad, qr.grad, 3e-2, 3e-2, "attn dq")
-    _close(k.grad, kr.grad, 3e-2, 3e-2, "attn dk")
-    _close(v.grad, vr.grad, 3e-2, 3e-2, "attn dv")
+    tol = (2e-2, 3e-2) if dtype == torch.bfloat16 else (2e-4, 5e-4)  # fp32: exact-f32 MFMA vs fp32 math
+    _close(o, orf, tol[0], tol[0], "attn o")
+    _close(q.grad, qr.grad, tol[1], tol[1], "attn dq")
+    _close(k.grad, kr.grad, tol[1], tol[1], "attn dk")
+    _close(v.grad, vr.grad, tol[1], tol[1], "attn dv")
 
 
 @pytest.mark.parametrize("case", [
@@ -249,6 +250,21 @@ def _attn_case(B, Sq, Sk, Hq, Hkv, causal, seqlens=None, strided=False, dropout_
 ])
 def test_flash_attention(case):
     _attn_case(**case)
+
+
+@pytest.mark.parametrize("case", [
+    dict(B=2, Sq=256, Sk=256, Hq=4, Hkv=4, causal=True),
+    dict(B=1, Sq=200, Sk=200, Hq=4, Hkv=2, causal=True, D=64),
+    dict(B=2, Sq=130, Sk=130, Hq=2, Hkv=2, causal=False),
+    dict(B=1, Sq=64, Sk=192, Hq=2, Hkv=1, causal=True, D=64),
+    dict(B=2, Sq=256, Sk=256, Hq=4, Hkv=2, causal=True, strided=True),
+    dict(B=2, Sq=160, Sk=160, Hq=2, Hkv=2, causal=False, seqlens=[160, 77]),
+    dict(B=2, Sq=256, Sk=256, Hq=4, Hkv=4, causal=True, dropout_p=0.1),
+    dict(B=1, Sq=200, Sk=200, Hq=2, Hkv=2, causal=True, dropout_p=0.3, D=64),
+])
+def test_flash_attention_fp32(case):
+    """exact-fp32 kernels (attention_f32.hip, BasicLLM's reference dtype) vs the fp32 math path"""
+    _attn_case(dtype=torch.float32, **case)
 
 
 def test_rope_attention_fused():
