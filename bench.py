@@ -59,6 +59,9 @@ def parse():
                     "adds one host sync per step, so it is off for the headline number")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--no-tuned-gemm", action="store_true", help="library-default GEMM solutions (A/B)")
+    ap.add_argument("--overlap-opt", default="auto", choices=["auto", "on", "off"],
+                    help="replicated DDP: run the AdamW update per module on a side stream, overlapped with the "
+                         "next forward (parallel/overlap.py); auto = on unless ZeRO / FSDP")
     ap.add_argument("--ipc", action="store_true", help="latency-bound collectives (grad-norm all-reduce) over the "
                     "xGMI IPC one-shot kernel instead of RCCL (GRT_IPC_COLLECTIVES=1)")
     ap.add_argument("--backend", default="", help="process-group backend (default: nccl = RCCL on GPU, gloo on CPU)")
@@ -98,6 +101,9 @@ def build(a, cfg, dev, dtype, world):
     zero = a.zero == "on" or (a.zero == "auto" and world > 1)
     eng = DistributedDataParallel(fwd, bucket_cap_mb=a.bucket_mb or None, shard_optimizer=zero)
     opt = FusedAdamW(eng.optimizer_param_groups(weight_decay=0.0), lr=a.lr)
+    if a.overlap_opt == "on" or (a.overlap_opt == "auto" and not zero and dev.type == "cuda"):
+        from gke_ray_train_amd.parallel.overlap import OverlappedOptimizer
+        opt = OverlappedOptimizer(eng, opt)
     return fwd, eng, fwd, opt
 
 
@@ -258,6 +264,7 @@ def main():
             "config": {"model": cfg.name, "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": par,
                        "micro_batch": mb, "grad_accum": accum, "optimizer": "fused AdamW fp32 states",
                        "max_grad_norm": a.max_grad_norm, "activation_checkpointing": a.checkpointing,
+                       "optimizer_overlap": type(opt).__name__ == "OverlappedOptimizer",
                        "library_gemms": "offline-tuned" if tuned else "default"},
             "samples_per_sec": round(tps / a.seq, 2),
             "mfu_bf16_dense": round(mfu, 4),

@@ -103,6 +103,37 @@ class FusedAdamW(torch.optim.Optimizer):
             self._hyper[(dev, key)] = hb
         return hb
 
+    def _init_state(self, p):
+        st = self.state[p]
+        if len(st) == 0:
+            st["step"] = torch.tensor(0.0)
+            st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
+            st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
+            if self.master_weights and p.dtype != torch.float32:
+                st["master"] = p.detach().float().contiguous()
+        return st
+
+    @torch.no_grad()
+    def prepare_gpu_step(self):
+        """Bump the step counters and upload each group's hyper-parameters (current stream);
+        returns [(p, grad, exp_avg, exp_avg_sq, master, hyper)] for the caller to launch the
+        update kernels on (views of) these tensors — used by the overlapped optimizer."""
+        out = []
+        for gi, group in enumerate(self.param_groups):
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None or not p.is_cuda:
+                    continue
+                st = self._init_state(p)
+                st["step"] += 1
+                step = float(st["step"])
+                hb = self._hyper_buf(p.device, (gi,))
+                hb.copy_(torch.tensor([group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** step,
+                                       1.0 - b2 ** step, 1.0], dtype=torch.float32), non_blocking=True)
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                out.append((p, g, st["exp_avg"], st["exp_avg_sq"], st.get("master"), hb))
+        return out
+
     @torch.no_grad()
     def step(self, closure=None, grad_scale: Optional[GradClipState] = None):
         loss = None
@@ -116,13 +147,7 @@ class FusedAdamW(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0)
-                    st["exp_avg"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, dtype=torch.float32, memory_format=torch.contiguous_format)
-                    if self.master_weights and p.dtype != torch.float32:
-                        st["master"] = p.detach().float().contiguous()
+                st = self._init_state(p)
                 st["step"] += 1
                 step = float(st["step"].item()) if st["step"].device.type == "cpu" else float(st["step"])
                 bc1 = 1.0 - b1 ** step

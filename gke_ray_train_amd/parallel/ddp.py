@@ -48,6 +48,28 @@ def shared_param_ids(module: nn.Module) -> set:
     return shared
 
 
+def forward_wait_modules(module: nn.Module, unit_types, param_ids: set) -> Dict[nn.Module, List[int]]:
+    """Which module's forward pre-hook must wait for each parameter (ids in ``param_ids``) to be
+    ready: the enclosing transformer layer (``unit_types``) for parameters inside one — layers read
+    their norm weights directly, not through submodule calls — else the parameter's own module
+    (embedding, final norm, LM head). Returned in module registration order = forward order."""
+    waits: Dict[nn.Module, List[int]] = {}
+    claimed = set()
+    for m in module.modules():
+        if type(m).__name__ in unit_types:
+            for p in m.parameters():
+                if id(p) in param_ids and id(p) not in claimed:
+                    claimed.add(id(p))
+                    waits.setdefault(m, []).append(id(p))
+    for m in module.modules():
+        for p in m.parameters(recurse=False):
+            if id(p) in param_ids and id(p) not in claimed:
+                claimed.add(id(p))
+                waits.setdefault(m, []).append(id(p))
+    order = {m: i for i, m in enumerate(module.modules())}
+    return dict(sorted(waits.items(), key=lambda kv: order[kv[0]]))
+
+
 def _no_decay(name: str, p: torch.Tensor) -> bool:
     # HF Trainer's rule: biases and normalisation weights are excluded from weight decay
     n = name.lower()
@@ -201,28 +223,13 @@ class DistributedDataParallel(nn.Module):
                 for b in g.buckets:
                     c = (b.end - b.start) // W
                     g.shard_param[b.shard_off:b.shard_off + c].copy_(g.flat[b.start + r * c:b.start + (r + 1) * c])
-        # Which module's forward pre-hook waits for a bucket: the enclosing transformer layer for
-        # parameters inside one (layers read their norm weights directly, not via submodule calls),
-        # else the parameter's own module (embedding, final norm, LM head).
         owner = {}
         for g in self.groups:
             for b in g.buckets:
                 for p in b.params:
                     owner[id(p)] = b
-        waits = {}
-        claimed = set()
-        for m in self.module.modules():
-            if type(m).__name__ in self.UNIT_TYPES:
-                for p in m.parameters():
-                    if id(p) in owner and id(p) not in claimed:
-                        claimed.add(id(p))
-                        waits.setdefault(m, {})[id(owner[id(p)])] = owner[id(p)]
-        for m in self.module.modules():
-            for p in m.parameters(recurse=False):
-                if id(p) in owner and id(p) not in claimed:
-                    claimed.add(id(p))
-                    waits.setdefault(m, {})[id(owner[id(p)])] = owner[id(p)]
-        for m, bs in waits.items():
+        for m, ps in forward_wait_modules(self.module, self.UNIT_TYPES, set(owner)).items():
+            bs = {id(owner[i]): owner[i] for i in ps}
             self._hooks.append(m.register_forward_pre_hook(self._make_gather_wait(list(bs.values()))))
 
     @staticmethod

@@ -79,3 +79,38 @@ def test_fsdp_world1_matches_ddp_on_gpu(offload):
     for k, v in ref.state_dict().items():
         d = (full[k].float() - v.float()).abs().max().item()
         assert d < 5e-3, (k, d)
+
+
+def test_overlapped_optimizer_matches_serial():
+    """Chunked AdamW on a side stream, released to each module's forward pre-hook, gives
+    bit-identical parameters and losses to the serial end-of-step update."""
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.ops import FusedAdamW, clip_grad_norm_
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    from gke_ray_train_amd.parallel.overlap import OverlappedOptimizer
+    runs = []
+    for overlap in (False, True):
+        m = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=5)
+        ddp = DistributedDataParallel(m)
+        opt = FusedAdamW(ddp.optimizer_param_groups(0.01), lr=1e-3)
+        if overlap:
+            opt = OverlappedOptimizer(ddp, opt)
+            assert len(opt.chunks) == m.config.num_hidden_layers + 3  # embed, layers, norm, head
+        g = torch.Generator(device="cuda").manual_seed(9)
+        losses = []
+        for _ in range(4):
+            ids = torch.randint(0, m.config.vocab_size, (2, 128), device="cuda", generator=g)
+            loss = ddp(ids, labels=ids)["loss"]
+            loss.backward()
+            ddp.finish_gradient_sync()
+            st = clip_grad_norm_(ddp.grad_buffers(), 0.5)
+            opt.step(grad_scale=st)
+            ddp.zero_grad()
+            losses.append(loss.item())
+        if overlap:
+            opt.synchronize()
+        torch.cuda.synchronize()
+        runs.append((losses, {k: v.clone() for k, v in m.state_dict().items()}))
+    assert runs[0][0] == runs[1][0]
+    for k, v in runs[0][1].items():
+        assert torch.equal(v, runs[1][1][k]), k
