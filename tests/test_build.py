@@ -24,3 +24,23 @@ def test_runtime_library_exports():
     lib = _native.runtime_lib()
     for sym in ("grt_gather_windows_i64", "grt_pad_collate", "grt_ring_create", "grt_ring_pop"):
         assert hasattr(lib, sym), sym
+
+
+@pytest.mark.parametrize("sanitizer", ["thread", "address,undefined"])
+def test_runtime_under_sanitizers(tmp_path, sanitizer):
+    """the native runtime (shm ring, batch gather, pad-collate) under TSan and
+    ASan+UBSan — producer/consumer threads on two mappings of one ring, zero-copy and copying
+    paths, close/timeout semantics, multi-threaded gathers; any report fails the run."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("no host compiler")
+    rt = os.path.join(ROOT, "gke_ray_train_amd", "csrc", "runtime")
+    exe = str(tmp_path / "stress")
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-pthread", f"-fsanitize={sanitizer}", "-fno-omit-frame-pointer",
+                    os.path.join(rt, "tests", "sanitize_stress.cpp"), os.path.join(rt, "shm_ring.cpp"),
+                    os.path.join(rt, "batch_gather.cpp"), "-o", exe, "-lrt"], check=True)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe, "20000"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "sanitize_stress ok" in r.stdout, r.stdout + r.stderr
