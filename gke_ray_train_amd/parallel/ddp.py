@@ -27,6 +27,7 @@ MI355X design (not a translation of torch's C++ Reducer):
 from __future__ import annotations
 
 import contextlib
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -121,7 +122,10 @@ class DistributedDataParallel(nn.Module):
         self.world_size = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world_size > 1 else 0
         self.zero = bool(shard_optimizer) and self.world_size > 1
-        self.gloo = self.world_size > 1 and dist.get_backend(process_group) == "gloo"
+        # gloo branch: list-based collectives. GRT_GLOO_TENSOR_COLLECTIVES=1 runs the RCCL code path
+        # (reduce_scatter_tensor / all_gather_into_tensor) over gloo so CPU tests exercise it.
+        self.gloo = (self.world_size > 1 and dist.get_backend(process_group) == "gloo"
+                     and os.environ.get("GRT_GLOO_TENSOR_COLLECTIVES", "0") != "1")
         self._sync = True
         self._hooks = []
         self._grad_view = {}

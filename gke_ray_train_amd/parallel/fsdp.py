@@ -26,6 +26,7 @@ Design for 8 x MI355X on xGMI:
 from __future__ import annotations
 
 import contextlib
+import os
 import math
 from typing import Dict, List, Optional
 
@@ -94,7 +95,9 @@ class FullyShardedDataParallel(nn.Module):
         self.cpu_offload = cpu_offload
         self.offload_chunk = offload_chunk_elems
         self._sync = True
-        self.gloo = dist.is_initialized() and dist.get_backend(process_group) == "gloo"
+        # GRT_GLOO_TENSOR_COLLECTIVES=1: run the RCCL code path over gloo (CPU tests), see ddp.py
+        self.gloo = (dist.is_initialized() and dist.get_backend(process_group) == "gloo"
+                     and os.environ.get("GRT_GLOO_TENSOR_COLLECTIVES", "0") != "1")
         first = next(module.parameters())
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if first.device.type == "meta" else first.device)
@@ -348,6 +351,8 @@ class FullyShardedDataParallel(nn.Module):
                 else:
                     u.shard_grad.copy_(part)
             else:
+                if u.rs_work is not None:  # previous micro-step's reduce-scatter of this unit
+                    self._finish_rs(u)
                 out = u.shard_grad if not self._accumulating(u) else torch.empty_like(u.shard_grad)
                 u.rs_work = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
                 u.rs_out = out if out is not u.shard_grad else None
@@ -358,6 +363,17 @@ class FullyShardedDataParallel(nn.Module):
         u.acc_started = True
         if u.module is not self.module:
             self._unbind(u)
+
+    @staticmethod
+    def _finish_rs(u: _Unit):
+        """Wait a unit's reduce-scatter (stream-ordered for RCCL) and fold an accumulation
+        temporary into the shard; its source buffer may be released only after this."""
+        u.rs_work.wait()
+        u.rs_work = None
+        if u.rs_out is not None:
+            u.shard_grad.add_(u.rs_out)
+            u.rs_out = None
+        u._rs_src = None
 
     def _accumulating(self, u):
         return getattr(u, "acc_started", False)
@@ -399,12 +415,7 @@ class FullyShardedDataParallel(nn.Module):
                 self._param_ready(u.params[-1]) if u.params else None
         for u in self.units:
             if u.rs_work is not None:
-                u.rs_work.wait()
-                u.rs_work = None
-                if u.rs_out is not None:
-                    u.shard_grad.add_(u.rs_out)
-                    u.rs_out = None
-                u._rs_src = None
+                self._finish_rs(u)
         if self.world > 1 and self.replicated and self._sync:
             dist.all_reduce(self.rep_grad, group=self.pg)
         if self._root_unit is not None and self.world > 1:

@@ -79,8 +79,10 @@ def test_ddp_matches_single_process(accum):
         assert torch.allclose(p.grad, g0[n], atol=1e-5, rtol=1e-4), f"{n}: max {(p.grad - g0[n]).abs().max()}"
 
 
-def _zero_worker(rank, world, port, q, zero):
+def _zero_worker(rank, world, port, q, zero, tensor_coll=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if tensor_coll:  # the RCCL code path (reduce_scatter_tensor / all_gather_into_tensor) over gloo
+        os.environ["GRT_GLOO_TENSOR_COLLECTIVES"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gke_ray_train_amd.models import build_llama
@@ -111,15 +113,18 @@ def _zero_worker(rank, world, port, q, zero):
         dist.destroy_process_group()
 
 
-def test_zero_sharded_optimizer_matches_ddp():
-    """ZeRO-1/2 mode (reduce-scatter + sharded AdamW + async all-gather) == plain DDP, 3 steps."""
+@pytest.mark.parametrize("tensor_coll", [False, True])
+def test_zero_sharded_optimizer_matches_ddp(tensor_coll):
+    """ZeRO-1/2 mode (reduce-scatter + sharded AdamW + async all-gather) == plain DDP, 3 steps.
+    tensor_coll=True runs the exact collective calls of the RCCL path (reduce_scatter_tensor into
+    the shard views, all_gather_into_tensor into the flat buckets) over gloo."""
     world = 2
     ctx = mp.get_context("spawn")
     out = {}
     for zero in (False, True):
         q = ctx.Queue()
         port = _free_port()
-        procs = [ctx.Process(target=_zero_worker, args=(r, world, port, q, zero)) for r in range(world)]
+        procs = [ctx.Process(target=_zero_worker, args=(r, world, port, q, zero, tensor_coll)) for r in range(world)]
         for p in procs:
             p.start()
         res = {}

@@ -19,8 +19,10 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q, ckpt, accum):
+def _worker(rank, world, port, q, ckpt, accum, tensor_coll=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if tensor_coll:  # the RCCL code path (reduce_scatter_tensor / all_gather_into_tensor) over gloo
+        os.environ["GRT_GLOO_TENSOR_COLLECTIVES"] = "1"
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gke_ray_train_amd.models import build_llama
@@ -49,13 +51,13 @@ def _worker(rank, world, port, q, ckpt, accum):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ckpt,accum", [(False, 1), (True, 2)])
-def test_fsdp_matches_single_process(ckpt, accum):
+@pytest.mark.parametrize("ckpt,accum,tensor_coll", [(False, 1, False), (True, 2, False), (True, 2, True)])
+def test_fsdp_matches_single_process(ckpt, accum, tensor_coll):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, ckpt, accum)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, ckpt, accum, tensor_coll)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
