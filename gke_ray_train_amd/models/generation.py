@@ -7,6 +7,15 @@ layer (sized for prompt + max_new_tokens up front, no re-allocation while decodi
 every decode step run the SAME flash-attention kernel over a strided view of the cache
 (bottom-right-aligned causal mask, Sq = new tokens, Sk = tokens so far) with RoPE applied at the
 absolute positions by the RoPE kernel's position array.
+
+On MI355X the one-token decode step is launch-bound (≈10 kernels per layer, a few µs of work
+each), so ``GraphDecoder`` captures the WHOLE step — embedding, every layer, final norm, LM head
+and the greedy argmax — into one HIP graph and replays it per token. Everything that changes
+between tokens lives in device tensors the graph reads: the current position (RoPE position
+array and the KV-cache write index) and the per-row valid key length, which the flash kernel
+takes as its padding mask (``seqlens_k``) over the full-length cache, so the kernel's tile loop
+still covers only the keys written so far. EOS checks touch the host every ``sync_every``
+tokens instead of every token; the output is trimmed to HF's stopping point.
 """
 from __future__ import annotations
 
@@ -71,22 +80,138 @@ def forward_cached(model, ids: torch.Tensor, cache: KVCache) -> torch.Tensor:
     return model.lm_head(last).float()
 
 
+def _graph_layer_step(layer, h, residual, B, cos, sin, cache: KVCache, li: int, pos_b, pos_l, lens):
+    """One-token layer step with every position-dependent value read from device tensors."""
+    attn = layer.self_attn
+    eps = layer.input_layernorm.eps
+    if residual is None:
+        residual = h
+        x = ops.rms_norm(h, layer.input_layernorm.weight, eps)
+    else:
+        x, residual = ops.add_rms_norm(h, residual, layer.input_layernorm.weight, eps)
+    qkv = attn.qkv_proj(x)
+    hq, hkv, D = attn.hq, attn.hkv, attn.hd
+    q, k = _native.kernels().rope_fwd(qkv.contiguous(), cos, sin, pos_b, hq, hkv, D, cos.shape[0])
+    v = qkv.view(B, 1, hq + 2 * hkv, D)[:, :, hq + hkv:]
+    cache.k[li].index_copy_(1, pos_l, k.view(B, 1, hkv, D))
+    cache.v[li].index_copy_(1, pos_l, v)
+    o = ops.flash_attention(q.view(B, 1, hq, D), cache.k[li], cache.v[li], causal=False, seqlens_k=lens)
+    h = attn.o_proj(o.reshape(B, hq * D))
+    x, residual = ops.add_rms_norm(h, residual, layer.post_attention_layernorm.weight, eps)
+    return layer.mlp(x), residual
+
+
+class GraphDecoder:
+    """Greedy / sampling decode with the per-token step captured in a HIP graph (see module doc).
+
+    Usage: ``dec = GraphDecoder(model, B, max_len)``; ``logits = dec.prefill(ids)`` (eager, any
+    prompt length); then ``logits = dec.step(next_ids)`` per token (graph replay). Needs a bf16
+    Llama on the GPU with head_dim 128 (the HIP RoPE / flash kernels)."""
+
+    def __init__(self, model, B: int, max_len: int):
+        self.model = model
+        p = next(model.parameters())
+        self.device = p.device
+        dt = p.dtype if p.dtype in (torch.bfloat16, torch.float32) else torch.bfloat16
+        self.cache = KVCache(model.config, B, max_len, self.device, dt)
+        self.B = B
+        self.cos, self.sin = model.rope(max_len, self.device)
+        self.ids = torch.zeros(B, 1, dtype=torch.long, device=self.device)
+        self.pos_b = torch.zeros(B, dtype=torch.int32, device=self.device)   # RoPE positions
+        self.pos_l = torch.zeros(1, dtype=torch.long, device=self.device)    # cache write index
+        self.lens = torch.zeros(B, dtype=torch.int32, device=self.device)    # valid keys incl. new token
+        self.graph = None
+        self.logits = None
+
+    @torch.no_grad()
+    def prefill(self, input_ids: torch.Tensor) -> torch.Tensor:
+        logits = forward_cached(self.model, input_ids, self.cache)
+        n = self.cache.len
+        self.pos_b.fill_(n)
+        self.pos_l.fill_(n)
+        self.lens.fill_(n + 1)
+        return logits
+
+    @torch.no_grad()
+    def _step_body(self):
+        m = self.model
+        h = m.model.embed_tokens(self.ids).view(self.B, -1)
+        residual = None
+        for li, layer in enumerate(m.model.layers):
+            h, residual = _graph_layer_step(layer, h, residual, self.B, self.cos, self.sin, self.cache, li,
+                                            self.pos_b, self.pos_l, self.lens)
+        x, _ = ops.add_rms_norm(h, residual, m.model.norm.weight, m.model.norm.eps)
+        logits = m.lm_head(x).float()
+        self.pos_b.add_(1)
+        self.pos_l.add_(1)
+        self.lens.add_(1)
+        return logits
+
+    def _capture(self):
+        # warm up on a side stream (allocator pools, library handles), then capture one step;
+        # the warm-up step's cache writes land at the current position and are rewritten by the
+        # first replay, and the position tensors are restored afterwards
+        saved = (self.pos_b.clone(), self.pos_l.clone(), self.lens.clone())
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._step_body()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        for t, v in zip((self.pos_b, self.pos_l, self.lens), saved):
+            t.copy_(v)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.logits = self._step_body()
+        for t, v in zip((self.pos_b, self.pos_l, self.lens), saved):
+            t.copy_(v)
+
+    @torch.no_grad()
+    def step(self, next_ids: torch.Tensor) -> torch.Tensor:
+        if self.cache.len >= self.cache.max_len:
+            raise RuntimeError("KV cache full")
+        self.ids.copy_(next_ids.view(self.B, 1))
+        if self.graph is None:
+            self._capture()
+        self.graph.replay()
+        self.cache.len += 1
+        return self.logits
+
+
+def _graph_ok(model, input_ids) -> bool:
+    p = next(model.parameters())
+    cfg = model.config
+    return (input_ids.is_cuda and p.dtype == torch.bfloat16 and cfg.head_dim == 128
+            and _native.kernels_available())
+
+
 @torch.no_grad()
 def generate(model, input_ids: torch.Tensor, max_new_tokens: int = 32,
              eos_token_id: Optional[Union[int, List[int]]] = None, do_sample: bool = False, temperature: float = 1.0,
-             top_p: Optional[float] = None, attention_mask=None, pad_token_id=None, generator=None, **_):
+             top_p: Optional[float] = None, attention_mask=None, pad_token_id=None, generator=None,
+             use_graph: Optional[bool] = None, sync_every: int = 16, **_):
     """Returns [B, prompt + generated] token ids (HF ``generate`` output convention)."""
     was = model.training
     model.eval()
     B, S = input_ids.shape
     eos = set([eos_token_id] if isinstance(eos_token_id, int) else (eos_token_id or []))
-    p = next(model.parameters())
-    cache = KVCache(model.config, B, S + max_new_tokens, input_ids.device,
-                    p.dtype if p.dtype in (torch.bfloat16, torch.float32) else torch.bfloat16)
-    logits = forward_cached(model, input_ids, cache)
+    eos_t = torch.tensor(sorted(eos), device=input_ids.device) if eos else None
+    graph = use_graph if use_graph is not None else _graph_ok(model, input_ids)
+    if graph:
+        dec = GraphDecoder(model, B, S + max_new_tokens)
+        logits = dec.prefill(input_ids)
+        forward = dec.step
+    else:
+        p = next(model.parameters())
+        cache = KVCache(model.config, B, S + max_new_tokens, input_ids.device,
+                        p.dtype if p.dtype in (torch.bfloat16, torch.float32) else torch.bfloat16)
+        logits = forward_cached(model, input_ids, cache)
+
+        def forward(nxt):
+            return forward_cached(model, nxt[:, None], cache)
     out = [input_ids]
     finished = torch.zeros(B, dtype=torch.bool, device=input_ids.device)
-    for _ in range(max_new_tokens):
+    all_done = []  # device flags: every row finished after token t
+    for t in range(max_new_tokens):
         if do_sample:
             probs = torch.softmax(logits / max(temperature, 1e-5), -1)
             if top_p is not None and top_p < 1.0:
@@ -100,11 +225,18 @@ def generate(model, input_ids: torch.Tensor, max_new_tokens: int = 32,
         if pad_token_id is not None:
             nxt = torch.where(finished, torch.full_like(nxt, pad_token_id), nxt)
         out.append(nxt[:, None])
-        if eos:
-            finished |= torch.isin(nxt, torch.tensor(sorted(eos), device=nxt.device))
-            if bool(finished.all()):
+        if eos_t is not None:
+            finished |= torch.isin(nxt, eos_t)
+            all_done.append(finished.all())
+            if (t + 1) % sync_every == 0 and bool(finished.all()):
                 break
-        logits = forward_cached(model, nxt[:, None], cache)
+        if t + 1 < max_new_tokens:
+            logits = forward(nxt)
+    if all_done:  # HF stops right after the token that finished the last row
+        flags = torch.stack(all_done)
+        if bool(flags.any()):
+            first = int(flags.nonzero()[0, 0])
+            out = out[:first + 2]
     if was:
         model.train()
     return torch.cat(out, 1)

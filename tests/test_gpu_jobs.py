@@ -66,3 +66,20 @@ def test_basic_llm_job_on_gpu(_rt, tmp_path):
                     "--pvc", str(tmp_path), "--dtype", "bf16", "--max-windows", "2048"])
     assert res.metrics["loss"] < 5.0
     assert os.path.exists(os.path.join(res.checkpoint.path, "model.pth"))
+
+
+def test_graph_decode_matches_eager_decode():
+    """HIP-graph decode (one captured step replayed per token, device-side positions and KV
+    lengths) produces the same tokens as the eager cached decode, incl. EOS trimming."""
+    from gke_ray_train_amd.models import build_llama
+    m = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=0)
+    g = torch.Generator(device="cuda").manual_seed(4)
+    ids = torch.randint(0, 512, (2, 37), device="cuda", generator=g)
+    eager = m.generate(ids, max_new_tokens=40, use_graph=False)
+    graph = m.generate(ids, max_new_tokens=40, use_graph=True)
+    assert eager.shape == graph.shape == (2, 77)
+    assert (eager == graph).float().mean().item() > 0.98, (eager[:, 37:], graph[:, 37:])
+    eos = int(eager[0, 37 + 5])  # a token row 0 emits early: HF stops once every row has finished
+    e2 = m.generate(ids, max_new_tokens=40, use_graph=False, eos_token_id=eos, pad_token_id=0)
+    g2 = m.generate(ids, max_new_tokens=40, use_graph=True, eos_token_id=eos, pad_token_id=0, sync_every=7)
+    assert e2.shape == g2.shape and (e2 == g2).float().mean().item() > 0.98
