@@ -25,17 +25,20 @@ FAMILIES = [
 ]
 
 
-def main(path, top=25):
+def main(path, total_steps, top=25):
+    """total_steps = warm-up + timed steps of the profiled run (the optimizer launches one AdamW
+    kernel per parameter group, or one per module chunk when overlapped)."""
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     ad = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
-    if len(ad) < 2:
-        sys.exit("need >= 2 optimizer steps in the trace")
-    t_begin = int(rows[ad[0]]["End_Timestamp"])
+    per = len(ad) // total_steps
+    if total_steps < 2 or per < 1 or len(ad) % total_steps:
+        sys.exit(f"{len(ad)} optimizer kernels do not split into {total_steps} steps")
+    t_begin = int(rows[ad[per - 1]]["End_Timestamp"])
     t_end = int(rows[ad[-1]]["End_Timestamp"])
-    steps = len(ad) - 1
+    steps = total_steps - 1
     fam = defaultdict(float)
-    per = defaultdict(lambda: [0.0, 0])
+    perk = defaultdict(lambda: [0.0, 0])
     busy = 0.0
     for r in rows:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
@@ -44,8 +47,8 @@ def main(path, top=25):
         d = (e - s) / 1e6
         busy += d
         n = r["Kernel_Name"]
-        per[n][0] += d
-        per[n][1] += 1
+        perk[n][0] += d
+        perk[n][1] += 1
         for f, pat in FAMILIES:
             if re.search(pat, n):
                 fam[f] += d
@@ -58,9 +61,9 @@ def main(path, top=25):
     for f, v in sorted(fam.items(), key=lambda x: -x[1]):
         print(f"| {f} | {v / steps:.2f} | {100 * v / busy:.1f} |")
     print("\n| ms/step | calls/step | avg us | kernel |\n|---|---|---|---|")
-    for n, (t, c) in sorted(per.items(), key=lambda x: -x[1][0])[:top]:
+    for n, (t, c) in sorted(perk.items(), key=lambda x: -x[1][0])[:top]:
         print(f"| {t / steps:.2f} | {c / steps:.0f} | {1000 * t / c:.1f} | `{n[:110]}` |")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]))
