@@ -26,7 +26,7 @@ def enable_tuned_gemms(path: str | os.PathLike | None = None) -> bool:
     global _enabled
     if os.environ.get("GRT_TUNED_GEMM", "1") == "0" or not torch.cuda.is_available():
         return False
-    p = Path(path) if path else RESULTS
+    p = Path(path or os.environ.get("GRT_TUNED_GEMM_FILE") or RESULTS)
     if not p.exists():
         return False
     tun = torch.cuda.tunable

@@ -14,6 +14,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--tokens", type=int, default=8192)
 ap.add_argument("--models", default="llama2-7b")
 ap.add_argument("--out", default=str(RESULTS))
+ap.add_argument("--rotating-mb", type=int, default=0,
+                help="rotate operands over this many MB while timing candidates (>256 MB defeats the "
+                     "Infinity Cache: in-step conditions, where activations and weights arrive cold)")
+ap.add_argument("--iters", type=int, default=40)
 a = ap.parse_args()
 
 from gke_ray_train_amd.models import get_config  # noqa: E402
@@ -22,7 +26,9 @@ tun = torch.cuda.tunable
 tun.enable(True)
 tun.tuning_enable(True)
 tun.set_max_tuning_duration(30)
-tun.set_max_tuning_iterations(40)
+tun.set_max_tuning_iterations(a.iters)
+if a.rotating_mb:
+    tun.set_rotating_buffer_size(a.rotating_mb)
 os.makedirs(os.path.dirname(a.out), exist_ok=True)
 tun.set_filename(a.out)
 T = a.tokens
