@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--micro-batch", type=int, default=0, help="micro-batch (grad accumulation); 0 = batch")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--parallel", default="ddp", choices=["ddp", "fsdp"])
+    ap.add_argument("--sp", type=int, default=1, help="sequence-parallel degree (Ulysses all-to-all, "
+                    "parallel/sequence.py): groups of --sp consecutive ranks share each sequence")
     ap.add_argument("--offload", action="store_true", help="FSDP: optimizer states in pinned host memory")
     ap.add_argument("--peft", default="none", choices=["none", "lora", "qlora"])
     ap.add_argument("--lora-r", type=int, default=64)
@@ -92,6 +94,9 @@ def build(a, cfg, dev, dtype, world):
     model = build_llama(cfg, device=dev, dtype=dtype, seed=1234)
     if a.checkpointing:
         model.gradient_checkpointing_enable()
+    if a.sp > 1:
+        from gke_ray_train_amd.parallel.sequence import enable_sequence_parallel
+        enable_sequence_parallel(model, a.sp_group)
     fwd = model
     if a.peft != "none":
         from gke_ray_train_amd.peft import BitsAndBytesConfig, LoraConfig, get_peft_model, quantize_model_
@@ -129,6 +134,16 @@ def main():
     from gke_ray_train_amd.data import TokenBatchLoader, synthetic_tokens
     from gke_ray_train_amd.models import get_config
 
+    a.sp_group = None
+    if a.sp > 1:
+        if world % a.sp or a.parallel != "ddp" or a.peft != "none":
+            raise SystemExit("--sp needs world % sp == 0 and the DDP engine without PEFT")
+        for g0 in range(0, world, a.sp):  # every rank creates every group (collective)
+            grp = dist.new_group(list(range(g0, g0 + a.sp)))
+            if g0 <= rank < g0 + a.sp:
+                a.sp_group = grp
+    dp_world, dp_rank = world // a.sp, rank // a.sp
+
     torch.manual_seed(1234)
     dtype = torch.float32 if cpu else torch.bfloat16
     tuned = False
@@ -145,7 +160,7 @@ def main():
     total_micro = (a.warmup + a.steps) * accum
     if a.data == "loader":
         toks = synthetic_tokens(max(total_micro * mb * a.seq * world + a.seq + 2, 1 << 20), cfg.vocab_size, seed=7)
-        loader = TokenBatchLoader(toks, a.seq, mb, device=dev, rank=rank, world=world, shuffle=True, seed=3,
+        loader = TokenBatchLoader(toks, a.seq, mb, device=dev, rank=dp_rank, world=dp_world, shuffle=True, seed=3,
                                   stride=a.seq)
         it = iter(loader)
 
@@ -153,7 +168,7 @@ def main():
             return next(it)[0]
     else:
         g = torch.Generator(device=dev)
-        g.manual_seed(rank + 17)
+        g.manual_seed(dp_rank + 17)  # ranks of one SP group share their sequences
         batches = [torch.randint(0, cfg.vocab_size, (mb, a.seq), device=dev, generator=g) for _ in range(4 * accum)]
 
         def next_batch(i):
@@ -178,7 +193,12 @@ def main():
             counter[0] += 1
             with eng.no_sync(j < accum - 1):
                 with ph("forward"):
-                    loss = call(ids, labels=ids)["loss"] / accum
+                    if a.sp > 1:  # this rank's S/sp tokens of its SP group's sequences
+                        from gke_ray_train_amd.parallel.sequence import shard_sequence
+                        ids_l, lab_l, w = shard_sequence(ids, a.sp_group)
+                        loss = call(ids_l, shifted_labels=lab_l)["loss"] * (w / accum)
+                    else:
+                        loss = call(ids, labels=ids)["loss"] / accum
                 with ph("backward"):
                     loss.backward()
         with ph("grad_sync"):
@@ -238,13 +258,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = 1000.0 * elapsed / a.steps
-    tokens_per_step = a.batch * a.seq * world
+    tokens_per_step = a.batch * a.seq * (world // a.sp)
     tps = tokens_per_step / (elapsed / a.steps)
     fpt = cfg.flops_per_token(a.seq)
     if a.peft != "none":
         fpt = fpt * 2.0 / 3.0  # frozen base: no weight-gradient GEMMs (adapter FLOPs are negligible)
     mfu = tps / world * fpt / 2.5e15
-    par = f"{'fsdp' if fsdp else 'dp'}{world}" + ("+zero1" if getattr(eng, "zero", False) else "") + \
+    par = f"{'fsdp' if fsdp else 'dp'}{world // a.sp}" + (f"+sp{a.sp}" if a.sp > 1 else "") + ("+zero1" if getattr(eng, "zero", False) else "") + \
         ("+offload" if a.offload else "") + \
         ("" if a.peft == "none" else f"+{a.peft}")
     if rank == 0:
@@ -261,7 +281,7 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if not cpu else "fp32",
             "data": "synthetic Wikitext-2-shaped token stream (Zipf ids) via the streaming loader; random-init weights",
-            "config": {"model": cfg.name, "global_batch": a.batch * world, "seq_len": a.seq, "parallelism": par,
+            "config": {"model": cfg.name, "global_batch": a.batch * (world // a.sp), "seq_len": a.seq, "parallelism": par,
                        "micro_batch": mb, "grad_accum": accum, "optimizer": "fused AdamW fp32 states",
                        "max_grad_norm": a.max_grad_norm, "activation_checkpointing": a.checkpointing,
                        "optimizer_overlap": type(opt).__name__ == "OverlappedOptimizer",

@@ -141,7 +141,12 @@ class LlamaAttention(nn.Module):
 
     def forward(self, x, B, S, cos, sin):
         qkv = self.qkv_proj(x)
-        o = ops.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, causal=True)
+        sp = getattr(self, "sp_group", None)
+        if sp is not None:  # sequence parallel: S is this rank's token count (parallel/sequence.py)
+            from ..parallel.sequence import ulysses_attention
+            o = ulysses_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, sp, causal=True)
+        else:
+            o = ops.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, causal=True)
         return self.o_proj(o)
 
 
@@ -245,7 +250,8 @@ class LlamaForCausalLM(nn.Module):
     # -------------------------------------------------------------- forward
     def hidden_states(self, input_ids):
         B, S = input_ids.shape
-        cos, sin = self.rope(S, input_ids.device)
+        # sequence parallel: RoPE tables span the full sequence (this rank holds S of S * sp_size)
+        cos, sin = self.rope(S * getattr(self, "sp_size", 1), input_ids.device)
         h = self.model.embed_tokens(input_ids).view(B * S, -1)
         residual = None
         for layer in self.model.layers:
@@ -259,18 +265,22 @@ class LlamaForCausalLM(nn.Module):
         x, _ = self.model.norm(h, residual)
         return x
 
-    def forward(self, input_ids, labels=None, attention_mask=None, return_logits=None):
+    def forward(self, input_ids, labels=None, attention_mask=None, return_logits=None, shifted_labels=None):
+        """``labels``: HF convention (shifted here). ``shifted_labels``: already next-token aligned
+        (sequence-parallel shards, whose last token's label lives on the next rank)."""
         B, S = input_ids.shape
         x = self.hidden_states(input_ids)
         out = {}
-        if labels is not None:
+        if shifted_labels is not None:
+            out["loss"] = self.lm_head(x, labels=shifted_labels.reshape(-1))
+        elif labels is not None:
             # shift labels (not logits): position t predicts token t+1
             shifted = torch.full_like(labels, -100)
             shifted[:, :-1] = labels[:, 1:]
             if attention_mask is not None:
                 shifted[:, :-1].masked_fill_(attention_mask[:, 1:] == 0, -100)
             out["loss"] = self.lm_head(x, labels=shifted.view(-1))
-        if labels is None or return_logits:
+        if (labels is None and shifted_labels is None) or return_logits:
             out["logits"] = self.lm_head(x).view(B, S, -1)
         return out
 

@@ -114,3 +114,31 @@ def test_overlapped_optimizer_matches_serial():
     assert runs[0][0] == runs[1][0]
     for k, v in runs[0][1].items():
         assert torch.equal(v, runs[1][1][k]), k
+
+
+def test_sequence_parallel_single_rank_matches_plain_on_gpu():
+    """Ulysses path on the GPU (RoPE at absolute positions through the HIP kernel's position array,
+    all-to-all degenerate at P=1, flash kernel) == the fused rope_attention path."""
+    import os
+    import torch.distributed as dist
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.parallel.sequence import enable_sequence_parallel, shard_sequence
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29671")
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        ids = torch.randint(0, 512, (2, 256), device="cuda", generator=torch.Generator(device="cuda").manual_seed(2))
+        a = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=4)
+        b = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=4)
+        enable_sequence_parallel(b)
+        la = a(ids, labels=ids)["loss"]
+        la.backward()
+        ids_l, lab_l, w = shard_sequence(ids)
+        lb = b(ids_l, shifted_labels=lab_l)["loss"] * w
+        lb.backward()
+        assert abs(la.item() - lb.item()) < 1e-3 * max(1.0, la.item())
+        for (n, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+            rel = (pa.grad.float() - pb.grad.float()).norm() / pa.grad.float().norm().clamp_min(1e-12)
+            assert rel < 2e-2, (n, float(rel))
+    finally:
+        dist.destroy_process_group()
