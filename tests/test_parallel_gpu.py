@@ -142,3 +142,29 @@ def test_sequence_parallel_single_rank_matches_plain_on_gpu():
             assert rel < 2e-2, (n, float(rel))
     finally:
         dist.destroy_process_group()
+
+
+def test_llama3_70b_shapes_fsdp_offload_step():
+    """BASELINE config #5 shapes on one GPU: Llama-3-70B layer geometry (d 8192, GQA 64:8,
+    FFN 28672, V 128256) with 2 of its 80 layers, FSDP meta init + CPU-offloaded AdamW, two steps
+    through every HIP kernel at those shapes; loss finite and decreasing."""
+    from gke_ray_train_amd.models.llama import LlamaForCausalLM, RMSNorm, get_config
+    from gke_ray_train_amd.parallel.fsdp import FullyShardedDataParallel
+    cfg = get_config("llama3-70b", num_hidden_layers=2)
+    m = LlamaForCausalLM(cfg, device="meta", dtype=torch.bfloat16)
+
+    def init(mod):
+        with torch.no_grad():
+            if isinstance(mod, (torch.nn.Linear, torch.nn.Embedding)):
+                mod.weight.normal_(0, 0.02)
+            elif isinstance(mod, RMSNorm):
+                mod.weight.fill_(1.0)
+    f = FullyShardedDataParallel(m, param_init_fn=init, device="cuda", cpu_offload=True)
+    opt = f.build_optimizer(lr=1e-4)
+    ids = torch.randint(0, cfg.vocab_size, (2, 1024), device="cuda", generator=torch.Generator(device="cuda").manual_seed(1))
+    losses = []
+    for _ in range(3):
+        loss, _ = _step(f, opt, ids)
+        losses.append(loss)
+    assert all(l == l and l < 20 for l in losses), losses
+    assert losses[-1] < losses[0], losses
