@@ -27,6 +27,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -55,7 +56,10 @@ def parse():
     ap.add_argument("--max-grad-norm", type=float, default=0.3)
     ap.add_argument("--lr", type=float, default=2e-5)
     ap.add_argument("--checkpointing", action="store_true", help="activation checkpointing")
-    ap.add_argument("--data", default="loader", choices=["loader", "static"])
+    ap.add_argument("--data", default="loader", choices=["loader", "pipeline", "static"],
+                    help="loader: native window gather + pinned H2D; pipeline: the Ray-Data-like Dataset "
+                         "(shuffle -> map_batches -> per-rank streaming shard -> iter_torch_batches, produced "
+                         "in a separate process through the shared-memory ring); static: on-device batches")
     ap.add_argument("--profile-dir", default="", help="write a torch.profiler trace here")
     ap.add_argument("--metrics-jsonl", default="", help="per-step metrics (phase breakdown, MFU, HBM) -> JSONL; "
                     "adds one host sync per step, so it is off for the headline number")
@@ -166,6 +170,18 @@ def main():
 
         def next_batch(_i):
             return next(it)[0]
+    elif a.data == "pipeline":
+        from gke_ray_train_amd.data.pipeline import Dataset
+        n_win = total_micro * mb * dp_world + 8 * dp_world
+        toks = synthetic_tokens(n_win * a.seq, cfg.vocab_size, seed=7)
+        ds = (Dataset.from_numpy({"input_ids": toks.reshape(n_win, a.seq)}, parallelism=16)
+              .random_shuffle(seed=3)
+              .map_batches(lambda b: {"input_ids": b["input_ids"].astype(np.int64)}))
+        it = iter(ds.shard_for_rank(dp_rank, dp_world).iter_torch_batches(
+            batch_size=mb, device=dev, drop_last=True, producer_process=True))
+
+        def next_batch(_i):
+            return next(it)["input_ids"]
     else:
         g = torch.Generator(device=dev)
         g.manual_seed(dp_rank + 17)  # ranks of one SP group share their sequences
@@ -280,7 +296,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16" if not cpu else "fp32",
-            "data": "synthetic Wikitext-2-shaped token stream (Zipf ids) via the streaming loader; random-init weights",
+            "data": "synthetic Wikitext-2-shaped token stream (Zipf ids) via "
+                    + {"loader": "the streaming loader", "pipeline": "the Ray-Data-like pipeline (shm-ring producer process)",
+                       "static": "on-device batches"}[a.data] + "; random-init weights",
             "config": {"model": cfg.name, "global_batch": a.batch * (world // a.sp), "seq_len": a.seq, "parallelism": par,
                        "micro_batch": mb, "grad_accum": accum, "optimizer": "fused AdamW fp32 states",
                        "max_grad_norm": a.max_grad_norm, "activation_checkpointing": a.checkpointing,
