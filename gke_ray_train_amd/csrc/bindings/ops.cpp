@@ -466,6 +466,33 @@ Tensor nf4_dequantize(const Tensor& q, const Tensor& absmax, int64_t n, int64_t 
   return w;
 }
 
+Tensor nf4_dequantize_t(const Tensor& q, const Tensor& absmax, int64_t rows, int64_t cols, int64_t blocksize) {
+  check_contig(q, "q");
+  check_contig(absmax, "absmax");
+  TORCH_CHECK(blocksize == 64 && cols % 64 == 0, "nf4_dequantize_t: blocksize 64 and cols % 64 == 0");
+  TORCH_CHECK(q.numel() * 2 == rows * cols && absmax.numel() * blocksize == rows * cols, "nf4 shapes");
+  TORCH_CHECK(rows <= INT32_MAX && cols <= INT32_MAX, "nf4_dequantize_t: dims");
+  c10::OptionalDeviceGuard g(q.device());
+  Tensor wt = at::empty({cols, rows}, q.options().dtype(at::kBFloat16));
+  grt::nf4_dequantize_t(q.data_ptr<uint8_t>(), absmax.data_ptr<float>(), wt.data_ptr(), (int)rows, (int)cols,
+                        (int)blocksize, cur_stream(q));
+  return wt;
+}
+
+void transpose_into(const Tensor& src, Tensor& dst) {
+  check_contig(src, "src");
+  check_contig(dst, "dst");
+  TORCH_CHECK(src.dim() == 2 && dst.dim() == 2 && src.scalar_type() == at::kBFloat16 &&
+                  dst.scalar_type() == at::kBFloat16, "transpose: 2-D bf16");
+  const int64_t R = src.size(0), Cc = src.size(1);
+  TORCH_CHECK(dst.size(0) == Cc && dst.size(1) == R, "transpose: dst must be [cols, rows]");
+  TORCH_CHECK(R % 64 == 0 && Cc % 64 == 0 && R <= INT32_MAX && Cc <= INT32_MAX, "transpose: dims must be multiples of 64");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0,
+              "transpose: 16-byte alignment");
+  c10::OptionalDeviceGuard g(src.device());
+  grt::transpose_bf16(src.data_ptr(), dst.data_ptr(), (int)R, (int)Cc, cur_stream(src));
+}
+
 // ------------------------------------------------------------------ embedding
 Tensor embedding_fwd(const Tensor& ids, const Tensor& w) {
   check_contig(ids, "ids");
@@ -633,6 +660,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
+  m.def("nf4_dequantize_t", &nf4_dequantize_t);
+  m.def("transpose_into", &transpose_into);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("gemm_wgrad", &gemm_wgrad, py::arg("x"), py::arg("y"), py::arg("out"), py::arg("accumulate"),

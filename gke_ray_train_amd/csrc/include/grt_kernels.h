@@ -117,6 +117,9 @@ void nf4_quantize(DType dt, const void* w, uint8_t* q, float* absmax, int64_t n,
                   hipStream_t s);
 void nf4_dequantize(DType dt, const uint8_t* q, const float* absmax, void* w, int64_t n,
                     int blocksize, hipStream_t s);
+// W^T [cols][rows] (bf16) from the NF4 codes of W [rows][cols]; cols % 64 == 0, blocksize 64
+void nf4_dequantize_t(const uint8_t* q, const float* absmax, void* wt, int rows, int cols, int blocksize,
+                      hipStream_t s);
 
 // ---------------- token embedding (embedding.hip) ----------------
 // out[i] = w[ids[i]]; rows of d elements (d % 8 == 0 for bf16, % 4 for fp32)
@@ -139,6 +142,10 @@ struct GemmTTParams {
 };
 bool gemm_tt_supported(int P, int Q, int R);
 void gemm_tt(const GemmTTParams& p, hipStream_t stream, int mode = 0);  // mode != 0: diagnostics
+
+// ---------------- transpose (transpose.hip) ----------------
+// dst [cols][rows] = src [rows][cols]^T, bf16, rows and cols multiples of 64, row-major contiguous
+void transpose_bf16(const void* src, void* dst, int rows, int cols, hipStream_t s);
 
 // ---------------- xGMI peer-to-peer collectives (ipc_comm.hip) ----------------
 constexpr int kIpcMaxRanks = 8;

@@ -70,7 +70,55 @@ __global__ __launch_bounds__(256) void nf4_dequant_kernel(const uint8_t* __restr
   }
 }
 
+// Transposing dequantisation for the input-gradient GEMM (dX = dY W runs as the TN GEMM on W^T):
+// one workgroup = a 64 x 64 tile of W [rows][cols] (cols a multiple of 64, so each tile row is one
+// 64-weight quant block: one absmax per tile row). Dequantised into an LDS tile (padded row), then
+// written transposed as 16-byte row segments of W^T [cols][rows].
+__global__ __launch_bounds__(256) void nf4_dequant_t_kernel(const uint8_t* __restrict__ q,
+                                                            const float* __restrict__ absmax, bf16* __restrict__ wt,
+                                                            int rows, int cols, int bs) {
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int t = threadIdx.x;
+  {  // read: thread t -> tile row t/4, 16 consecutive codes (8 bytes)
+    const int tr = t >> 2, tc = (t & 3) * 16;
+    const int r = r0 + tr;
+    if (r < rows) {
+      const int64_t e = (int64_t)r * cols + c0 + tc;
+      const uint2 codes = *reinterpret_cast<const uint2*>(q + e / 2);
+      const float sc = absmax[e / bs];
+      const uint32_t wds[2] = {codes.x, codes.y};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t byte = (wds[k >> 2] >> (8 * (k & 3))) & 0xFF;
+        tile[tr][tc + 2 * k] = kNF4[byte >> 4] * sc;
+        tile[tr][tc + 2 * k + 1] = kNF4[byte & 15] * sc;
+      }
+    }
+  }
+  __syncthreads();
+  {  // write: thread t -> W^T row c0 + t/4, 16 consecutive entries (rows r0 + 16*(t&3) ...)
+    const int oc = t >> 2, orr = (t & 3) * 16;
+    float o[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) o[k] = tile[orr + k][oc];
+    bf16* dst = wt + (int64_t)(c0 + oc) * rows + r0 + orr;
+    if (r0 + orr + 16 <= rows) {
+      store16(dst, o);
+      store16(dst + 8, o + 8);
+    } else {
+      for (int k = 0; k < 16 && r0 + orr + k < rows; ++k) dst[k] = static_cast<bf16>(o[k]);
+    }
+  }
+}
+
 }  // namespace
+
+void nf4_dequantize_t(const uint8_t* q, const float* absmax, void* wt, int rows, int cols, int blocksize,
+                      hipStream_t s) {
+  const dim3 grid((unsigned)(cols / 64), (unsigned)((rows + 63) / 64));
+  hipLaunchKernelGGL(nf4_dequant_t_kernel, grid, dim3(256), 0, s, q, absmax, (bf16*)wt, rows, cols, blocksize);
+}
 
 void nf4_quantize(DType dt, const void* w, uint8_t* q, float* absmax, int64_t n, int blocksize, hipStream_t s) {
   const unsigned grid = (unsigned)((n / 2 + 255) / 256);

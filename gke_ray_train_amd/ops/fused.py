@@ -12,7 +12,7 @@ import torch
 
 from .. import _native
 from . import _ref
-from .linear import wgrad
+from .linear import input_grad, transpose_for_backward, wgrad
 
 
 def _gpu(t: torch.Tensor) -> bool:
@@ -308,6 +308,7 @@ class _LMHeadCE(torch.autograd.Function):
         loss_rows, lse = C.ce_fwd(logits, labels, ignore_index)
         nvalid = (labels != ignore_index).sum().clamp_min(1).float()
         ctx.save_for_backward(hidden, weight, logits, labels, lse, nvalid)
+        ctx.wt_ev = transpose_for_backward(weight) if ctx.needs_input_grad[0] else None
         ctx.ignore_index = ignore_index
         ctx.has_bias = bias is not None
         return loss_rows.sum() / nvalid
@@ -319,7 +320,8 @@ class _LMHeadCE(torch.autograd.Function):
         dlogits = _native.kernels().ce_bwd(logits, labels, lse, gscale, ctx.ignore_index, True)
         dh = dw = db = None
         if ctx.needs_input_grad[0]:
-            dh = dlogits @ weight
+            dh = input_grad(dlogits, weight, ctx.wt_ev)
+            ctx.wt_ev = None
         if ctx.needs_input_grad[1]:
             slot = getattr(weight, "_grt_slot", None)
             if slot is not None:   # GEMM writes dW straight into the DDP bucket (ops/linear.py)

@@ -31,6 +31,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from .. import _native, ops
+from ..ops.linear import input_grad
 from .quant import NF4Linear
 
 
@@ -58,6 +59,14 @@ class LoraConfig:
 
 def _base_weight(base: nn.Module) -> torch.Tensor:
     return base.dequantize() if isinstance(base, NF4Linear) else base.weight
+
+
+def _base_input_grad(base: nn.Module, dy2: torch.Tensor) -> torch.Tensor:
+    """dX of the frozen base projection: TN GEMM on a transposed weight (cached for a bf16 base;
+    for NF4 the dequantising kernel writes W^T directly)."""
+    if isinstance(base, NF4Linear):
+        return base.input_grad(dy2)
+    return input_grad(dy2, base.weight)
 
 
 class _LoraFn(torch.autograd.Function):
@@ -96,9 +105,7 @@ class _LoraFn(torch.autograd.Function):
             dy2 = dy2.to(acat.dtype)
         dx = None
         if ctx.needs_input_grad[0]:
-            w = _base_weight(ctx.base)
-            dx = dy2 @ w                                     # base dX (frozen weight)
-            del w
+            dx = _base_input_grad(ctx.base, dy2)           # base dX (frozen weight)
         gs, dBs = [], []
         for i, (off, n) in enumerate(spec):
             dyi = dy2[:, off:off + n]

@@ -44,8 +44,8 @@ class _NF4Matmul(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        w = ctx.layer.dequantize()  # recomputed: the bf16 weight is never kept alive for autograd
-        return dy @ w, None
+        # recomputed (the bf16 weight is never kept alive for autograd), dequantised transposed
+        return ctx.layer.input_grad(dy), None
 
 
 class NF4Linear(nn.Module):
@@ -101,6 +101,17 @@ class NF4Linear(nn.Module):
         n = self.in_features * self.out_features
         w = ops.nf4_dequantize(self.qweight, self._absmax().contiguous(), n, self.blocksize, self.compute_dtype)
         return w.view(self.out_features, self.in_features)
+
+    def input_grad(self, dy: torch.Tensor) -> torch.Tensor:
+        """dX = dY W: on MI355X the HIP kernel dequantises straight into W^T so the GEMM runs in the
+        TN layout (ops.linear.input_grad); elsewhere dY @ W."""
+        if dy.is_cuda and self.compute_dtype == torch.bfloat16 and self.blocksize == 64 \
+                and self.in_features % 64 == 0 and self.out_features % 8 == 0:
+            from .. import _native
+            wt = _native.kernels().nf4_dequantize_t(self.qweight, self._absmax().contiguous(), self.out_features,
+                                                    self.in_features, self.blocksize)
+            return F.linear(dy, wt)
+        return dy @ self.dequantize()
 
     @property
     def weight(self):  # read-only dequantised view (merge_and_unload, inspection)

@@ -429,3 +429,41 @@ def test_fused_lora_matches_reference(nf4, p):
         for got, ref, what in ((mod.lora_A[n].grad, A[n].grad, "dA"), (mod.lora_B[n].grad, B[n].grad, "dB")):
             rel = (got.float() - ref).norm() / ref.norm().clamp_min(1e-6)
             assert rel < 2e-2, f"lora {what} {n}: rel err {rel.item():.3g}"
+
+
+def test_transpose_and_nf4_dequant_t():
+    """HIP transpose and transposing NF4 dequant match torch exactly."""
+    from gke_ray_train_amd import ops
+    C = _C()
+    w = torch.randn(384, 640, device=DEV, dtype=torch.bfloat16)
+    wt = torch.empty(640, 384, device=DEV, dtype=torch.bfloat16)
+    C.transpose_into(w, wt)
+    assert torch.equal(wt, w.t())
+    q, absmax = ops.nf4_quantize(w.reshape(-1), 64)
+    deq = ops.nf4_dequantize(q, absmax, w.numel(), 64, torch.bfloat16).view(384, 640)
+    assert torch.equal(C.nf4_dequantize_t(q, absmax, 384, 640, 64), deq.t())
+
+
+def test_transposed_dgrad_linear_matches_nn():
+    """Trainable DDP weight: forward writes W^T on a side stream, backward runs the TN GEMM;
+    gradients equal the NN path (GRT_TRANSPOSED_DGRAD=0) to bf16 rounding."""
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.ops import linear as L
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    ids = torch.randint(0, 512, (2, 256), device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+    out = []
+    L._TRANSPOSED_DGRAD_TRAINABLE = True
+    for flag in (False, True):
+        L._TRANSPOSED_DGRAD = flag
+        m = build_llama("llama-tiny-gqa", device=DEV, dtype=torch.bfloat16, seed=2)
+        ddp = DistributedDataParallel(m)
+        m(ids, labels=ids)["loss"].backward()
+        ddp.finish_gradient_sync()
+        out.append({n: p.grad.float().clone() for n, p in m.named_parameters()})
+        if flag:
+            assert any(getattr(p, "_grt_wt_buf", None) is not None for p in m.parameters())
+    L._TRANSPOSED_DGRAD = True
+    L._TRANSPOSED_DGRAD_TRAINABLE = False
+    for n in out[0]:
+        rel = (out[0][n] - out[1][n]).norm() / out[0][n].norm().clamp_min(1e-12)
+        assert rel < 1e-2, (n, float(rel))
