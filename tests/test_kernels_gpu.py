@@ -378,9 +378,10 @@ def test_embedding_module_autograd(monkeypatch):
     _close(e.weight.grad, ref, 2e-2, 2e-2, "Embedding module grad")
 
 
+@pytest.mark.parametrize("targets", ["qv", "qkv"])
 @pytest.mark.parametrize("nf4", [False, True])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_fused_lora_matches_reference(nf4, p):
+def test_fused_lora_matches_reference(nf4, p, targets):
     """The fused LoRA op (epilogue accumulation, seeded dropout regenerated in backward, in-place
     dX accumulation) equals the unfused formula y = W x + s * B_i A_i drop(x) per target slice."""
     from gke_ray_train_amd.ops.linear import Linear
@@ -394,9 +395,11 @@ def test_fused_lora_matches_reference(nf4, p):
     for q in base.parameters():
         q.requires_grad_(False)
     cfg = LoraConfig(r=16, lora_alpha=32, lora_dropout=p)
-    mod = LoraLinear(base, [("q_proj", 0, 256), ("v_proj", 512, 256)], cfg).train()
+    tg = [("q_proj", 0), ("v_proj", 512)] if targets == "qv" else [("q_proj", 0), ("k_proj", 256), ("v_proj", 512)]
+    mod = LoraLinear(base, [(n, off, 256) for n, off in tg], cfg).train()
+    names = [n for n, _ in tg]
     with torch.no_grad():
-        for n in ("q_proj", "v_proj"):
+        for n in names:
             mod.lora_B[n].normal_(0, 0.05)
     x = torch.randn(4, 64, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     from gke_ray_train_amd.ops import fused
@@ -408,8 +411,8 @@ def test_fused_lora_matches_reference(nf4, p):
     seed = int(torch.cuda.default_generators[0].initial_seed()) & 0xFFFFFF
     x2 = x.detach().view(-1, 256).float().requires_grad_()
     w = (base.dequantize() if nf4 else lin.weight).detach().float()
-    A = {n: mod.lora_A[n].detach().float().requires_grad_() for n in ("q_proj", "v_proj")}
-    B = {n: mod.lora_B[n].detach().float().requires_grad_() for n in ("q_proj", "v_proj")}
+    A = {n: mod.lora_A[n].detach().float().requires_grad_() for n in names}
+    B = {n: mod.lora_B[n].detach().float().requires_grad_() for n in names}
     if p > 0:
         xb = x.detach().view(-1, 256).contiguous()
         keep = (_native.kernels().dropout_fwd_seeded(torch.ones_like(xb), p, seed, start) != 0).float()
@@ -418,12 +421,12 @@ def test_fused_lora_matches_reference(nf4, p):
         xd = x2
     yr = x2 @ w.t()
     yr = yr.clone()
-    for n, off in (("q_proj", 0), ("v_proj", 512)):
+    for n, off in tg:
         yr[:, off:off + 256] = yr[:, off:off + 256] + cfg.scaling * (xd @ A[n].t()) @ B[n].t()
     (yr * dy.view(-1, 768).float()).sum().backward()
     _close(y.view(-1, 768), yr, 3e-2, 3e-2, "lora y")
     _close(x.grad.view(-1, 256), x2.grad, 3e-2, 3e-2, "lora dx")
-    for n in ("q_proj", "v_proj"):
+    for n in names:
         # adapter grads are reductions over all tokens of bf16 intermediates (as in PEFT under bf16):
         # compare by relative Frobenius error
         for got, ref, what in ((mod.lora_A[n].grad, A[n].grad, "dA"), (mod.lora_B[n].grad, B[n].grad, "dB")):
