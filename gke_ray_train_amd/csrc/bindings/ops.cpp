@@ -440,6 +440,44 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   return {dq, dk, dv};
 }
 
+Tensor attn_decode(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& seqlens_k, double scale) {
+  check_bshd(q, "q");
+  check_bshd(k, "k");
+  check_bshd(v, "v");
+  TORCH_CHECK(q.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 && v.scalar_type() == at::kBFloat16,
+              "attn_decode: bf16");
+  TORCH_CHECK(q.size(1) == 1, "attn_decode: one query token per sequence");
+  TORCH_CHECK(k.sizes() == v.sizes() && k.size(0) == q.size(0), "attn_decode: k/v shapes");
+  const int64_t Hq = q.size(2), Hkv = k.size(2);
+  TORCH_CHECK(Hq % Hkv == 0, "attn_decode: Hq % Hkv");
+  const int64_t G = Hq / Hkv;
+  TORCH_CHECK(G == 1 || G == 2 || G == 4 || G == 8, "attn_decode: GQA group must be 1, 2, 4 or 8");
+  c10::OptionalDeviceGuard g(q.device());
+  grt::AttnDecodeParams p{};
+  p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr();
+  auto o = at::empty(q.sizes(), q.options());
+  p.o = o.data_ptr();
+  p.q_bs = q.stride(0); p.q_hs = q.stride(2);
+  p.k_bs = k.stride(0); p.k_ss = k.stride(1); p.k_hs = k.stride(2);
+  p.v_bs = v.stride(0); p.v_ss = v.stride(1); p.v_hs = v.stride(2);
+  p.o_bs = o.stride(0); p.o_hs = o.stride(2);
+  p.B = (int)q.size(0); p.Hq = (int)Hq; p.Hkv = (int)Hkv; p.Sk = (int)k.size(1);
+  p.NS = grt::attn_decode_splits(p.B, p.Hkv, p.Sk);
+  p.seqlens_k = nullptr;
+  if (seqlens_k.has_value()) {
+    check_contig(*seqlens_k, "seqlens_k");
+    TORCH_CHECK(seqlens_k->scalar_type() == at::kInt && seqlens_k->numel() == q.size(0), "seqlens_k int32 [B]");
+    p.seqlens_k = seqlens_k->data_ptr<int32_t>();
+  }
+  p.scale_log2 = (float)(scale * 1.4426950408889634);
+  auto ws = at::empty({(int64_t)p.B * Hq * p.NS * (128 + 2)}, q.options().dtype(at::kFloat));
+  p.part_o = ws.data_ptr<float>();
+  p.part_m = p.part_o + (int64_t)p.B * Hq * p.NS * 128;
+  p.part_l = p.part_m + (int64_t)p.B * Hq * p.NS;
+  grt::attn_decode(p, cur_stream(q));
+  return o;
+}
+
 // ------------------------------------------------------------------ NF4
 std::vector<Tensor> nf4_quantize(const Tensor& w, int64_t blocksize) {
   check_contig(w, "w");
@@ -491,6 +529,23 @@ void transpose_into(const Tensor& src, Tensor& dst) {
               "transpose: 16-byte alignment");
   c10::OptionalDeviceGuard g(src.device());
   grt::transpose_bf16(src.data_ptr(), dst.data_ptr(), (int)R, (int)Cc, cur_stream(src));
+}
+
+Tensor gemv(const Tensor& x, const Tensor& w) {
+  check_cuda(x, "x");
+  check_contig(w, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "gemv: x [M, K], w [N, K]");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "gemv: bf16");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(M >= 1 && M <= 4, "gemv: 1..4 rows");
+  TORCH_CHECK(K % 8 == 0 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemv: K and row stride multiples of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemv: 16-byte alignment");
+  TORCH_CHECK(N <= INT32_MAX && K <= INT32_MAX, "gemv: dims");
+  c10::OptionalDeviceGuard g(x.device());
+  Tensor y = at::empty({M, N}, x.options());
+  grt::gemv_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), N, (int)M, (int)N, (int)K, cur_stream(x));
+  return y;
 }
 
 // ------------------------------------------------------------------ embedding
@@ -662,6 +717,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);
   m.def("transpose_into", &transpose_into);
+  m.def("gemv", &gemv);
+  m.def("attn_decode", &attn_decode);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("gemm_wgrad", &gemm_wgrad, py::arg("x"), py::arg("y"), py::arg("out"), py::arg("accumulate"),

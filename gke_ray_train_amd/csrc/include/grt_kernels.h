@@ -107,6 +107,17 @@ struct AttnBwdParams {
 };
 void attn_bwd(const AttnBwdParams& p, hipStream_t s);
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int D);
+// decode (Sq = 1) split-K attention (decode_attention.hip): bf16, head_dim 128, Hq / Hkv in {1,2,4,8}
+struct AttnDecodeParams {
+  const void* q; const void* k; const void* v; void* o;
+  int64_t q_bs, q_hs, k_bs, k_ss, k_hs, v_bs, v_ss, v_hs, o_bs, o_hs;
+  int B, Hq, Hkv, Sk, NS;
+  const int32_t* seqlens_k;   // valid keys per batch row (may be null: all Sk)
+  float scale_log2;           // softmax scale * log2(e)
+  float* part_o; float* part_m; float* part_l;  // workspace [B, Hq, NS, (D | 1 | 1)]
+};
+int attn_decode_splits(int B, int Hkv, int Sk);
+void attn_decode(const AttnDecodeParams& p, hipStream_t s);
 // exact-fp32 variants (attention_f32.hip): same params with fp32 tensors, head_dim 64 or 128
 bool attn_f32_supported(int head_dim);
 void attn_fwd_f32(const AttnParams& p, hipStream_t s);
@@ -146,6 +157,10 @@ void gemm_tt(const GemmTTParams& p, hipStream_t stream, int mode = 0);  // mode 
 // ---------------- transpose (transpose.hip) ----------------
 // dst [cols][rows] = src [rows][cols]^T, bf16, rows and cols multiples of 64, row-major contiguous
 void transpose_bf16(const void* src, void* dst, int rows, int cols, hipStream_t s);
+
+// ---------------- decode GEMV (gemv.hip) ----------------
+// y[m][n] = sum_k x[m][k] * w[n][k] for m < M <= 4; bf16, K % 8 == 0, rows 16-byte aligned
+void gemv_bf16(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int M, int N, int K, hipStream_t s);
 
 // ---------------- xGMI peer-to-peer collectives (ipc_comm.hip) ----------------
 constexpr int kIpcMaxRanks = 8;

@@ -187,6 +187,9 @@ class _FlashAttn(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None
 
 
+_DECODE_KERNEL = __import__("os").environ.get("GRT_DECODE_ATTN", "1") != "0"
+
+
 def _dropout_seed() -> int:
     # drawn from torch's CPU generator (torch.manual_seed reproducible, no device sync)
     return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
@@ -203,6 +206,12 @@ def flash_attention(q, k, v, causal=True, scale=None, seqlens_k=None, dropout_p=
     if dropout_p > 0.0 and seed is None:
         seed = _dropout_seed()
     seed = 0 if seed is None else int(seed)
+    if (_gpu(q) and q.shape[1] == 1 and q.dtype == torch.bfloat16 and q.shape[-1] == 128 and dropout_p == 0.0
+            and not torch.is_grad_enabled() and (q.shape[2] // k.shape[2]) in (1, 2, 4, 8)
+            and q.shape[2] % k.shape[2] == 0 and _DECODE_KERNEL):
+        # one query token per sequence (decode): split-K kernel over the cached keys; every cached
+        # key is at or before the query position, so the causal mask is the valid-length mask
+        return _native.kernels().attn_decode(q, k, v, seqlens_k, scale)
     if _gpu(q) and ((q.dtype == torch.bfloat16 and q.shape[-1] == 128) or
                     (q.dtype == torch.float32 and q.shape[-1] in (64, 128))):
         return _FlashAttn.apply(q, k, v, causal, scale, seqlens_k, float(dropout_p), seed)

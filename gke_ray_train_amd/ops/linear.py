@@ -190,9 +190,24 @@ class _DirectGradLinear(torch.autograd.Function):
         return dx, dw, db
 
 
+_GEMV = os.environ.get("GRT_GEMV", "1") != "0"
+
+
 def linear(x, weight, bias=None):
     if weight.requires_grad and getattr(weight, "_grt_slot", None) is not None and torch.is_grad_enabled():
         return _DirectGradLinear.apply(x, weight, bias)
+    K = weight.shape[-1]
+    if (_GEMV and x.is_cuda and not torch.is_grad_enabled() and x.dtype == torch.bfloat16
+            and weight.dtype == torch.bfloat16 and weight.dim() == 2 and weight.is_contiguous()
+            and x.numel() // K <= 4 and K % 8 == 0 and x.shape[-1] == K):
+        # decode: 1-4 tokens per step are a weight stream -> HBM-bound GEMV kernel (gemv.hip)
+        from .. import _native
+        x2 = x.reshape(-1, K)
+        if x2.stride(-1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0:
+            y = _native.kernels().gemv(x2, weight)
+            if bias is not None:
+                y = y + bias
+            return y.view(*x.shape[:-1], weight.shape[0])
     return F.linear(x, weight, bias)
 
 

@@ -470,3 +470,37 @@ def test_transposed_dgrad_linear_matches_nn():
     for n in out[0]:
         rel = (out[0][n] - out[1][n]).norm() / out[0][n].norm().clamp_min(1e-12)
         assert rel < 1e-2, (n, float(rel))
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (1000, 11008), (37, 264)])
+def test_gemv_decode(M, N, K):
+    """Decode GEMV (gemv.hip) vs the fp32 product; routed automatically by ops.linear under no_grad."""
+    from gke_ray_train_amd.ops.linear import linear
+    g = torch.Generator(device=DEV).manual_seed(M * N + K)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16, generator=g) * 0.02
+    y = _C().gemv(x, w)
+    ref = x.float() @ w.float().t()
+    _close(y, ref, 2e-2, 2e-2, "gemv")
+    with torch.no_grad():
+        y2 = linear(x.view(M, 1, K), w)
+    assert y2.shape == (M, 1, N) and torch.equal(y2.view(M, N), y)
+
+
+@pytest.mark.parametrize("B,Sk,hq,hkv,pad", [(1, 1, 4, 4, False), (1, 600, 32, 8, False), (3, 77, 8, 1, True),
+                                             (2, 1300, 16, 8, True), (2, 33, 8, 4, False)])
+def test_decode_attention(B, Sk, hq, hkv, pad):
+    """Split-K decode kernel (decode_attention.hip) vs the fp32 math path: one query per sequence
+    at the last position (causal) or under a valid-length mask (seqlens_k)."""
+    from gke_ray_train_amd import ops
+    from gke_ray_train_amd.ops import _ref
+    g = torch.Generator(device=DEV).manual_seed(B * Sk + hq)
+    q = torch.randn(B, 1, hq, 128, device=DEV, dtype=torch.bfloat16, generator=g)
+    k = torch.randn(B, Sk, hkv, 128, device=DEV, dtype=torch.bfloat16, generator=g)
+    v = torch.randn(B, Sk, hkv, 128, device=DEV, dtype=torch.bfloat16, generator=g)
+    sl = torch.randint(1, Sk + 1, (B,), device=DEV, generator=g).to(torch.int32) if pad else None
+    with torch.no_grad():
+        o = ops.flash_attention(q, k, v, causal=not pad, seqlens_k=sl)
+    ref = _ref.attention(q.float(), k.float(), v.float(), causal=not pad, seqlens_k=sl)
+    _close(o, ref, 1e-2, 1e-2, "decode attention")

@@ -15,12 +15,17 @@ from gke_ray_train_amd.models import build_llama  # noqa: E402
 model = sys.argv[1] if len(sys.argv) > 1 else "llama3.1-8b"
 m = build_llama(model, device="cuda", dtype=torch.bfloat16, seed=0)
 ids = torch.randint(0, m.config.vocab_size, (1, 512), device="cuda")
-for mode in (False, True):
+from gke_ray_train_amd.ops import linear as _lin  # noqa: E402
+
+runs = [(False, True), (True, False), (True, True)]  # (graph, gemv)
+for mode, gemv in runs:
+    _lin._GEMV = gemv
     m.generate(ids, max_new_tokens=8, use_graph=mode)  # warm-up (kernels, graph pools)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     out = m.generate(ids, max_new_tokens=128, use_graph=mode)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(json.dumps({"model": model, "mode": "hip_graph" if mode else "eager", "new_tokens": out.shape[1] - 512,
+    print(json.dumps({"model": model, "mode": ("hip_graph" if mode else "eager") + ("+gemv" if gemv else "+library_gemm"),
+                      "new_tokens": out.shape[1] - 512,
                       "seconds": round(dt, 3), "tokens_per_s": round((out.shape[1] - 512) / dt, 1)}), flush=True)

@@ -1,0 +1,13 @@
+"""Llama-3.1-8B batch-1 decode (prompt 512, 64 new tokens, HIP graph + GEMV) for kernel profiling."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gke_ray_train_amd.models import build_llama  # noqa: E402
+
+m = build_llama("llama3.1-8b", device="cuda", dtype=torch.bfloat16, seed=0)
+ids = torch.randint(0, m.config.vocab_size, (1, 512), device="cuda")
+m.generate(ids, max_new_tokens=64, use_graph=False)
+torch.cuda.synchronize()
