@@ -265,21 +265,25 @@ class LlamaForCausalLM(nn.Module):
         x, _ = self.model.norm(h, residual)
         return x
 
-    def forward(self, input_ids, labels=None, attention_mask=None, return_logits=None, shifted_labels=None):
+    def forward(self, input_ids, labels=None, attention_mask=None, return_logits=None, shifted_labels=None,
+                loss_weights=None):
         """``labels``: HF convention (shifted here). ``shifted_labels``: already next-token aligned
-        (sequence-parallel shards, whose last token's label lives on the next rank)."""
+        (sequence-parallel shards, whose last token's label lives on the next rank).
+        ``loss_weights`` ([B, S] fp32, optional): the loss is the weighted SUM of the per-position
+        next-token CE (position t predicts t+1) instead of the mean over valid positions."""
         B, S = input_ids.shape
         x = self.hidden_states(input_ids)
         out = {}
+        rw = None if loss_weights is None else loss_weights.reshape(-1)
         if shifted_labels is not None:
-            out["loss"] = self.lm_head(x, labels=shifted_labels.reshape(-1))
+            out["loss"] = self.lm_head(x, labels=shifted_labels.reshape(-1), row_weights=rw)
         elif labels is not None:
             # shift labels (not logits): position t predicts token t+1
             shifted = torch.full_like(labels, -100)
             shifted[:, :-1] = labels[:, 1:]
             if attention_mask is not None:
                 shifted[:, :-1].masked_fill_(attention_mask[:, 1:] == 0, -100)
-            out["loss"] = self.lm_head(x, labels=shifted.view(-1))
+            out["loss"] = self.lm_head(x, labels=shifted.view(-1), row_weights=rw)
         if (labels is None and shifted_labels is None) or return_logits:
             out["logits"] = self.lm_head(x).view(B, S, -1)
         return out

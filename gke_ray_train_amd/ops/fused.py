@@ -308,24 +308,34 @@ def cross_entropy(logits, labels, ignore_index=-100, inplace_backward=False):
 
 class _LMHeadCE(torch.autograd.Function):
     """loss = CE(hidden @ W^T [+ b], labels): the logits never escape, so the backward writes
-    dlogits over the logits buffer in place (saves a [tokens, V] allocation per step)."""
+    dlogits over the logits buffer in place (saves a [tokens, V] allocation per step).
+
+    ``row_weights`` (fp32 [N], optional): loss = sum_i w_i * CE_i over non-ignored rows instead of
+    the mean; the CE backward kernel already takes a per-row gradient scale, so weighting costs
+    nothing (used to run several gradient-accumulation micro-batches as one batch, each keeping
+    its own mean — trainer/sft.py)."""
 
     @staticmethod
-    def forward(ctx, hidden, weight, bias, labels, ignore_index):
+    def forward(ctx, hidden, weight, bias, labels, ignore_index, row_weights):
         C = _native.kernels()
         logits = torch.nn.functional.linear(hidden, weight, bias)
         loss_rows, lse = C.ce_fwd(logits, labels, ignore_index)
-        nvalid = (labels != ignore_index).sum().clamp_min(1).float()
-        ctx.save_for_backward(hidden, weight, logits, labels, lse, nvalid)
+        if row_weights is None:
+            scale = (labels != ignore_index).sum().clamp_min(1).float().reciprocal()
+            loss = loss_rows.sum() * scale
+        else:
+            scale = row_weights * (labels != ignore_index)
+            loss = (loss_rows.float() * scale).sum()
+        ctx.save_for_backward(hidden, weight, logits, labels, lse, scale)
         ctx.wt_ev = transpose_for_backward(weight) if ctx.needs_input_grad[0] else None
         ctx.ignore_index = ignore_index
         ctx.has_bias = bias is not None
-        return loss_rows.sum() / nvalid
+        return loss
 
     @staticmethod
     def backward(ctx, g):
-        hidden, weight, logits, labels, lse, nvalid = ctx.saved_tensors
-        gscale = (g.float() / nvalid).expand(logits.shape[0]).contiguous()
+        hidden, weight, logits, labels, lse, scale = ctx.saved_tensors
+        gscale = (g.float() * scale).expand(logits.shape[0]).contiguous()
         dlogits = _native.kernels().ce_bwd(logits, labels, lse, gscale, ctx.ignore_index, True)
         dh = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -340,14 +350,19 @@ class _LMHeadCE(torch.autograd.Function):
                 dw = wgrad(dlogits, hidden)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dlogits.sum(0)
-        return dh, dw, db, None, None
+        return dh, dw, db, None, None, None
 
 
-def lm_head_cross_entropy(hidden, weight, labels, bias=None, ignore_index=-100):
+def lm_head_cross_entropy(hidden, weight, labels, bias=None, ignore_index=-100, row_weights=None):
+    """Mean CE of ``hidden @ weight^T`` over non-ignored rows, or the ``row_weights``-weighted sum."""
     if _gpu(hidden):
-        return _LMHeadCE.apply(hidden, weight, bias, labels.contiguous(), ignore_index)
+        rw = None if row_weights is None else row_weights.reshape(-1).float().contiguous()
+        return _LMHeadCE.apply(hidden, weight, bias, labels.contiguous(), ignore_index, rw)
     logits = torch.nn.functional.linear(hidden, weight, bias)
-    return _ref.cross_entropy(logits, labels, ignore_index)
+    if row_weights is None:
+        return _ref.cross_entropy(logits, labels, ignore_index)
+    rows = torch.nn.functional.cross_entropy(logits.float(), labels, ignore_index=ignore_index, reduction="none")
+    return (rows * row_weights.reshape(-1).float() * (labels != ignore_index)).sum()
 
 
 # ----------------------------------------------------------------------------- NF4

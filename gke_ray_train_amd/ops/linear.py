@@ -219,10 +219,11 @@ class Linear(nn.Linear):
     gather wait of parallel/ddp.py) firing for the head's weight.
     """
 
-    def forward(self, x, labels=None, ignore_index: int = -100):
+    def forward(self, x, labels=None, ignore_index: int = -100, row_weights=None):
         if labels is not None:
             from .fused import lm_head_cross_entropy
-            return lm_head_cross_entropy(x, self.weight, labels, bias=self.bias, ignore_index=ignore_index)
+            return lm_head_cross_entropy(x, self.weight, labels, bias=self.bias, ignore_index=ignore_index,
+                                         row_weights=row_weights)
         return linear(x, self.weight, self.bias)
 
 

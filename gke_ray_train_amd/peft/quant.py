@@ -3,13 +3,15 @@
 Reference role: ``BitsAndBytesConfig(load_in_4bit=True, bnb_4bit_quant_type="nf4",
 bnb_4bit_compute_dtype=bfloat16, bnb_4bit_use_double_quant=USE_NESTED_QUANT)``
 (ray-jobs/fine_tune_llama_ray.py:215-227). Weights are quantised once on the GPU by the HIP
-kernel (blocks of 64, fp32 absmax); every forward AND backward dequantises into a transient
-bf16 weight (never stored for autograd, so the base model costs ~0.53 bytes/param resident) and
-runs the hipBLASLt GEMM. ``double_quant`` additionally stores the absmax vector as 8-bit codes
+kernel (blocks of 64, fp32 absmax); forward and backward dequantise into a bf16 weight (never
+stored for autograd, so the base model costs ~0.53 bytes/param resident) and run the hipBLASLt
+GEMM — or, when ``set_dequant_cache`` finds room in HBM (auto for 8B on a 288 GB MI355X), reuse a
+resident dequantised W / W^T (bit-identical; the base is frozen). ``double_quant`` additionally stores the absmax vector as 8-bit codes
 with one fp32 scale per 256 blocks (bitsandbytes' nested quantisation) and expands it on device.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -97,25 +99,54 @@ class NF4Linear(nn.Module):
         sc = self.absmax_scale.repeat_interleave(256)[:nb]
         return codes / 127.0 * sc + self.absmax_offset
 
-    def dequantize(self) -> torch.Tensor:
+    def _dequant(self) -> torch.Tensor:
         n = self.in_features * self.out_features
         w = ops.nf4_dequantize(self.qweight, self._absmax().contiguous(), n, self.blocksize, self.compute_dtype)
         return w.view(self.out_features, self.in_features)
 
+    def _dequant_t(self) -> Optional[torch.Tensor]:
+        if self.qweight.is_cuda and self.compute_dtype == torch.bfloat16 and self.blocksize == 64 \
+                and self.in_features % 64 == 0 and self.out_features % 8 == 0:
+            from .. import _native
+            return _native.kernels().nf4_dequantize_t(self.qweight, self._absmax().contiguous(), self.out_features,
+                                                      self.in_features, self.blocksize)
+        return None
+
+    def _cache_key(self):
+        return (self.qweight.data_ptr(), self.qweight._version)
+
+    def dequantize(self) -> torch.Tensor:
+        """bf16 W [out, in]. With the dequant cache on (``set_dequant_cache``) the result of the
+        first call is kept until the packed weights change (frozen base: never in training)."""
+        if getattr(self, "_cache_on", False):
+            c = getattr(self, "_w_cache", None)
+            if c is None or c[0] != self._cache_key():
+                self._w_cache = c = (self._cache_key(), self._dequant())
+            return c[1]
+        return self._dequant()
+
     def input_grad(self, dy: torch.Tensor) -> torch.Tensor:
         """dX = dY W: on MI355X the HIP kernel dequantises straight into W^T so the GEMM runs in the
         TN layout (ops.linear.input_grad); elsewhere dY @ W."""
-        if dy.is_cuda and self.compute_dtype == torch.bfloat16 and self.blocksize == 64 \
-                and self.in_features % 64 == 0 and self.out_features % 8 == 0:
-            from .. import _native
-            wt = _native.kernels().nf4_dequantize_t(self.qweight, self._absmax().contiguous(), self.out_features,
-                                                    self.in_features, self.blocksize)
+        if getattr(self, "_cache_on", False):
+            c = getattr(self, "_wt_cache", None)
+            if c is None or c[0] != self._cache_key():
+                self._wt_cache = c = (self._cache_key(), self._dequant_t())
+            wt = c[1]
+        else:
+            wt = self._dequant_t() if dy.is_cuda else None
+        if wt is not None:
             return F.linear(dy, wt)
         return dy @ self.dequantize()
 
+    def set_dequant_cache(self, on: bool):
+        self._cache_on = bool(on)
+        if not on:
+            self._w_cache = self._wt_cache = None
+
     @property
-    def weight(self):  # read-only dequantised view (merge_and_unload, inspection)
-        return self.dequantize()
+    def weight(self):  # dequantised copy (merge_and_unload, inspection): never the cached tensor
+        return self._dequant()
 
     def forward(self, x):
         if x.dtype != self.compute_dtype:
@@ -137,4 +168,33 @@ def quantize_model_(model: nn.Module, cfg: BitsAndBytesConfig, skip=("lm_head",)
         p.requires_grad_(False)
     if torch.cuda.is_available():
         torch.cuda.empty_cache()
+    set_dequant_cache(model)
     return model
+
+
+def set_dequant_cache(model: nn.Module, mode: Optional[str] = None, budget_fraction: float = 0.15) -> bool:
+    """Keep each NF4 layer's dequantised bf16 W and W^T resident instead of re-dequantising them in
+    every forward and backward.
+
+    The base weights are frozen, so the dequantised values never change: caching is bit-identical
+    to dequantising per use. It trades HBM for time — 4 bytes per base parameter on top of the
+    0.53 of the packed NF4 — which on a 288 GB MI355X is ~28 GB for Llama-3.1-8B (the SFT job's
+    dequant kernels were 13.8 % of its step, profiles/r1_sft_job_kernel_breakdown.md) but does not
+    fit for 70B. ``mode`` (default ``GRT_NF4_CACHE``, else "auto"): "1" on, "0" off, "auto" on
+    when the cache fits in ``budget_fraction`` of the device's memory. Returns whether it is on."""
+    layers = [m for m in model.modules() if isinstance(m, NF4Linear)]
+    mode = mode or os.environ.get("GRT_NF4_CACHE", "auto")
+    if not layers:
+        return False
+    dev = layers[0].qweight.device
+    if mode == "auto":
+        if dev.type != "cuda":
+            on = False
+        else:
+            need = sum(4 * m.in_features * m.out_features for m in layers)
+            on = need <= budget_fraction * torch.cuda.get_device_properties(dev).total_memory
+    else:
+        on = mode not in ("0", "off", "false")
+    for m in layers:
+        m.set_dequant_cache(on)
+    return on

@@ -80,6 +80,12 @@ class SFTConfig:
     max_length: Optional[int] = None
     master_weights: bool = False
     disable_tqdm: bool = True
+    # MI355X execution plan (not HF keys): run the gradient-accumulation micro-batches of one
+    # optimizer step as ONE padded batch (up to fuse_max_tokens tokens per forward) with each
+    # micro-batch's own loss mean kept through per-token loss weights — the same gradient, bigger
+    # GEMMs. None = on for GPU models whose forward takes ``loss_weights``.
+    fuse_accumulation: Optional[bool] = None
+    fuse_max_tokens: int = 16384
 
     def __post_init__(self):
         if self.evaluation_strategy is not None:  # deprecated alias used by the reference (:317)
@@ -202,6 +208,56 @@ class SFTTrainer:
             out.append(self.collator([seqs[j] for j in chunk]))
         return out
 
+    def _fuse_enabled(self) -> bool:
+        a = self.args
+        if a.gradient_accumulation_steps <= 1:
+            return False
+        if a.fuse_accumulation is not None:
+            return bool(a.fuse_accumulation)
+        if os.environ.get("GRT_SFT_FUSE_ACCUM", "1") == "0" or self.device.type != "cuda":
+            return False
+        import inspect
+        inner = getattr(self.model, "base_model", self.model)
+        try:
+            return "loss_weights" in inspect.signature(inner.forward).parameters
+        except (TypeError, ValueError):
+            return False
+
+    def _step_chunks(self, batches, mis, fuse):
+        """The micro-batches ``mis`` of one optimizer step -> [(batch, loss_weights | None)].
+        Unfused: one entry per micro-batch (loss = mean / accum). Fused: micro-batches are right-
+        padded to a common length and concatenated while the padded size stays within
+        ``fuse_max_tokens``; every position of micro-batch m carries weight 1 / (n_m * accum)
+        (n_m = its valid next-token labels), so the weighted-sum loss and its gradient equal the
+        sum of the unfused micro-batch losses."""
+        if not fuse:
+            return [(batches[mi], None) for mi in mis]
+        accum = self.args.gradient_accumulation_steps
+        groups, cur, cur_len, cur_rows = [], [], 0, 0
+        for mi in mis:
+            b = batches[mi]
+            L, R = b["input_ids"].shape[1], b["input_ids"].shape[0]
+            nl, nr = max(cur_len, L), cur_rows + R
+            if cur and nl * nr > self.args.fuse_max_tokens:
+                groups.append(cur)
+                cur, nl, nr = [], L, R
+            cur.append(b)
+            cur_len, cur_rows = nl, nr
+        if cur:
+            groups.append(cur)
+        out = []
+        for g in groups:
+            L = max(b["input_ids"].shape[1] for b in g)
+            pads = {"input_ids": self.pad_id, "labels": -100, "attention_mask": 0}
+            merged = {k: torch.cat([torch.nn.functional.pad(b[k], (0, L - b[k].shape[1]), value=v) for b in g])
+                      for k, v in pads.items()}
+            ws = []
+            for b in g:
+                n = int(((b["labels"][:, 1:] != -100) & (b["attention_mask"][:, 1:] != 0)).sum())
+                ws.append(torch.full((b["input_ids"].shape[0], L), 1.0 / (n * accum) if n else 0.0))
+            out.append((merged, torch.cat(ws)))
+        return out
+
     def _to_dev(self, b):
         return {k: v.pin_memory().to(self.device, non_blocking=True) if self.device.type == "cuda" else v.to(self.device)
                 for k, v in b.items()}
@@ -235,25 +291,33 @@ class SFTTrainer:
         step = start_step
         epochs = math.ceil(total / steps_per_epoch)
         done = False
+        fuse = self._fuse_enabled()
         for epoch in range(start_step // steps_per_epoch, epochs):
             batches = self._batches(self.train_seqs, bs, epoch)
-            skip = (start_step - epoch * steps_per_epoch) * accum if epoch == start_step // steps_per_epoch else 0
+            skip = (start_step - epoch * steps_per_epoch) if epoch == start_step // steps_per_epoch else 0
             nb = len(batches)
-            for mi in range(max(0, skip), nb):
-                boundary = ((mi + 1) % accum == 0) or (mi == nb - 1)
-                ntok += int(batches[mi]["attention_mask"].sum())  # CPU tensor: no device sync
-                b = self._to_dev(batches[mi])
-                with self.engine.no_sync(not boundary):
-                    with roctx.range("forward"):
-                        out = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])
-                        loss = out["loss"] / accum
-                    with roctx.range("backward"):
-                        loss.backward()
-                tr_loss_sum += loss.detach()
-                log_loss += loss.detach()
-                nsamples += b["input_ids"].shape[0]
-                if not boundary:
-                    continue
+            for gi in range(max(0, skip), steps_per_epoch):
+                mis = list(range(gi * accum, min(nb, (gi + 1) * accum)))
+                if not mis:
+                    break
+                mi = mis[-1]
+                chunks = self._step_chunks(batches, mis, fuse)
+                for ci, (cb, lw) in enumerate(chunks):
+                    ntok += int(cb["attention_mask"].sum())  # CPU tensor: no device sync
+                    b = self._to_dev(cb)
+                    with self.engine.no_sync(ci != len(chunks) - 1):
+                        with roctx.range("forward"):
+                            if lw is None:
+                                out = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])
+                                loss = out["loss"] / accum
+                            else:
+                                loss = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"],
+                                                  loss_weights=lw.to(self.device, non_blocking=True))["loss"]
+                        with roctx.range("backward"):
+                            loss.backward()
+                    tr_loss_sum += loss.detach()
+                    log_loss += loss.detach()
+                    nsamples += b["input_ids"].shape[0]
                 with roctx.range("grad_sync"):
                     self.engine.finish_gradient_sync()
                 with roctx.range("optimizer"):

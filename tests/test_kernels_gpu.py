@@ -168,6 +168,27 @@ def test_lm_head_ce():
     _close(W.grad, Wr.grad, 2e-3, 5e-2, "lmce dW")
 
 
+def test_lm_head_ce_row_weights():
+    """Weighted-sum loss (fused grad accumulation): per-row scale goes through the CE backward."""
+    from gke_ray_train_amd import ops
+    torch.manual_seed(15)
+    N, d, V = 96, 256, 1000
+    h = torch.randn(N, d, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    W = (0.05 * torch.randn(V, d, device=DEV, dtype=torch.bfloat16)).requires_grad_()
+    lab = torch.randint(0, V, (N,), device=DEV)
+    lab[::7] = -100
+    rw = torch.rand(N, device=DEV) / 8
+    loss = ops.lm_head_cross_entropy(h, W, lab, row_weights=rw)
+    loss.backward()
+    hr, Wr = h.detach().float().requires_grad_(), W.detach().float().requires_grad_()
+    rows = torch.nn.functional.cross_entropy(hr @ Wr.t(), lab, reduction="none")
+    ref = (rows * rw * (lab != -100)).sum()
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 2e-2 * max(1.0, abs(ref.item()))
+    _close(h.grad, hr.grad, 2e-3, 5e-2, "lmce-w dh")
+    _close(W.grad, Wr.grad, 2e-3, 5e-2, "lmce-w dW")
+
+
 @pytest.mark.parametrize("pdt", [torch.bfloat16, torch.float32])
 def test_adamw_and_clip(pdt):
     from gke_ray_train_amd.ops import FusedAdamW, clip_grad_norm_, _ref

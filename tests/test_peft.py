@@ -99,3 +99,27 @@ def test_attention_dropout_reference_mask_statistics():
     base = _ref.attention(q, k, v, causal=True)
     avg = torch.stack([_ref.attention(q, k, v, causal=True, dropout_p=0.2, seed=s) for s in range(400)]).mean(0)
     assert (avg - base).abs().max().item() < 0.15
+
+
+def test_nf4_dequant_cache_cpu():
+    import torch
+    import torch.nn as nn
+    from gke_ray_train_amd.peft import BitsAndBytesConfig
+    from gke_ray_train_amd.peft.quant import NF4Linear, set_dequant_cache
+    torch.manual_seed(0)
+    lin = nn.Linear(128, 64, bias=False)
+    q = NF4Linear.from_linear(lin, BitsAndBytesConfig(bnb_4bit_compute_dtype=torch.float32))
+    model = nn.Sequential(q)
+    assert set_dequant_cache(model, "auto") is False  # CPU: auto keeps the transient path
+    w0 = q.dequantize()
+    assert set_dequant_cache(model, "1") is True
+    w1 = q.dequantize()
+    assert q.dequantize() is w1  # resident
+    torch.testing.assert_close(w0, w1, rtol=0, atol=0)
+    dy = torch.randn(3, 64)
+    torch.testing.assert_close(q.input_grad(dy), dy @ w0)
+    q.qweight.add_(0)  # packed weights rewritten -> cache invalidated
+    assert q.dequantize() is not w1
+    assert q.weight is not q.dequantize()  # the public view is a copy
+    set_dequant_cache(model, "0")
+    assert q._w_cache is None

@@ -75,3 +75,71 @@ def test_full_ft_job_and_resume(tmp_path):
                     train_dataset=rows)
     out = tr.train(resume_from_checkpoint=str(sft / ck))
     assert out.global_step == 4
+
+
+def _fused_vs_unfused(tmp_path, fuse):
+    import torch
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    torch.manual_seed(0)
+    m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
+    # varied lengths so micro-batches pad differently and carry different valid-token counts
+    rows = [{"text": "select * from t where x = %d " % i * (1 + i % 4)} for i in range(16)]
+    tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path / str(fuse)), per_device_train_batch_size=2,
+                                 gradient_accumulation_steps=4, max_steps=2, logging_steps=1, save_strategy="no",
+                                 learning_rate=1e-3, max_grad_norm=1e9, fuse_accumulation=fuse, fuse_max_tokens=10 ** 6),
+                    train_dataset=rows)
+    out = tr.train()
+    return out, {k: v.detach().clone() for k, v in m.state_dict().items()}
+
+
+def test_fused_grad_accumulation_matches_unfused(tmp_path):
+    """One padded batch per optimizer step with per-micro-batch loss weights == HF-style
+    accumulation of per-micro-batch means (same loss, same updated parameters)."""
+    import torch
+    a, pa = _fused_vs_unfused(tmp_path, False)
+    b, pb = _fused_vs_unfused(tmp_path, True)
+    assert abs(a.training_loss - b.training_loss) < 1e-4 * max(1.0, abs(a.training_loss))
+    # AdamW's first steps are ~lr * sign(g): elements whose gradient is ~0 may flip under fp32
+    # summation-order changes, so allow a handful of such elements (bounded by 2 steps x lr)
+    for k in pa:
+        d = (pa[k] - pb[k]).abs()
+        assert float(d.max()) <= 2e-3, k
+        assert int((d > 1e-5).sum()) <= max(2, pa[k].numel() // 10000), k
+
+
+def test_step_chunks_respect_token_cap(tmp_path):
+    import torch
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
+    rows = [{"text": "abc " * (3 + i)} for i in range(8)]
+    tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path), per_device_train_batch_size=2, gradient_accumulation_steps=4,
+                                 fuse_accumulation=True, fuse_max_tokens=2 * 48), train_dataset=rows)
+    batches = tr._batches(tr.train_seqs, 2, 0, shuffle=False)
+    chunks = tr._step_chunks(batches, list(range(4)), True)
+    assert 1 < len(chunks) <= 4
+    tot_w = 0.0
+    for cb, w in chunks:
+        assert cb["input_ids"].numel() <= 2 * 48 or cb["input_ids"].shape[0] == 2
+        assert w.shape == cb["input_ids"].shape
+        valid = (cb["labels"][:, 1:] != -100) & (cb["attention_mask"][:, 1:] != 0)
+        tot_w += float((w[:, :-1] * valid).sum())
+    assert abs(tot_w - 1.0) < 1e-6  # 4 micro-batches x (n_m * 1 / (n_m * 4))
+
+
+def test_lm_head_row_weights_cpu():
+    import torch
+    import torch.nn.functional as F
+    from gke_ray_train_amd.ops.fused import lm_head_cross_entropy
+    torch.manual_seed(0)
+    h = torch.randn(10, 16, requires_grad=True)
+    w = torch.randn(32, 16, requires_grad=True)
+    lab = torch.randint(0, 32, (10,))
+    lab[3] = -100
+    rw = torch.rand(10)
+    loss = lm_head_cross_entropy(h, w, lab, row_weights=rw)
+    ref = (F.cross_entropy(h @ w.t(), lab, reduction="none") * rw * (lab != -100)).sum()
+    torch.testing.assert_close(loss, ref)
+    loss.backward()
+    assert h.grad is not None and torch.isfinite(h.grad).all()

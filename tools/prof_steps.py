@@ -20,6 +20,8 @@ FAMILIES = [
     ("grad norm", r"sumsq|clip"),
     ("embedding", r"embedding|compute_grad_weight|sum_and_scatter|gather"),
     ("lora", r"lora"),
+    ("nf4 dequant", r"nf4"),
+    ("transpose", r"transpose"),
     ("rccl", r"ncclDevKernel|rccl|nccl"),
     ("copies/fills", r"copyBuffer|fillBuffer|FillFunctor|copy_kernel"),
 ]
