@@ -303,7 +303,7 @@ void clip_finalize(const Tensor& ws, int64_t nparts, double max_norm, double pre
                           cur_stream(ws));
 }
 void adamw(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const optional<Tensor>& master, const Tensor& hyper,
-           const optional<Tensor>& gscale) {
+           const optional<Tensor>& gscale, int64_t max_blocks) {
   check_contig(p, "p");
   check_contig(gr, "g");
   check_contig(m, "m");
@@ -323,7 +323,7 @@ void adamw(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const optional<Ten
   c10::OptionalDeviceGuard g(p.device());
   grt::adamw_step(dtype_of(p), dtype_of(gr), p.data_ptr(), gr.data_ptr(), m.data_ptr<float>(), v.data_ptr<float>(),
                   master.has_value() ? master->data_ptr<float>() : nullptr, n, hyper.data_ptr<float>(),
-                  gscale.has_value() ? gscale->data_ptr<float>() : nullptr, cur_stream(p));
+                  gscale.has_value() ? gscale->data_ptr<float>() : nullptr, cur_stream(p), (int)max_blocks);
 }
 void scale_(Tensor& x, double a, const optional<Tensor>& a_ptr) {
   check_contig(x, "x");
@@ -706,7 +706,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq_blocks", &sumsq_blocks);
   m.def("sumsq", &sumsq);
   m.def("clip_finalize", &clip_finalize);
-  m.def("adamw", &adamw);
+  m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("master"),
+        py::arg("hyper"), py::arg("gscale"), py::arg("max_blocks") = 0);
   m.def("scale_", &scale_);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("scale"),
         py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);

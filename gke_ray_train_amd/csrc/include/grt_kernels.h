@@ -74,8 +74,10 @@ void clip_coef_finalize(const float* ws, int nparts, float max_norm, float presc
                         hipStream_t s);
 // Fused AdamW on a flat range. hyper (device): [lr, beta1, beta2, eps, weight_decay, bc1, bc2,
 // grad_scale]; grad_scale_ptr (device, may be null) multiplies grads (clip coefficient).
+// max_blocks > 0 caps the grid (grid-stride loop): a bandwidth-throttled update that can run
+// beside compute-bound kernels on another stream without starving them (parallel/overlap.py).
 void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
-                int64_t n, const float* hyper, const float* grad_scale_ptr, hipStream_t s);
+                int64_t n, const float* hyper, const float* grad_scale_ptr, hipStream_t s, int max_blocks = 0);
 // Scale in place: x *= a (device scalar pointer or host value when a_ptr == null).
 void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s);
 

@@ -171,8 +171,10 @@ void clip_coef_finalize(const float* ws, int nparts, float max_norm, float presc
 }
 
 void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
-                int64_t n, const float* hyper, const float* gsp, hipStream_t s) {
-  const dim3 grid(grid_for(n / 4 + 1));
+                int64_t n, const float* hyper, const float* gsp, hipStream_t s, int max_blocks) {
+  unsigned nb = grid_for(n / 4 + 1);
+  if (max_blocks > 0 && nb > (unsigned)max_blocks) nb = (unsigned)max_blocks;
+  const dim3 grid(nb);
   if (pdt == DType::BF16 && gdt == DType::BF16)
     hipLaunchKernelGGL((adamw_kernel<bf16, bf16>), grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, master, n, hyper, gsp);
   else if (pdt == DType::BF16)

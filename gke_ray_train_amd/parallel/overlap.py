@@ -25,6 +25,7 @@ Ordering hazards and why they are safe:
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -36,12 +37,15 @@ from .ddp import DistributedDataParallel, forward_wait_modules
 
 
 class OverlappedOptimizer:
-    def __init__(self, engine: DistributedDataParallel, optimizer: FusedAdamW):
+    def __init__(self, engine: DistributedDataParallel, optimizer: FusedAdamW, max_blocks: Optional[int] = None):
         if engine.zero:
             raise ValueError("ZeRO mode already overlaps its parameter all-gather with the forward; "
                              "the overlapped optimizer is for replicated parameters")
         self.engine = engine
         self.opt = optimizer
+        # grid cap of the update kernels (0 = full grid): a few workgroups pull a bounded share
+        # of HBM bandwidth beside the forward's GEMMs instead of flooding every CU
+        self.max_blocks = int(os.environ.get("GRT_OVERLAP_OPT_BLOCKS", "0")) if max_blocks is None else int(max_blocks)
         flat_ids = {}
         for gi, g in enumerate(engine.groups):
             for p, off in zip(g.params, g.offsets):
@@ -119,7 +123,7 @@ class OverlappedOptimizer:
                 for gi, lo, hi in rs:
                     p, g, ea, eas, master, hb = per_group[gi]
                     C.adamw(p.data[lo:hi], g[lo:hi], ea[lo:hi], eas[lo:hi],
-                            None if master is None else master[lo:hi], hb, gs)
+                            None if master is None else master[lo:hi], hb, gs, self.max_blocks)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
                 self._events[m] = ev
