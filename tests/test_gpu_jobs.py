@@ -48,6 +48,48 @@ def test_qlora_gpu_step():
     assert all(p.grad is not None for p in pm.parameters() if p.requires_grad)
 
 
+def test_fused_accumulation_loss_weights_match_micro_batches_on_gpu():
+    """The SFT trainer's fused step (one padded batch, per-micro-batch loss weights) on the HIP
+    path (row-weighted LM-head CE, NF4 dequant cache) gives the gradient of HF-style accumulation."""
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.peft import BitsAndBytesConfig, LoraConfig, get_peft_model, quantize_model_
+    from gke_ray_train_amd.peft.quant import set_dequant_cache
+    torch.manual_seed(0)
+    m = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=0)
+    quantize_model_(m, BitsAndBytesConfig())
+    assert set_dequant_cache(m, "1")
+    pm = get_peft_model(m, LoraConfig(r=8, lora_alpha=16, lora_dropout=0.0))
+    for n, p in pm.named_parameters():  # non-zero B so every adapter gradient is exercised
+        if "lora_B" in n:
+            p.data.normal_(0, 0.02)
+    lens = [(2, 100), (2, 64), (2, 128), (2, 40)]
+    micro = []
+    for B, L in lens:
+        ids = torch.randint(0, 512, (B, L), device="cuda")
+        mask = torch.ones_like(ids)
+        mask[0, L - 7:] = 0  # a padded row
+        lab = ids.masked_fill(mask == 0, -100)
+        micro.append((ids, mask, lab))
+    accum = len(micro)
+    params = [p for p in pm.parameters() if p.requires_grad]
+    for ids, mask, lab in micro:
+        (pm(ids, labels=lab, attention_mask=mask)["loss"] / accum).backward()
+    ref = [p.grad.float().clone() for p in params]
+    for p in params:
+        p.grad = None
+    Lm = 128
+    pad = lambda t, v: torch.nn.functional.pad(t, (0, Lm - t.shape[1]), value=v)
+    ids = torch.cat([pad(i, 0) for i, _, _ in micro])
+    mask = torch.cat([pad(k, 0) for _, k, _ in micro])
+    lab = torch.cat([pad(l, -100) for _, _, l in micro])
+    w = torch.cat([torch.full((i.shape[0], Lm), 1.0 / (int(((l[:, 1:] != -100) & (k[:, 1:] != 0)).sum()) * accum),
+                              device="cuda") for i, k, l in micro])
+    pm(ids, labels=lab, attention_mask=mask, loss_weights=w)["loss"].backward()
+    for p, r in zip(params, ref):
+        g = p.grad.float()
+        assert (g - r).norm() <= 2e-2 * r.norm() + 1e-6
+
+
 def test_sft_job_on_gpu(_rt, tmp_path):
     import fine_tune_llama_ray as job
     cfg = job.load_config(overrides={"MODEL_ID": "llama-tiny-gqa", "OUTPUT_DIR_BASE": str(tmp_path / "out"),
