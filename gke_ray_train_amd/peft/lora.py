@@ -269,6 +269,10 @@ class PeftModel(nn.Module):
         os.makedirs(path, exist_ok=True)
         save_file({k: v.cpu() for k, v in self.adapter_state_dict().items()},
                   os.path.join(path, "adapter_model.safetensors"))
+        self.save_adapter_config(path)
+
+    def save_adapter_config(self, path: str):
+        os.makedirs(path, exist_ok=True)
         cfg = self.peft_config["default"].to_dict()
         cfg["base_model_name_or_path"] = getattr(self.config, "name", "llama")
         with open(os.path.join(path, "adapter_config.json"), "w") as f:

@@ -121,6 +121,17 @@ def _world():
     return 0, 1
 
 
+def _to_host(obj):
+    """Deep copy with every tensor moved to host memory (checkpoint snapshot)."""
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().to("cpu", copy=True)
+    if isinstance(obj, dict):
+        return {k: _to_host(v) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_to_host(v) for v in obj)
+    return obj
+
+
 def _rows(ds) -> List[Dict[str, Any]]:
     if ds is None:
         return []
@@ -370,6 +381,7 @@ class SFTTrainer:
                 self._save_checkpoint(step)
             if done:
                 break
+        self._finish_save()  # the runtime includes the last checkpoint's write
         if self.device.type == "cuda":
             torch.cuda.synchronize()
         rt = time.time() - t0
@@ -456,18 +468,40 @@ class SFTTrainer:
                 self.tokenizer.save_pretrained(out)
 
     def _save_checkpoint(self, step: int):
+        """``checkpoint-<step>/`` (HF layout). For adapter models rank 0 snapshots the adapter and
+        optimizer tensors to host memory (~2 GB for Llama-3.1-8B r=64, tens of ms) and writes the
+        files on a background thread while training continues; full-model checkpoints are written
+        synchronously. The previous write is always finished before a new one starts, before
+        ``train`` returns and before a checkpoint is loaded."""
+        self._finish_save()
         a = self.args
         d = os.path.join(a.output_dir, f"checkpoint-{step}")
+        job = None
         if self.rank == 0:
             os.makedirs(d, exist_ok=True)
-            self.save_model(d)
-            torch.save(self.optimizer.state_dict(), os.path.join(d, "optimizer.pt"))
-            torch.save(self.scheduler.state_dict(), os.path.join(d, "scheduler.pt"))
-            torch.save(a.to_dict(), os.path.join(d, "training_args.bin"))
+            m = self._unwrapped()
+            files = {"optimizer.pt": _to_host(self.optimizer.state_dict()),
+                     "scheduler.pt": self.scheduler.state_dict(), "training_args.bin": a.to_dict()}
             st = dict(self.state, train_batch_size=a.per_device_train_batch_size, max_steps=a.max_steps,
                       logging_steps=a.logging_steps, save_steps=a.save_steps, eval_steps=a.eval_steps)
-            with open(os.path.join(d, "trainer_state.json"), "w") as f:
-                json.dump(st, f, indent=2)
+            st = json.loads(json.dumps(st))  # frozen copy: the live state keeps changing
+            adapter = None
+            if hasattr(m, "adapter_state_dict") and hasattr(m, "lora_modules"):
+                adapter = _to_host(m.adapter_state_dict())
+                m.save_adapter_config(d)
+                if hasattr(self.tokenizer, "save_pretrained"):
+                    self.tokenizer.save_pretrained(d)
+            else:
+                self.save_model(d)
+
+            def job():
+                if adapter is not None:
+                    from safetensors.torch import save_file
+                    save_file(adapter, os.path.join(d, "adapter_model.safetensors"))
+                for name, obj in files.items():
+                    torch.save(obj, os.path.join(d, name))
+                with open(os.path.join(d, "trainer_state.json"), "w") as f:
+                    json.dump(st, f, indent=2)
         if self.world > 1:
             dist.barrier()
         os.makedirs(d, exist_ok=True)
@@ -475,8 +509,43 @@ class SFTTrainer:
         if torch.cuda.is_available():
             rng["cuda"] = torch.cuda.get_rng_state_all()
         torch.save(rng, os.path.join(d, f"rng_state_{self.rank}.pth"))
+        # the async decision must be identical on every rank: _finish_save has a barrier
+        use_async = os.environ.get("GRT_ASYNC_CHECKPOINT", "1") != "0"
+        self._pending = (d, job)
+        self._save_thread = None
+        if job is not None:
+            if use_async:
+                import threading
+                def run(job=job):
+                    try:
+                        job()
+                    except BaseException as e:  # surfaced by _finish_save on the training thread
+                        self._save_error = e
+                self._save_error = None
+                self._save_thread = threading.Thread(target=run, name="grt-ckpt", daemon=False)
+                self._save_thread.start()
+            else:
+                job()
+        if not use_async:
+            self._finish_save()
+
+    def _finish_save(self):
+        """Complete the pending checkpoint: join the writer, rotate old checkpoints, run callbacks."""
+        pending = getattr(self, "_pending", None)
+        if pending is None:
+            return
+        d, _ = pending
+        t = getattr(self, "_save_thread", None)
+        if t is not None:
+            t.join()
+            self._save_thread = None
+        self._pending = None
+        err, self._save_error = getattr(self, "_save_error", None), None
+        if err is not None:
+            raise RuntimeError(f"writing checkpoint {d} failed") from err
         if self.world > 1:
             dist.barrier()
+        a = self.args
         if self.rank == 0 and a.save_total_limit:
             ck = sorted(glob.glob(os.path.join(a.output_dir, "checkpoint-*")), key=lambda p: int(p.rsplit("-", 1)[1]))
             for old in ck[:-a.save_total_limit]:
@@ -486,6 +555,7 @@ class SFTTrainer:
                 cb.on_save(self, d)
 
     def _load_checkpoint(self, d: str) -> int:
+        self._finish_save()
         m = self._unwrapped()
         if hasattr(m, "load_adapter") and os.path.exists(os.path.join(d, "adapter_model.safetensors")):
             m.load_adapter(d)
@@ -494,8 +564,8 @@ class SFTTrainer:
             loaded = from_pretrained(d, device=self.device, torch_dtype=next(m.parameters()).dtype)
             m.load_state_dict(loaded.state_dict())
         self.optimizer.load_state_dict(torch.load(os.path.join(d, "optimizer.pt"), map_location=self.device,
-                                                  weights_only=False))
-        self.scheduler.load_state_dict(torch.load(os.path.join(d, "scheduler.pt"), weights_only=False))
+                                                  weights_only=True))
+        self.scheduler.load_state_dict(torch.load(os.path.join(d, "scheduler.pt"), weights_only=True))
         with open(os.path.join(d, "trainer_state.json")) as f:
             st = json.load(f)
         self.state.update(st)

@@ -118,8 +118,8 @@ def train_loop_per_worker(config: dict):
     if ck is not None:
         with ck.as_directory() as d:
             model.module.load_state_dict(torch.load(os.path.join(d, "model.pth"), map_location=device, weights_only=True))
-            opt.load_state_dict(torch.load(os.path.join(d, "optimizer.pth"), map_location=device, weights_only=False))
-            sched.load_state_dict(torch.load(os.path.join(d, "scheduler.pth"), weights_only=False))
+            opt.load_state_dict(torch.load(os.path.join(d, "optimizer.pth"), map_location=device, weights_only=True))
+            sched.load_state_dict(torch.load(os.path.join(d, "scheduler.pth"), weights_only=True))
             start_epoch = sched.state_dict().get("last_epoch", 0) // max(1, len(loader))
             step = sched.last_epoch
     log_every = config.get("log_frequency_batches", 20)

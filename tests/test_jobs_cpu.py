@@ -43,6 +43,9 @@ def test_basic_llm_job_two_cpu_workers(tmp_path):
     sd = torch.load(os.path.join(latest, "model.pth"), weights_only=True)
     assert "token_embedding.weight" in sd and "transformer_decoder.layers.0.self_attn.in_proj_weight" in sd
     assert "positional_encoding.pe" in sd and "fc_out.bias" in sd
+    # the resume path loads optimizer / scheduler state with the no-code-execution loader
+    assert "state" in torch.load(os.path.join(latest, "optimizer.pth"), weights_only=True)
+    assert "last_epoch" in torch.load(os.path.join(latest, "scheduler.pth"), weights_only=True)
     rows = [json.loads(l) for l in open(os.path.join(trial, "result.json"))]
     assert [r["epoch"] for r in rows] == [1, 2]
     assert rows[1]["loss"] < rows[0]["loss"] + 1.0
