@@ -331,7 +331,7 @@ class SFTTrainer:
                 chunks = self._step_chunks(batches, mis, fuse)
                 for ci, (cb, lw) in enumerate(chunks):
                     ntok += int(cb["attention_mask"].sum())  # CPU tensor: no device sync
-                    b = self._to_dev(cb)
+                    b = self._to_dev(cb if lw is None else dict(cb, loss_weights=lw))
                     with self.engine.no_sync(ci != len(chunks) - 1):
                         with roctx.range("forward"):
                             if lw is None:
@@ -339,7 +339,7 @@ class SFTTrainer:
                                 loss = out["loss"] / accum
                             else:
                                 loss = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"],
-                                                  loss_weights=lw.to(self.device, non_blocking=True))["loss"]
+                                                  loss_weights=b["loss_weights"])["loss"]
                         with roctx.range("backward"):
                             loss.backward()
                     tr_loss_sum += loss.detach()
