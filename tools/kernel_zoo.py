@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Every hand-written gfx950 kernel of the hot paths at its production shape, a few launches each,
+for rocprofv3 PMC passes (tools/gpu_pmc_zoo.sh). Shapes: the Llama-2-7B training step (8 x 1024
+tokens) and the Llama-3.1-8B decode step."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gke_ray_train_amd import _native, ops  # noqa: E402
+from gke_ray_train_amd.ops.linear import wgrad  # noqa: E402
+
+REP = int(os.environ.get("ZOO_REP", "3"))
+dev = "cuda"
+bf = torch.bfloat16
+C = _native.kernels()
+T, d, f = 8192, 4096, 11008
+torch.manual_seed(0)
+
+
+def rep(fn):
+    for _ in range(REP):
+        fn()
+    torch.cuda.synchronize()
+
+
+# weight-gradient GEMM (qkv and down projections)
+dy = torch.randn(T, 3 * d, device=dev, dtype=bf)
+x = torch.randn(T, d, device=dev, dtype=bf)
+rep(lambda: wgrad(dy, x))
+dy2 = torch.randn(T, d, device=dev, dtype=bf)
+x2 = torch.randn(T, f, device=dev, dtype=bf)
+rep(lambda: wgrad(dy2, x2))
+del dy, x, dy2, x2
+
+# flash attention fwd + bwd (B 8, S 1024, 32 heads, D 128, causal)
+q, k, v = (torch.randn(8, 1024, 32, 128, device=dev, dtype=bf, requires_grad=True) for _ in range(3))
+do = torch.randn(8, 1024, 32, 128, device=dev, dtype=bf)
+
+
+def attn():
+    o = ops.flash_attention(q, k, v, causal=True)
+    torch.autograd.backward(o, do)
+
+
+rep(attn)
+del q, k, v, do
+
+# RMSNorm (+residual) fwd/bwd, SwiGLU fwd/bwd
+h = torch.randn(T, d, device=dev, dtype=bf, requires_grad=True)
+r = torch.randn(T, d, device=dev, dtype=bf, requires_grad=True)
+w = torch.ones(d, device=dev, dtype=bf, requires_grad=True)
+
+
+def norm():
+    y, res = ops.add_rms_norm(h, r, w)
+    torch.autograd.backward([y, res], [torch.ones_like(y), torch.ones_like(res)])
+
+
+rep(norm)
+gu = torch.randn(T, 2 * f, device=dev, dtype=bf, requires_grad=True)
+
+
+def sw():
+    y = ops.swiglu(gu)
+    y.backward(torch.ones_like(y))
+
+
+rep(sw)
+del h, r, gu
+
+# fused AdamW over 512 M parameters (bf16 params / grads, fp32 states)
+n = 512 * 1024 * 1024
+p = torch.randn(n, device=dev, dtype=bf)
+g = torch.randn(n, device=dev, dtype=bf)
+m = torch.zeros(n, device=dev)
+vv = torch.zeros(n, device=dev)
+hyper = torch.tensor([1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, 1.0], device=dev)
+rep(lambda: C.adamw(p, g, m, vv, None, hyper, None))
+del p, g, m, vv
+
+# decode: GEMV (gate_up of Llama-3.1-8B, 1 token) and split-K decode attention (4K context)
+xw = torch.randn(1, 4096, device=dev, dtype=bf)
+W = torch.randn(2 * 14336, 4096, device=dev, dtype=bf)
+rep(lambda: C.gemv(xw, W))
+del W
+qd = torch.randn(1, 1, 32, 128, device=dev, dtype=bf)
+kc = torch.randn(1, 4096, 8, 128, device=dev, dtype=bf)
+vc = torch.randn(1, 4096, 8, 128, device=dev, dtype=bf)
+sl = torch.full((1,), 4096, device=dev, dtype=torch.int32)
+rep(lambda: C.attn_decode(qd, kc, vc, sl, 128 ** -0.5))
+
+# NF4 dequant (Llama-3.1-8B gate_up weight) and its transposed variant
+wq = torch.randn(2 * 14336, 4096, device=dev, dtype=bf)
+qw, am = ops.nf4_quantize(wq.view(-1))
+rep(lambda: ops.nf4_dequantize(qw, am, wq.numel()))
+rep(lambda: C.nf4_dequantize_t(qw, am, 2 * 14336, 4096, 64))
+print("zoo done", flush=True)

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Summarise tools/gpu_pmc_zoo.sh output: per kernel, mean duration (kernel trace), MFMA busy share,
+wave-state split, LDS bank-conflict cycles, HBM-side bytes and bandwidth.
+
+Derived columns (MI355X: 256 CUs x 4 SIMDs):
+* GRBM_GUI_ACTIVE is summed over the 8 XCDs: cycles = GRBM_GUI_ACTIVE / 8;
+* mfma %  = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycles) — share of the time the matrix
+  cores are busy at the clock the kernel actually ran (calibrated on the wgrad GEMM: 824.6 GFLOP
+  in 847 us = 0.97 PF at a 1.69 GHz effective clock = 55 % of the 1.76 PF peak at that clock,
+  counter ratio 52 %);
+* clk GHz = cycles / duration (2.4 GHz nominal; MFMA-heavy kernels run power-limited below it);
+* wait / issue-stall / active = SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES;
+* read GB = 2 x FETCH_SIZE KiB (gfx950 FETCH_SIZE counts half of a wide coalesced read,
+  MI355X_MICROARCH.md §HBM), write GB = WRITE_SIZE KiB; GB/s over the trace duration.
+"""
+import csv
+import glob
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    n = name.replace("void ", "").replace("grt::(anonymous namespace)::", "")
+    m = re.match(r"_ZN3grt12_GLOBAL__N_1\d+(\w+?)I", n)
+    if m:
+        return m.group(1)
+    return re.sub(r"\(.*", "", n)[:60]
+
+
+def load_counters(path):
+    """-> {kernel: {counter: [per-dispatch values]}}"""
+    per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
+    names = {}
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"]
+        did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+        per[k][r["Counter_Name"]][did] += float(r["Counter_Value"])
+        names[k] = 1
+    out = {}
+    for k, cs in per.items():
+        out[k] = {c: sum(v.values()) / max(1, len(v)) for c, v in cs.items()}
+    return out
+
+
+def main(d):
+    tr = glob.glob(os.path.join(d, "**", "trace_kernel_trace.csv"), recursive=True)
+    dur = defaultdict(list)
+    for r in csv.DictReader(open(tr[0])):
+        dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e9)
+    ctr = {}
+    for tag in ("sq", "fetch", "write"):
+        f = glob.glob(os.path.join(d, "**", f"{tag}_counter_collection.csv"), recursive=True)
+        if f:
+            for k, cs in load_counters(f[0]).items():
+                ctr.setdefault(k, {}).update(cs)
+    rows = []
+    for k, ds in dur.items():
+        if "grt" not in k and "gemm_tt" not in k:
+            continue
+        c = ctr.get(k, {})
+        t = sorted(ds)[len(ds) // 2]
+        gui = c.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+        wc = c.get("SQ_WAVE_CYCLES", 0.0) or 1.0
+        mf = c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        rd = 2 * c.get("FETCH_SIZE", 0.0) * 1024 / 1e9
+        wr = c.get("WRITE_SIZE", 0.0) * 1024 / 1e9
+        hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
+        rows.append((short(k), len(ds), t * 1e6, 100 * mf / (1024 * gui) if gui else 0.0, gui / t / 1e9 if gui else 0.0,
+                     100 * c.get("SQ_WAIT_ANY", 0) / wc, 100 * c.get("SQ_WAIT_INST_ANY", 0) / wc,
+                     100 * c.get("SQ_ACTIVE_INST_ANY", 0) / wc, c.get("SQ_LDS_BANK_CONFLICT", 0.0),
+                     rd, wr, (rd + wr) / t if t else 0.0, 100 * hit / (hit + miss) if hit + miss else 0.0))
+    rows.sort(key=lambda r: -r[2])
+    print("| kernel | calls | median us | mfma % | clk GHz | wait % | issue-stall % | active % | LDS bank-conflict cycles | read GB | write GB | HBM GB/s | L2 hit % |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for r in rows:
+        print(f"| `{r[0]}` | {r[1]} | {r[2]:.1f} | {r[3]:.1f} | {r[4]:.2f} | {r[5]:.0f} | {r[6]:.0f} | {r[7]:.0f} | "
+              f"{r[8]:.3g} | {r[9]:.3f} | {r[10]:.3f} | {r[11]:.0f} | {r[12]:.0f} |")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
