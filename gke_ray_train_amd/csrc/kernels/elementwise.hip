@@ -184,19 +184,39 @@ __global__ __launch_bounds__(kNT) void scale_add_pe_kernel(const T* __restrict__
 }
 
 // ------------------------------- dropout -------------------------------------
-__device__ __forceinline__ uint32_t hash_u32(uint64_t x) {
+__device__ __forceinline__ uint64_t hash_u64(uint64_t x) {
   // splitmix64 finaliser: counter-based, stateless, graph-replay safe (seed/offset are args)
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  return (uint32_t)x;
+  return x ^ (x >> 31);
 }
 
-// 16-byte vectors per thread (8 bf16 / 4 fp32); the keep decision of element i is a pure function
-// of (seed, offset + i), so a backward can regenerate it instead of reading a stored mask.
+// The keep decision of element idx is a pure function of (seed, idx), so a backward regenerates
+// it instead of reading a stored mask: 16 bits of the 64-bit hash of its 4-element group
+// (idx / 4) against p in 1/65536 units. One hash per 4 elements: the 64-bit multiplies of the
+// hash are emulated with 32-bit ones on CDNA, and one hash per element made the kernel VALU-bound
+// (~2.9 TB/s); per group it streams at HBM speed. Keep probability 1 - round(p * 65536) / 65536.
+__device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
 __device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
-  return hash_u32((seed << 40) ^ idx) >= thr;
+  const uint64_t h = hash_u64((seed << 40) ^ (idx >> 2));
+  return ((uint32_t)(h >> (16 * (idx & 3))) & 0xffffu) >= thr;
+}
+// V consecutive decisions from idx0; one hash per 4 elements when idx0 is 4-aligned
+template <int V>
+__device__ __forceinline__ void drop_keep_vec(uint64_t seed, uint64_t idx0, uint32_t thr, bool (&keep)[V]) {
+  static_assert(V % 4 == 0, "vector of whole 4-element groups");
+  if ((idx0 & 3) == 0) {
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q) {
+      const uint64_t h = hash_u64((seed << 40) ^ ((idx0 >> 2) + q));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) keep[4 * q + j] = ((uint32_t)(h >> (16 * j)) & 0xffffu) >= thr;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < V; ++k) keep[k] = drop_keep(seed, idx0 + k, thr);
+  }
 }
 
 template <typename T>
@@ -204,7 +224,7 @@ __global__ __launch_bounds__(kNT) void dropout_fwd_kernel(const T* __restrict__ 
                                                           uint8_t* __restrict__ mask, int64_t n, float p,
                                                           uint64_t seed, uint64_t offset) {
   constexpr int V = Vec16<T>::N;
-  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  const uint32_t thr = drop_thr(p);
   const float sc = 1.f / (1.f - p);
   const int64_t nv = n / V;
   for (int64_t v = (int64_t)blockIdx.x * kNT + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kNT) {
@@ -212,11 +232,12 @@ __global__ __launch_bounds__(kNT) void dropout_fwd_kernel(const T* __restrict__ 
     float a[V];
     load16(x + i0, a);
     uint8_t mk[V];
+    bool kp[V];
+    drop_keep_vec<V>(seed, offset + (uint64_t)i0, thr, kp);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const bool keep = drop_keep(seed, offset + (uint64_t)(i0 + k), thr);
-      mk[k] = keep;
-      a[k] = keep ? a[k] * sc : 0.f;
+      mk[k] = kp[k];
+      a[k] = kp[k] ? a[k] * sc : 0.f;
     }
     store16(y + i0, a);
     if (mask) {
@@ -238,7 +259,7 @@ __global__ __launch_bounds__(kNT) void dropout_bwd_kernel(const T* __restrict__ 
                                                           T* __restrict__ dx, int64_t n, float p, uint64_t seed,
                                                           uint64_t offset, int accumulate) {
   constexpr int V = Vec16<T>::N;
-  const uint32_t thr = (uint32_t)(p * 4294967296.0);
+  const uint32_t thr = drop_thr(p);
   const float sc = 1.f / (1.f - p);
   const int64_t nv = n / V;
   for (int64_t v = (int64_t)blockIdx.x * kNT + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kNT) {
@@ -246,9 +267,16 @@ __global__ __launch_bounds__(kNT) void dropout_bwd_kernel(const T* __restrict__ 
     float g[V], o[V];
     load16(dy + i0, g);
     if (accumulate) load16(dx + i0, o);
+    bool kp[V];
+    if (mask) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) kp[k] = mask[i0 + k] != 0;
+    } else {
+      drop_keep_vec<V>(seed, offset + (uint64_t)i0, thr, kp);
+    }
 #pragma unroll
     for (int k = 0; k < V; ++k) {
-      const bool keep = mask ? mask[i0 + k] != 0 : drop_keep(seed, offset + (uint64_t)(i0 + k), thr);
+      const bool keep = kp[k];
       const float d = keep ? g[k] * sc : 0.f;
       o[k] = accumulate ? o[k] + d : d;
     }
