@@ -221,8 +221,11 @@ Tensor scale_add_pe(const Tensor& emb, const optional<Tensor>& pe, int64_t S, do
   return out;
 }
 
+void check_drop_p(double p) { TORCH_CHECK(p >= 0.0 && p < 1.0, "dropout p must be in [0, 1), got ", p); }
+
 std::vector<Tensor> dropout_fwd(const Tensor& x, double p, int64_t seed, int64_t offset) {
   check_contig(x, "x");
+  check_drop_p(p);
   c10::OptionalDeviceGuard g(x.device());
   auto y = at::empty_like(x);
   auto mask = at::empty(x.sizes(), x.options().dtype(at::kByte));
@@ -232,6 +235,8 @@ std::vector<Tensor> dropout_fwd(const Tensor& x, double p, int64_t seed, int64_t
 }
 Tensor dropout_bwd(const Tensor& dy, const Tensor& mask, double p) {
   check_contig(dy, "dy");
+  check_drop_p(p);
+  TORCH_CHECK(mask.numel() == dy.numel(), "dropout_bwd: mask / dy sizes differ");
   check_contig(mask, "mask");
   c10::OptionalDeviceGuard g(dy.device());
   auto dx = at::empty_like(dy);
@@ -242,6 +247,7 @@ Tensor dropout_bwd(const Tensor& dy, const Tensor& mask, double p) {
 // mask-free variants: forward stores no mask; backward regenerates it and can accumulate into dx
 Tensor dropout_fwd_seeded(const Tensor& x, double p, int64_t seed, int64_t offset) {
   check_contig(x, "x");
+  check_drop_p(p);
   c10::OptionalDeviceGuard g(x.device());
   auto y = at::empty_like(x);
   grt::dropout_fwd(dtype_of(x), x.data_ptr(), y.data_ptr(), nullptr, x.numel(), (float)p, (uint64_t)seed,
@@ -251,6 +257,7 @@ Tensor dropout_fwd_seeded(const Tensor& x, double p, int64_t seed, int64_t offse
 void dropout_bwd_seeded(const Tensor& dy, const Tensor& dx, double p, int64_t seed, int64_t offset, bool accumulate) {
   check_contig(dy, "dy");
   check_contig(dx, "dx");
+  check_drop_p(p);
   TORCH_CHECK(dy.numel() == dx.numel() && dy.scalar_type() == dx.scalar_type(), "dropout_bwd_seeded: shapes");
   c10::OptionalDeviceGuard g(dy.device());
   grt::dropout_bwd(dtype_of(dy), dy.data_ptr(), nullptr, dx.data_ptr(), dy.numel(), (float)p, cur_stream(dy),

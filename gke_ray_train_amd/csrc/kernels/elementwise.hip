@@ -193,29 +193,30 @@ __device__ __forceinline__ uint64_t hash_u64(uint64_t x) {
 }
 
 // The keep decision of element idx is a pure function of (seed, idx), so a backward regenerates
-// it instead of reading a stored mask: 16 bits of the 64-bit hash of its 4-element group
-// (idx / 4) against p in 1/65536 units. One hash per 4 elements: the 64-bit multiplies of the
-// hash are emulated with 32-bit ones on CDNA, and one hash per element made the kernel VALU-bound
-// (~2.9 TB/s); per group it streams at HBM speed. Keep probability 1 - round(p * 65536) / 65536.
+// it instead of reading a stored mask: 16 bits of hash(key ^ (idx / 4)) against p in 1/65536
+// units, key = hash(seed) (all 64 seed bits matter; computed once per thread). One hash per 4
+// elements: the 64-bit multiplies of the hash are emulated with 32-bit ones on CDNA, and one hash
+// per element made the kernel VALU-bound; per group it streams at memory speed. Keep probability
+// 1 - round(p * 65536) / 65536. ops/_ref.py::dropout_keep_mask is the host reimplementation.
 __device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
-__device__ __forceinline__ bool drop_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
-  const uint64_t h = hash_u64((seed << 40) ^ (idx >> 2));
+__device__ __forceinline__ bool drop_keep(uint64_t key, uint64_t idx, uint32_t thr) {
+  const uint64_t h = hash_u64(key ^ (idx >> 2));
   return ((uint32_t)(h >> (16 * (idx & 3))) & 0xffffu) >= thr;
 }
 // V consecutive decisions from idx0; one hash per 4 elements when idx0 is 4-aligned
 template <int V>
-__device__ __forceinline__ void drop_keep_vec(uint64_t seed, uint64_t idx0, uint32_t thr, bool (&keep)[V]) {
+__device__ __forceinline__ void drop_keep_vec(uint64_t key, uint64_t idx0, uint32_t thr, bool (&keep)[V]) {
   static_assert(V % 4 == 0, "vector of whole 4-element groups");
   if ((idx0 & 3) == 0) {
 #pragma unroll
     for (int q = 0; q < V / 4; ++q) {
-      const uint64_t h = hash_u64((seed << 40) ^ ((idx0 >> 2) + q));
+      const uint64_t h = hash_u64(key ^ ((idx0 >> 2) + q));
 #pragma unroll
       for (int j = 0; j < 4; ++j) keep[4 * q + j] = ((uint32_t)(h >> (16 * j)) & 0xffffu) >= thr;
     }
   } else {
 #pragma unroll
-    for (int k = 0; k < V; ++k) keep[k] = drop_keep(seed, idx0 + k, thr);
+    for (int k = 0; k < V; ++k) keep[k] = drop_keep(key, idx0 + k, thr);
   }
 }
 
@@ -226,6 +227,7 @@ __global__ __launch_bounds__(kNT) void dropout_fwd_kernel(const T* __restrict__ 
   constexpr int V = Vec16<T>::N;
   const uint32_t thr = drop_thr(p);
   const float sc = 1.f / (1.f - p);
+  const uint64_t key = hash_u64(seed);
   const int64_t nv = n / V;
   for (int64_t v = (int64_t)blockIdx.x * kNT + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kNT) {
     const int64_t i0 = v * V;
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(kNT) void dropout_fwd_kernel(const T* __restrict__ 
     load16(x + i0, a);
     uint8_t mk[V];
     bool kp[V];
-    drop_keep_vec<V>(seed, offset + (uint64_t)i0, thr, kp);
+    drop_keep_vec<V>(key, offset + (uint64_t)i0, thr, kp);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       mk[k] = kp[k];
@@ -246,7 +248,7 @@ __global__ __launch_bounds__(kNT) void dropout_fwd_kernel(const T* __restrict__ 
     }
   }
   for (int64_t i = nv * V + (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
-    const bool keep = drop_keep(seed, offset + (uint64_t)i, thr);
+    const bool keep = drop_keep(key, offset + (uint64_t)i, thr);
     if (mask) mask[i] = keep;
     y[i] = from_f<T>(keep ? to_f(x[i]) * sc : 0.f);
   }
@@ -261,6 +263,7 @@ __global__ __launch_bounds__(kNT) void dropout_bwd_kernel(const T* __restrict__ 
   constexpr int V = Vec16<T>::N;
   const uint32_t thr = drop_thr(p);
   const float sc = 1.f / (1.f - p);
+  const uint64_t key = hash_u64(seed);
   const int64_t nv = n / V;
   for (int64_t v = (int64_t)blockIdx.x * kNT + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kNT) {
     const int64_t i0 = v * V;
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(kNT) void dropout_bwd_kernel(const T* __restrict__ 
 #pragma unroll
       for (int k = 0; k < V; ++k) kp[k] = mask[i0 + k] != 0;
     } else {
-      drop_keep_vec<V>(seed, offset + (uint64_t)i0, thr, kp);
+      drop_keep_vec<V>(key, offset + (uint64_t)i0, thr, kp);
     }
 #pragma unroll
     for (int k = 0; k < V; ++k) {
@@ -283,7 +286,7 @@ __global__ __launch_bounds__(kNT) void dropout_bwd_kernel(const T* __restrict__ 
     store16(dx + i0, o);
   }
   for (int64_t i = nv * V + (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
-    const bool keep = mask ? mask[i] != 0 : drop_keep(seed, offset + (uint64_t)i, thr);
+    const bool keep = mask ? mask[i] != 0 : drop_keep(key, offset + (uint64_t)i, thr);
     const float d = keep ? to_f(dy[i]) * sc : 0.f;
     dx[i] = from_f<T>(accumulate ? to_f(dx[i]) + d : d);
   }

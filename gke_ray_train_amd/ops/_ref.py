@@ -94,6 +94,30 @@ def attn_dropout_keep(seed: int, B: int, H: int, Sq: int, Sk: int, p: float, dev
     return h >= thresh
 
 
+def _splitmix64(x):
+    """numpy uint64 splitmix64 finaliser (wrapping arithmetic), as hash_u64 in elementwise.hip."""
+    import numpy as np
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def dropout_keep_mask(seed: int, offset: int, n: int, p: float) -> torch.Tensor:
+    """[n] bool keep-mask of the element dropout kernels (elementwise.hip ``drop_keep``),
+    recomputed independently on the host: element i keeps iff 16 bits of
+    splitmix64(splitmix64(seed) ^ ((offset + i) / 4)), selected by (offset + i) % 4, are
+    >= round(p * 65536)."""
+    import numpy as np
+    key = _splitmix64(np.array([seed & 0xFFFFFFFFFFFFFFFF], dtype=np.uint64))[0]
+    idx = np.arange(offset, offset + n, dtype=np.uint64)
+    h = _splitmix64(key ^ (idx >> np.uint64(2)))
+    bits = (h >> (np.uint64(16) * (idx & np.uint64(3)))) & np.uint64(0xFFFF)
+    thr = int(np.float32(p) * np.float32(65536.0) + np.float32(0.5))
+    return torch.from_numpy(bits >= np.uint64(thr))
+
+
 def attention(q, k, v, causal=True, scale=None, seqlens_k=None, dropout_p=0.0, seed=0):
     """q [B,Sq,Hq,D], k/v [B,Sk,Hkv,D] -> o [B,Sq,Hq,D]; math in fp32 (explicit matmul/softmax —
     no SDPA backend dispatch). ``dropout_p`` drops attention probabilities with the kernel's mask."""

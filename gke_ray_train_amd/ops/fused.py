@@ -148,16 +148,15 @@ class _Dropout(torch.autograd.Function):
         return _native.kernels().dropout_bwd(dy.contiguous(), mask, ctx.p), None, None, None
 
 
-_dropout_counter = [0]
-
-
 def dropout_seed_offset(x):
-    """(seed, offset) for a counter-based dropout over ``x``: seed from the device generator, a
-    running element offset so successive calls draw disjoint counter ranges."""
-    seed = int(torch.cuda.default_generators[x.device.index or 0].initial_seed()) & 0xFFFFFF
-    off = _dropout_counter[0]
-    _dropout_counter[0] += x.numel()
-    return seed, off
+    """(seed, offset) for a counter-based dropout over ``x``: a fresh 62-bit seed drawn from
+    torch's CPU generator, offset 0. Drawing from the CPU generator (no device sync) makes the
+    mask a function of the RNG state that ``torch.utils.checkpoint`` saves and restores — the
+    recompute of a checkpointed segment draws the same seed, so the mask the backward
+    regenerates is the forward's — and that trainers save in ``rng_state_<rank>.pth``, so a
+    resumed run continues the mask sequence instead of replaying it from step 0."""
+    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    return seed, 0
 
 
 def dropout(x, p, training=True, seed=None):

@@ -132,6 +132,44 @@ def _to_host(obj):
     return obj
 
 
+def _rng_snapshot() -> Dict[str, Any]:
+    """Every RNG a training step draws from, in a form ``torch.load(weights_only=True)`` reads
+    back (numpy's key array as a tensor). The CPU generator also seeds the dropout kernels
+    (``ops.fused.dropout_seed_offset``), so restoring it resumes the dropout-mask sequence."""
+    name, keys, pos, has_gauss, cached = np.random.get_state()
+    rng = {"python": random.getstate(), "cpu": torch.get_rng_state(),
+           "numpy": {"name": name, "keys": torch.from_numpy(keys.astype(np.int64)), "pos": int(pos),
+                     "has_gauss": int(has_gauss), "cached": float(cached)}}
+    if torch.cuda.is_available():
+        rng["cuda"] = torch.cuda.get_rng_state_all()
+    return rng
+
+
+def _rng_restore(rng: Dict[str, Any]):
+    random.setstate(rng["python"])
+    torch.set_rng_state(rng["cpu"])
+    n = rng.get("numpy")
+    if isinstance(n, dict):
+        np.random.set_state((n["name"], n["keys"].numpy().astype(np.uint32), n["pos"], n["has_gauss"], n["cached"]))
+    if "cuda" in rng and torch.cuda.is_available() and len(rng["cuda"]) == torch.cuda.device_count():
+        torch.cuda.set_rng_state_all(rng["cuda"])
+
+
+def _rank_uniform_error(err: Optional[BaseException], world: int, what: str):
+    """Raise on EVERY rank if any rank failed ``what``: the ranks exchange a failure flag first,
+    so a failure on one rank cannot leave the others blocked in the next collective."""
+    failed = err is not None
+    if world > 1:
+        flag = torch.tensor([1 if failed else 0], dtype=torch.int32,
+                            device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(flag)
+        failed = bool(flag.item())
+    if err is not None:
+        raise RuntimeError(f"{what} failed") from err
+    if failed:
+        raise RuntimeError(f"{what} failed on another rank")
+
+
 def _rows(ds) -> List[Dict[str, Any]]:
     if ds is None:
         return []
@@ -477,42 +515,47 @@ class SFTTrainer:
         a = self.args
         d = os.path.join(a.output_dir, f"checkpoint-{step}")
         job = None
+        err = None
         if self.rank == 0:
-            os.makedirs(d, exist_ok=True)
-            m = self._unwrapped()
-            files = {"optimizer.pt": _to_host(self.optimizer.state_dict()),
-                     "scheduler.pt": self.scheduler.state_dict(), "training_args.bin": a.to_dict()}
-            st = dict(self.state, train_batch_size=a.per_device_train_batch_size, max_steps=a.max_steps,
-                      logging_steps=a.logging_steps, save_steps=a.save_steps, eval_steps=a.eval_steps)
-            st = json.loads(json.dumps(st))  # frozen copy: the live state keeps changing
-            adapter = None
-            if hasattr(m, "adapter_state_dict") and hasattr(m, "lora_modules"):
-                adapter = _to_host(m.adapter_state_dict())
-                m.save_adapter_config(d)
-                if hasattr(self.tokenizer, "save_pretrained"):
-                    self.tokenizer.save_pretrained(d)
-            else:
-                self.save_model(d)
+            try:
+                os.makedirs(d, exist_ok=True)
+                m = self._unwrapped()
+                files = {"optimizer.pt": _to_host(self.optimizer.state_dict()),
+                         "scheduler.pt": self.scheduler.state_dict(), "training_args.bin": a.to_dict()}
+                st = dict(self.state, train_batch_size=a.per_device_train_batch_size, max_steps=a.max_steps,
+                          logging_steps=a.logging_steps, save_steps=a.save_steps, eval_steps=a.eval_steps)
+                st = json.loads(json.dumps(st))  # frozen copy: the live state keeps changing
+                adapter = None
+                if hasattr(m, "adapter_state_dict") and hasattr(m, "lora_modules"):
+                    adapter = _to_host(m.adapter_state_dict())
+                    m.save_adapter_config(d)
+                    if hasattr(self.tokenizer, "save_pretrained"):
+                        self.tokenizer.save_pretrained(d)
+                else:
+                    self.save_model(d)
 
-            def job():
-                if adapter is not None:
-                    from safetensors.torch import save_file
-                    save_file(adapter, os.path.join(d, "adapter_model.safetensors"))
-                for name, obj in files.items():
-                    torch.save(obj, os.path.join(d, name))
-                with open(os.path.join(d, "trainer_state.json"), "w") as f:
-                    json.dump(st, f, indent=2)
-        if self.world > 1:
-            dist.barrier()
-        os.makedirs(d, exist_ok=True)
-        rng = {"python": random.getstate(), "numpy": np.random.get_state(), "cpu": torch.get_rng_state()}
-        if torch.cuda.is_available():
-            rng["cuda"] = torch.cuda.get_rng_state_all()
-        torch.save(rng, os.path.join(d, f"rng_state_{self.rank}.pth"))
-        # the async decision must be identical on every rank: _finish_save has a barrier
+                def job():
+                    if adapter is not None:
+                        from safetensors.torch import save_file
+                        save_file(adapter, os.path.join(d, "adapter_model.safetensors"))
+                    for name, obj in files.items():
+                        torch.save(obj, os.path.join(d, name))
+                    with open(os.path.join(d, "trainer_state.json"), "w") as f:
+                        json.dump(st, f, indent=2)
+            except Exception as e:  # reported on every rank below, not raised ahead of the others
+                err, job = e, None
+        try:
+            os.makedirs(d, exist_ok=True)
+            torch.save(_rng_snapshot(), os.path.join(d, f"rng_state_{self.rank}.pth"))
+        except Exception as e:
+            err = err or e
+        # every rank reaches this exchange, so a failed snapshot raises everywhere (no hang)
+        _rank_uniform_error(err, self.world, f"checkpoint {d}")
+        # the async decision must be identical on every rank: _finish_save exchanges the outcome
         use_async = os.environ.get("GRT_ASYNC_CHECKPOINT", "1") != "0"
         self._pending = (d, job)
         self._save_thread = None
+        self._save_error = None
         if job is not None:
             if use_async:
                 import threading
@@ -521,16 +564,19 @@ class SFTTrainer:
                         job()
                     except BaseException as e:  # surfaced by _finish_save on the training thread
                         self._save_error = e
-                self._save_error = None
                 self._save_thread = threading.Thread(target=run, name="grt-ckpt", daemon=False)
                 self._save_thread.start()
             else:
-                job()
+                try:
+                    job()
+                except Exception as e:
+                    self._save_error = e
         if not use_async:
             self._finish_save()
 
     def _finish_save(self):
-        """Complete the pending checkpoint: join the writer, rotate old checkpoints, run callbacks."""
+        """Complete the pending checkpoint: join the writer, rotate old checkpoints, run callbacks.
+        A failed write on rank 0 raises on every rank (flag exchanged before anyone raises)."""
         pending = getattr(self, "_pending", None)
         if pending is None:
             return
@@ -541,10 +587,7 @@ class SFTTrainer:
             self._save_thread = None
         self._pending = None
         err, self._save_error = getattr(self, "_save_error", None), None
-        if err is not None:
-            raise RuntimeError(f"writing checkpoint {d} failed") from err
-        if self.world > 1:
-            dist.barrier()
+        _rank_uniform_error(err, self.world, f"writing checkpoint {d}")
         a = self.args
         if self.rank == 0 and a.save_total_limit:
             ck = sorted(glob.glob(os.path.join(a.output_dir, "checkpoint-*")), key=lambda p: int(p.rsplit("-", 1)[1]))
@@ -569,4 +612,7 @@ class SFTTrainer:
         with open(os.path.join(d, "trainer_state.json")) as f:
             st = json.load(f)
         self.state.update(st)
+        rp = os.path.join(d, f"rng_state_{self.rank}.pth")
+        if os.path.exists(rp):  # continue the RNG streams (dropout masks, sampler) where they stopped
+            _rng_restore(torch.load(rp, weights_only=True))
         return int(st["global_step"])

@@ -110,6 +110,78 @@ def test_dropout():
     assert torch.equal((x.grad != 0), (y != 0))
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("offset", [0, 1, 3, 6, (1 << 40) + 5])
+@pytest.mark.parametrize("n", [12345, 4096, 7])
+def test_dropout_masks_match_host_hash(dtype, offset, n):
+    """Every dropout entry point (mask-storing fwd, mask-free fwd, seeded bwd with and without
+    accumulation) produces the keep pattern of the independent host reimplementation of the hash
+    (ops/_ref.py::dropout_keep_mask) — including unaligned offsets (offset % 4 != 0, the per-element
+    path of drop_keep_vec), the scalar tail (n % vector width != 0) and seeds above bit 40."""
+    from gke_ray_train_amd.ops import _ref
+    C = _C()
+    p, seed = 0.3, (0x5DEECE66D << 20) | 0xABC
+    ref = _ref.dropout_keep_mask(seed, offset, n, p).to(DEV)
+    ones = torch.ones(n, device=DEV, dtype=dtype)
+    y, mask = C.dropout_fwd(ones, p, seed, offset)
+    assert torch.equal(mask.bool(), ref), "stored mask"
+    assert torch.equal(y != 0, ref)
+    assert torch.allclose(y[ref].float(), torch.full_like(y[ref].float(), 1 / (1 - p)), rtol=1e-2)
+    assert torch.equal(C.dropout_fwd_seeded(ones, p, seed, offset) != 0, ref), "mask-free fwd"
+    dx = torch.empty_like(ones)
+    C.dropout_bwd_seeded(ones, dx, p, seed, offset, False)
+    assert torch.equal(dx != 0, ref), "seeded bwd"
+    acc = torch.full_like(ones, 2.0)
+    C.dropout_bwd_seeded(ones, acc, p, seed, offset, True)
+    expect = 2.0 + ref.to(dtype) / (1 - p)
+    assert torch.allclose(acc.float(), expect.float(), rtol=1e-2), "seeded bwd accumulate"
+    assert torch.equal(C.dropout_bwd(ones, mask, p) != 0, ref), "mask bwd"
+    if n >= 4096:
+        assert abs(ref.float().mean().item() - (1 - p)) < 0.03
+    # a different seed gives a different mask; seeds differing only above bit 40 too
+    assert not torch.equal(_ref.dropout_keep_mask(seed ^ (1 << 50), offset, n, p), ref.cpu()) or n < 64
+
+
+def test_dropout_rejects_bad_p():
+    C = _C()
+    x = torch.ones(64, device=DEV, dtype=torch.bfloat16)
+    for bad in (-0.1, 1.0, 1.5):
+        with pytest.raises(RuntimeError):
+            C.dropout_fwd(x, bad, 1, 0)
+        with pytest.raises(RuntimeError):
+            C.dropout_fwd_seeded(x, bad, 1, 0)
+        with pytest.raises(RuntimeError):
+            C.dropout_bwd_seeded(x, torch.empty_like(x), bad, 1, 0, False)
+
+
+def test_lora_dropout_under_gradient_checkpointing():
+    """LoRA input dropout inside a non-reentrant checkpoint: the recompute draws the same
+    (seed, offset) (torch's CPU RNG state is restored by checkpoint), so the gradients equal
+    those of the same step without checkpointing."""
+    import torch.utils.checkpoint as ckpt
+    from gke_ray_train_amd.ops.linear import Linear
+    from gke_ray_train_amd.peft.lora import LoraConfig, LoraLinear
+    torch.manual_seed(0)
+    lin = Linear(256, 512, bias=False, device=DEV, dtype=torch.bfloat16)
+    lin.weight.requires_grad_(False)
+    mod = LoraLinear(lin, [("q_proj", 0, 512)], LoraConfig(r=16, lora_alpha=32, lora_dropout=0.3)).train()
+    with torch.no_grad():
+        mod.lora_B["q_proj"].normal_(0, 0.05)
+    x0 = torch.randn(4, 64, 256, device=DEV, dtype=torch.bfloat16)
+    dy = torch.randn(4, 64, 512, device=DEV, dtype=torch.bfloat16)
+    grads = []
+    for use_ckpt in (False, True):
+        mod.zero_grad(set_to_none=True)
+        x = x0.clone().requires_grad_()
+        torch.manual_seed(123)
+        y = ckpt.checkpoint(mod, x, use_reentrant=False) if use_ckpt else mod(x)
+        torch.manual_seed(999)  # the RNG moves on between forward and backward
+        (y.float() * dy.float()).sum().backward()
+        grads.append((x.grad.clone(), mod.lora_A["q_proj"].grad.clone(), mod.lora_B["q_proj"].grad.clone()))
+    for a, b, what in zip(grads[0], grads[1], ("dx", "dA", "dB")):
+        assert torch.equal(a, b), what
+
+
 def test_rope():
     from gke_ray_train_amd.ops import _ref
     C = _C()
@@ -408,7 +480,6 @@ def test_fused_lora_matches_reference(nf4, p, targets):
     from gke_ray_train_amd.ops.linear import Linear
     from gke_ray_train_amd.peft.lora import LoraConfig, LoraLinear
     from gke_ray_train_amd.peft.quant import BitsAndBytesConfig, NF4Linear
-    from gke_ray_train_amd import _native
     torch.manual_seed(0)
     lin = Linear(256, 768, bias=False, device=DEV, dtype=torch.bfloat16)
     lin.slices = [("q_proj", 256), ("k_proj", 256), ("v_proj", 256)]
@@ -423,20 +494,21 @@ def test_fused_lora_matches_reference(nf4, p, targets):
         for n in names:
             mod.lora_B[n].normal_(0, 0.05)
     x = torch.randn(4, 64, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
-    from gke_ray_train_amd.ops import fused
-    start = fused._dropout_counter[0]
+    from gke_ray_train_amd.ops import _ref
+    rng = torch.get_rng_state()
     y = mod(x)
     dy = torch.randn_like(y)
     (y.float() * dy.float()).sum().backward()
-    # reference in fp32 with the same counter-based mask
-    seed = int(torch.cuda.default_generators[0].initial_seed()) & 0xFFFFFF
+    # reference in fp32; the mask from the host reimplementation of the hash with the seed the op
+    # drew from torch's CPU generator (ops/fused.py::dropout_seed_offset)
+    torch.set_rng_state(rng)
+    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
     x2 = x.detach().view(-1, 256).float().requires_grad_()
     w = (base.dequantize() if nf4 else lin.weight).detach().float()
     A = {n: mod.lora_A[n].detach().float().requires_grad_() for n in names}
     B = {n: mod.lora_B[n].detach().float().requires_grad_() for n in names}
     if p > 0:
-        xb = x.detach().view(-1, 256).contiguous()
-        keep = (_native.kernels().dropout_fwd_seeded(torch.ones_like(xb), p, seed, start) != 0).float()
+        keep = _ref.dropout_keep_mask(seed, 0, x2.numel(), p).to(DEV).view_as(x2).float()
         xd = x2 * keep / (1 - p)
     else:
         xd = x2
