@@ -105,7 +105,7 @@ struct AttnBwdParams {
   void* dq; int64_t dq_bs, dq_ss, dq_hs;
   void* dk; int64_t dk_bs, dk_ss, dk_hs;
   void* dv; int64_t dv_bs, dv_ss, dv_hs;
-  float* delta;    // fp32 workspace [B, Hq, Sq]
+  float* delta;    // fp32 workspace of attn_bwd_workspace_floats(): delta and lse2 rows
 };
 void attn_bwd(const AttnBwdParams& p, hipStream_t s);
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int D);

@@ -10,21 +10,33 @@
 // input — no transposes. D = 128. GQA: query head h reads kv head h / (Hq / Hkv).
 //
 // MFMA mapping (v_mfma_f32_32x32x16_bf16, cdna_hip_programming.md §3):
-//   forward, per wave = 32 query rows, per K/V tile = 64 keys:
-//     S^T[key][q] = K · Q^T   (A = K rows from LDS, B = Q rows held in VGPRs)  -> the query is
-//                  the MFMA lane, so row max / row sum of the online softmax are lane-local
-//                  (+ one lane^32 exchange) and the O^T rescale needs no cross-lane traffic;
-//     O^T[d][q]  += V^T · P^T  (A = V^T via ds_read_b64_tr_b16 on the row-major V tile,
-//                  B = the S^T accumulator converted to bf16 in place: §3 "accumulator tile as
-//                  the next MFMA's operand", with the permuted key order matched on the V side).
-//   backward, per workgroup = 128 keys of one kv head (32 per wave, key on the MFMA lane):
-//     S = Q·K^T, dP = dO·V^T (accumulators are directly the B operands of)
-//     dV^T += dO^T · P,  dK^T += Q^T · dS  (A operands by transposed LDS reads);
-//     dS crosses LDS once, transposed, for dQ = dS · K, which is added with fp32 atomics
-//     (256-byte row segments, the full-rate shape of MI355X_MICROARCH.md §Global float atomics).
+//   forward and dQ, per wave = 32 query rows on the MFMA lane:
+//     S^T[key][q] = K · Q^T  (A = K rows from LDS, B = Q rows held in VGPRs) -> row max / row sum
+//                  of the online softmax are lane-local (+ one permlane32 swap);
+//     O^T[d][q] += V^T · P^T, dQ^T += K^T · dS^T  (A = V^T / K^T by ds_read_b64_tr_b16 transposed
+//                  reads of the row-major tile, B = the S^T accumulator converted to bf16 in place:
+//                  §3 "accumulator tile as the next MFMA's operand");
+//   dK / dV, per wave = 32 keys on the MFMA lane, K / V fragments in VGPRs for the whole sweep:
+//     S = Q·K^T, dP = dO·V^T, then dV^T += dO^T · P and dK^T += Q^T · dS (transposed reads).
+//   No atomics anywhere: dQ and dK / dV come from separate kernels, each complete in registers.
+// Pipeline shared by the three kernels (cdna_hip_programming.md "Pipelining across barriers"):
+//   * the streamed operand (K / V for forward and dQ, Q / dO + row statistics for dK / dV) arrives
+//     in 32-row tiles by LDS-DMA (global_load_lds_dwordx4, no VGPR staging) into a 4-slot ring,
+//     with the XOR chunk swizzle applied to the per-lane SOURCE address (rule 21); two tiles stay
+//     in flight behind a counted vmcnt across a raw s_barrier (never __syncthreads);
+//   * software pipeline: the S (and dP) MFMAs of tile t+1 are issued ahead of tile t's VALU work
+//     (exponentials, dS) and its accumulation MFMAs, in one basic block;
+//   * the loop is unrolled over the ring, so every LDS address is a per-lane base + an immediate;
+//   * masks (causal diagonal, key padding) are selects on the tiles that touch them only; padded
+//     query rows carry lse = +inf and need none;
+//   * forward: deferred rescale of the online softmax (T13).
 //   All LDS tiles use the dual row-read / transposed-read XOR image of cdna_hip_programming.md
 //   T10 (b), conflict-free for both the ds_read_b128 row reads and the tr_b16 reads.
+// Measured on MI355X (B8 S1024 H32 D128 causal, tools/attn_ab.py; profiles/r2_attention.md).
+#include <limits.h>
 #include <stdlib.h>
+
+#include <type_traits>
 
 #include "grt_common.h"
 #include "grt_kernels.h"
@@ -87,20 +99,48 @@ __device__ __forceinline__ float drop_factor(const AttnParams& p, uint32_t bh, i
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
+// max over lanes l and l ^ 32 by v_permlane32_swap (a VALU op; no LDS round trip): after the
+// swap of x with itself, element 0 holds the lower half's value and element 1 the upper's in
+// every lane.
+__device__ __forceinline__ float halves_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// Deferred rescale (cdna_hip_programming.md T13): the running max m only moves when some row of
+// the wave sees a tile max more than kDeferLog2 above it, so most tiles skip the O / l rescale;
+// between rescales the exponentiated scores are bounded by 2^kDeferLog2 (exact in fp32 l / O,
+// bf16 P keeps its relative precision).
+constexpr float kDeferLog2 = 8.f;
+
+// 16-byte LDS-DMA per lane to (wave-uniform LDS byte address) + lane * 16; M0 is written in the
+// same statement (compiler-reserved). Not tracked by hipcc's waitcnt pass: the kernel counts vmcnt.
+__device__ __forceinline__ void lds_dma16(const void* gptr, uint32_t lds_byte_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(gptr), "s"(lds_byte_addr) : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+__device__ __forceinline__ int img_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
 // ---------------------------------------------------------------------------------------------
-// Forward
+// Forward: 4 waves x 32 query rows, 32-key K / V tiles through the ring, 16 MFMAs per tile and
+// wave, two workgroups per CU. (A 256-row / 8-wave workgroup, halving the K / V bytes per FLOP,
+// measured slower at S = 1024 from the causal tail; an explicit MFMA / VALU interleave by
+// sched_group_barrier measured neutral-to-slower: profiles/r2_attention.md.)
 // ---------------------------------------------------------------------------------------------
-constexpr int FBM = 128, FBN = 64, FNT = 256;
-constexpr int kTileBytes = FBN * D * 2;  // 16 KiB
+constexpr int F3M = 128, F3N = 32, F3NT = 256, F3NSLOT = 4;
+constexpr int F3IMG = F3N * D * 2;   // 8 KiB
+constexpr int F3SLOT = 2 * F3IMG;    // K, V
 
 template <bool DROP>
-__global__ __launch_bounds__(FNT, 2) void attn_fwd_kernel(const AttnParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // K[2], V[2]
-  auto Kl = [&](int buf) -> char* { return smem + buf * kTileBytes; };
-  auto Vl = [&](int buf) -> char* { return smem + (2 + buf) * kTileBytes; };
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int nqb = (p.Sq + FBM - 1) / FBM;
+__global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
+  __shared__ __attribute__((aligned(16))) char smem[F3NSLOT * F3SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, l16 = lane & 15;
+  const int nqb = (p.Sq + F3M - 1) / F3M;
   const int BH = p.B * p.Hq;
   const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) blocks first
   const int bh = blockIdx.x % BH;
@@ -109,129 +149,147 @@ __global__ __launch_bounds__(FNT, 2) void attn_fwd_kernel(const AttnParams p) {
   GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && qblk >= 0);
   const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
   const int off = p.Sk - p.Sq;  // bottom-right aligned causal mask
-  const int q0 = qblk * FBM, qw0 = q0 + w * 32;
+  const int q0 = qblk * F3M, qw0 = q0 + w * 32;
   const int myq = qw0 + l32;
 
   const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + (int64_t)hq * p.q_hs;
   const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs;
   const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs;
 
-  // Q fragments (B operand of S^T = K Q^T): lane holds Q[myq][16ks + 8h .. +7]
   bf16x8 qf[D / 16];
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) {
     if (myq < p.Sq) qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)myq * p.q_ss + ks * 16 + 8 * h);
     else qf[ks] = bf16x8{};
   }
+  const int klim = p.causal ? min(sk - 1, myq + off) : sk - 1;   // keys <= klim are kept
+  const int kmask = p.causal ? min(sk, qw0 + off + 1) : sk;      // tiles reaching past need the mask
 
   int kend = sk;
-  if (p.causal) kend = min(kend, q0 + FBM + off);
-  const int nt = kend > 0 ? (kend + FBN - 1) / FBN : 0;
+  if (p.causal) kend = min(kend, q0 + F3M + off);
+  const int nt = kend > 0 ? (kend + F3N - 1) / F3N : 0;
 
-  bf16x8 kreg[4], vreg[4];
-  auto load_tile = [&](int t) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = tid + FNT * r, row = i / kChunks, c = i % kChunks, key = t * FBN + row;
-      if (key < sk) {
-        kreg[r] = *reinterpret_cast<const bf16x8*>(K + (int64_t)key * p.k_ss + c * 8);
-        vreg[r] = *reinterpret_cast<const bf16x8*>(Vg + (int64_t)key * p.v_ss + c * 8);
-      } else {
-        kreg[r] = bf16x8{};
-        vreg[r] = bf16x8{};
-      }
-    }
+  const uint32_t smem0 = lds_u32(smem);
+  // wave w fills image rows 8w .. 8w+7 of K and V: two 1-KiB pieces of 4 rows per image
+  const int row0 = 8 * w + g, row1 = row0 + 4;
+  const int ch0 = l16 ^ img_swz(row0), ch1 = l16 ^ img_swz(row1);
+  auto dma_tile = [&](int t, uint32_t slot_off) {
+    const int64_t k0r = min(t * F3N + row0, p.Sk - 1), k1r = min(t * F3N + row1, p.Sk - 1);  // past Sk: masked
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(8 * w * 256));
+    lds_dma16(K + k0r * p.k_ss + ch0 * 8, dst);
+    lds_dma16(Vg + k0r * p.v_ss + ch0 * 8, dst + F3IMG);
+    lds_dma16(K + k1r * p.k_ss + ch1 * 8, dst + 1024);
+    lds_dma16(Vg + k1r * p.v_ss + ch1 * 8, dst + F3IMG + 1024);
   };
-  auto store_tile = [&](int buf) {
+  auto wait_dma = [&](int pending_tiles) {  // 4 DMA instructions per tile
+    if (pending_tiles >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (pending_tiles == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // S^T = K Q^T of the tile in slot SL; the 8 K-row fragments are read into registers before the
+  // MFMA chain so the reads are in flight together (not one LDS round trip per MFMA)
+  auto qk = [&](auto slot_c) {
+    constexpr int SL = decltype(slot_c)::value;
+    const char* ki = smem + SL * F3SLOT;
+    bf16x8 kr[D / 16];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = tid + FNT * r, row = i / kChunks, c = i % kChunks;
-      *reinterpret_cast<bf16x8*>(Kl(buf) + img_off(row, c)) = kreg[r];
-      *reinterpret_cast<bf16x8*>(Vl(buf) + img_off(row, c)) = vreg[r];
+    for (int ks = 0; ks < D / 16; ++ks) kr[ks] = lds_row_read(ki, l32, 2 * ks + h);
+    f32x16 s = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) s = mfma32(kr[ks], qf[ks], s);
+    return s;
+  };
+  // -inf on the masked keys of tile t, applied only on tiles that touch the diagonal / key padding
+  auto apply_mask = [&](int t, f32x16& s) {
+    const int kb = t * F3N;
+    if (kb + F3N > kmask) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = kb + acc_row(r, h) <= klim ? s[r] : -INFINITY;
     }
   };
 
   f32x16 o[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) o[i] = f32x16{};
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;  // m in log2 units of the scaled scores
   const float c = p.scale * kLog2e;
 
-  if (nt > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    const int kb = t * FBN;
-    if (t + 1 < nt) load_tile(t + 1);
-    const bool skip = p.causal && (kb > qw0 + 31 + off);   // whole tile masked for this wave
-    if (!skip) {
-      // ---- S^T = K Q^T : two 32-key subtiles
-      f32x16 s[2];
+  // one pipeline step. Order: the branchy parts first (ring wait / barrier / DMA, tile t's mask,
+  // row max and deferred rescale), then ONE basic block holding S^T of tile t+1 (independent
+  // MFMAs), tile t's exponentials and its P V MFMAs.
+  auto step = [&](int t, auto slot_c, f32x16& s_c, f32x16& s_n) {
+    constexpr int SL = decltype(slot_c)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + 1 < nt) wait_dma(min(nt, t + F3NSLOT - 1) - (t + 2));
+    __builtin_amdgcn_s_barrier();
+    if (t + F3NSLOT - 1 < nt) dma_tile(t + F3NSLOT - 1, (uint32_t)(((SL + F3NSLOT - 1) % F3NSLOT) * F3SLOT));
+
+    apply_mask(t, s_c);
+    float mx = fmaxf(s_c[0], s_c[1]);
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        s[n] = f32x16{};
-#pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          const bf16x8 a = lds_row_read(Kl(cur), n * 32 + l32, 2 * ks + h);
-          s[n] = mfma32(a, qf[ks], s[n]);
-        }
-      }
-      // ---- online softmax (query = lane, keys = registers)
-      const bool need_mask = (kb + FBN > sk) || (p.causal && kb + FBN - 1 > qw0 + off);
-      float mx = -INFINITY;
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float v = s[n][r] * c;
-          if (need_mask) {
-            const int key = kb + n * 32 + acc_row(r, h);
-            if (key >= sk || (p.causal && key > myq + off)) v = -INFINITY;
-          }
-          s[n][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    for (int r = 2; r < 16; ++r) mx = fmaxf(mx, s_c[r]);
+    mx = halves_max(mx) * c;  // tile row max, log2 units (-inf: every key masked)
+    if (__any(mx > m + kDeferLog2)) {
       const float mn = fmaxf(m, mx);
-      const float msub = (mn == -INFINITY) ? 0.f : mn;
-      const float alpha = fast_exp2(m - msub);
-      float rs = 0.f;
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float e = fast_exp2(s[n][r] - msub);
-          rs += e;  // the softmax normaliser uses the undropped probabilities
-          s[n][r] = DROP ? e * drop_factor(p, (uint32_t)bh, myq, kb + n * 32 + acc_row(r, h)) : e;
-        }
-      l = l * alpha + rs;
-      m = mn;
+      const float alpha = mn == -INFINITY ? 1.f : fast_exp2(m - mn);
+      l *= alpha;
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[i] *= alpha;
-      // ---- O^T += V^T P^T : 4 key-steps of 16, 4 d-blocks of 32
-      const int g = lane >> 4, l16 = lane & 15;
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8 pb = pack8(s[n], 8 * st);
-          const int kk = n * 32 + 16 * st + 4 * h;
-#pragma unroll
-          for (int db = 0; db < 4; ++db) {
-            const int c0 = db * 32 + (g & 1) * 16;
-            const bf16x8 a = cat(lds_tr_read(Vl(cur), kk, c0, l16), lds_tr_read(Vl(cur), kk + 8, c0, l16));
-            o[db] = mfma32(a, pb, o[db]);
-          }
-        }
+      m = mn;
     }
-    if (t + 1 < nt) store_tile(cur ^ 1);
-    __syncthreads();
-  }
+    const float msub = m == -INFINITY ? 0.f : m;
 
-  // ---- epilogue
+    s_n = qk(std::integral_constant<int, (SL + 1) % F3NSLOT>{});  // past the end: dropped
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float e = fast_exp2(fmaf(s_c[r], c, -msub));
+      rs += e;  // the softmax normaliser uses the undropped probabilities
+      s_c[r] = DROP ? e * drop_factor(p, (uint32_t)bh, myq, t * F3N + acc_row(r, h)) : e;
+    }
+    l += rs;
+    const char* vi = smem + SL * F3SLOT + F3IMG;
+    bf16x8 va[2][4];
+#pragma unroll
+    for (int stp = 0; stp < 2; ++stp) {
+      const int kk = 16 * stp + 4 * h;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int c0 = db * 32 + (g & 1) * 16;
+        va[stp][db] = cat(lds_tr_read(vi, kk, c0, l16), lds_tr_read(vi, kk + 8, c0, l16));
+      }
+    }
+#pragma unroll
+    for (int stp = 0; stp < 2; ++stp) {
+      const bf16x8 pb = pack8(s_c, 8 * stp);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] = mfma32(va[stp][db], pb, o[db]);
+    }
+  };
+
+  if (nt > 0) {
+    const int pre = min(nt, F3NSLOT - 1);
+    for (int t = 0; t < pre; ++t) dma_tile(t, (uint32_t)(t * F3SLOT));
+    wait_dma(pre - 1);
+    __builtin_amdgcn_s_barrier();
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    f32x16 sA = qk(I0{}), sB;
+    int t = 0;
+    for (; t + F3NSLOT <= nt; t += F3NSLOT) {
+      step(t, I0{}, sA, sB);
+      step(t + 1, I1{}, sB, sA);
+      step(t + 2, I2{}, sA, sB);
+      step(t + 3, I3{}, sB, sA);
+    }
+    if (t < nt) step(t, I0{}, sA, sB);
+    if (t + 1 < nt) step(t + 1, I1{}, sB, sA);
+    if (t + 2 < nt) step(t + 2, I2{}, sA, sB);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
   if (myq < p.Sq) {
@@ -253,17 +311,22 @@ __global__ __launch_bounds__(FNT, 2) void attn_fwd_kernel(const AttnParams p) {
 // ---------------------------------------------------------------------------------------------
 // Backward
 // ---------------------------------------------------------------------------------------------
-constexpr int BBN = 128, BBM = 32, BNT = 256;
+// Row statistics live in a padded workspace: per (batch, query head) a row of sq_pad(Sq) floats of
+// delta = rowsum(dO * O) and of lse2 = lse * log2(e) (+inf on the padding rows, so their
+// probabilities come out exactly 0 with no mask): query tiles of 32 rows never straddle a head, the
+// 16-byte DMA pieces are aligned, and no row index needs a bounds check.
+__host__ __device__ inline int sq_pad(int Sq) { return (Sq + 31) / 32 * 32; }
 
-// delta[b,h,q] = sum_d dO*O (fp32): 16 lanes x 8 elements per row, 4 rows per wave, 16 per block
 __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p) {
   const int l16 = threadIdx.x & 15;
+  const int Sqp = sq_pad(p.f.Sq);
   const int64_t row = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
-  const int64_t nrows = (int64_t)p.f.B * p.f.Hq * p.f.Sq;
+  const int64_t nrows = (int64_t)p.f.B * p.f.Hq * Sqp;
+  if (row >= nrows) return;
+  const int q = (int)(row % Sqp);
+  const int64_t bh = row / Sqp;
   float acc = 0.f;
-  if (row < nrows) {
-    const int q = (int)(row % p.f.Sq);
-    const int64_t bh = row / p.f.Sq;
+  if (q < p.f.Sq) {
     const int hq = (int)(bh % p.f.Hq), b = (int)(bh / p.f.Hq);
     const bf16* O = (const bf16*)p.f.o + (int64_t)b * p.f.o_bs + (int64_t)hq * p.f.o_hs + (int64_t)q * p.f.o_ss;
     const bf16* dO = (const bf16*)p.dout + (int64_t)b * p.do_bs + (int64_t)hq * p.do_hs + (int64_t)q * p.do_ss;
@@ -274,43 +337,45 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p
     for (int k = 0; k < 8; ++k) acc += a[k] * g[k];
   }
 #pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 64);
-  if (row < nrows && l16 == 0) p.delta[row] = acc;
+  for (int o = 8; o >= 1; o >>= 1) acc += __shfl_xor(acc, o, 16);
+  if (l16 == 0) {
+    float* lse2 = p.delta + nrows;
+    p.delta[row] = acc;
+    lse2[row] = q < p.f.Sq ? p.f.lse[bh * p.f.Sq + q] * kLog2e : INFINITY;
+  }
 }
 
-// dK / dV kernel: one workgroup = 128 keys of one (batch, kv head), 32 keys per wave with the key on
-// the MFMA lane; K and V fragments stay in VGPRs for the whole sweep over the group's query heads
-// x (32 * NQ)-row query tiles (Q / dO tiles double-buffered in LDS, one barrier per tile). No
-// atomics: dK and dV are complete in registers at the end. NQ = 2 gives every wave four independent
-// MFMA accumulation chains per tile (S and dP for two 32-row halves) and halves the barriers.
-template <bool DROP, int NQ>
-__global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdParams P) {
-  const AttnParams& p = P.f;
-  constexpr int TM = BBM * NQ;           // query rows per tile
-  constexpr int QB = TM * D * 2;
-  constexpr int LD = TM * kChunks / BNT;  // 16-byte chunks per thread per operand
-  __shared__ __attribute__((aligned(16))) char smem[4 * QB + 2 * 2 * TM * 4];
-  auto Ql = [&](int buf) -> char* { return smem + buf * QB; };
-  auto dOl = [&](int buf) -> char* { return smem + (2 + buf) * QB; };
-  float* lsel = (float*)(smem + 4 * QB);  // [2][TM]
-  float* dell = lsel + 2 * TM;            // [2][TM]
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+// dK / dV: one workgroup = 128 keys of one (batch, kv head), 32 keys per wave on the MFMA lane,
+// K / V fragments in registers for the whole sweep over the group's query heads x 32-row query
+// tiles (Q / dO tiles and their row statistics through the ring). Per tile the wave does 32 MFMAs
+// (S, dP, dV^T, dK^T, 8 each); the S accumulator starts at -inf on masked (query, key) pairs of
+// the diagonal / padding tiles. One workgroup (one wave per SIMD) per CU: K / V fragments and the
+// dK / dV accumulators take ~450 registers. Heaviest (earliest, causal) key blocks launch first.
+constexpr int K2N = 128, K2M = 32, K2NT = 256, K2NSLOT = 4;
+constexpr int K2IMG = K2M * D * 2;           // one 32-row image: 8 KiB
+constexpr int K2SLOT = 2 * K2IMG + 4 * 1024;  // Q image, dO image, per-wave statistics copy
+
+template <bool DROP>
+__global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdParams P) {
+  const AttnParams& p = P.f;
+  __shared__ __attribute__((aligned(16))) char smem[K2NSLOT * K2SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
   const int g = lane >> 4, l16 = lane & 15;
-  const int nkb = (p.Sk + BBN - 1) / BBN;
-  const int kblk = nkb - 1 - (int)(blockIdx.x / (p.B * p.Hkv));  // causal: lightest key blocks last
-  const int bhk = blockIdx.x % (p.B * p.Hkv);
+  const int BHk = p.B * p.Hkv;
+  const int kblk = (int)(blockIdx.x / BHk);  // causal: heaviest (earliest) key blocks first
+  const int bhk = blockIdx.x % BHk;
   const int b = bhk / p.Hkv, hkv = bhk % p.Hkv;
   const int grp = p.Hq / p.Hkv;
-  GRT_DEVICE_CHECK(kblk >= 0 && grp * p.Hkv == p.Hq);
+  GRT_DEVICE_CHECK(grp * p.Hkv == p.Hq && kblk * K2N < p.Sk);
   const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
   const int off = p.Sk - p.Sq;
-  const int k0 = kblk * BBN;
-  const int kw0 = k0 + w * 32;
-  const int mykey = kw0 + l32;
+  const int k0 = kblk * K2N, kw0 = k0 + w * 32, mykey = kw0 + l32;
   const float c = p.scale * kLog2e;
+  const int Sqp = sq_pad(p.Sq);
+  const float* lse2 = P.delta + (int64_t)p.B * p.Hq * Sqp;
 
-  // K / V fragments (B operands of S = Q K^T and dP = dO V^T): lane holds row `mykey`
   const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs;
   const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs;
   bf16x8 kf[D / 16], vf[D / 16];
@@ -324,116 +389,154 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
       vf[ks] = bf16x8{};
     }
   }
-
   f32x16 dk[4], dv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) { dk[i] = f32x16{}; dv[i] = f32x16{}; }
 
-  int qstart = 0;
-  if (p.causal) qstart = max(0, k0 - off);
-  qstart = (qstart / BBM) * BBM;
-  const int nqt = qstart < p.Sq ? (p.Sq - qstart + TM - 1) / TM : 0;
+  int qstart = p.causal ? max(0, k0 - off) : 0;
+  qstart = (qstart / K2M) * K2M;
+  const int nqt = qstart < p.Sq ? (p.Sq - qstart + K2M - 1) / K2M : 0;
   const int total = (k0 < sk) ? nqt * grp : 0;
+  // per-lane mask: probability of (q, mykey) kept iff mykey < sk and (non-causal or q >= qlim)
+  const int qlim = mykey < sk ? (p.causal ? mykey - off : INT_MIN) : INT_MAX;
+  // the tile starting at query qt needs the mask iff qt < qmask (diagonal) or the block has padding
+  const int qmask = (k0 + K2N > sk) ? INT_MAX : (p.causal ? kw0 + 31 - off : INT_MIN);
 
-  bf16x8 qreg[LD], oreg[LD];
-  float lse_r = 0.f, del_r = 0.f;
-  auto load_q = [&](int it) {
-    const int hq = hkv * grp + it / nqt;
-    const int qt = qstart + (it % nqt) * TM;
+  // ---- LDS-DMA of tile j into a slot: wave w fills image rows 8w .. 8w+7 of Q and dO (two 1-KiB
+  // pieces each; the XOR swizzle goes on the per-lane SOURCE chunk) and its own copy of the tile's
+  // 32 lse2 and 32 delta values (lanes 0-7 / 8-15; lanes 16-63 repeat them).
+  const uint32_t smem0 = lds_u32(smem);
+  const int row0 = 8 * w + g, row1 = row0 + 4;
+  const int ch0 = l16 ^ img_swz(row0), ch1 = l16 ^ img_swz(row1);
+  const int sl = l16 & 7;
+  const int64_t st_lane = (l16 < 8 ? (int64_t)p.B * p.Hq * Sqp : 0) + 4 * sl;  // lse2 | delta
+  auto dma_tile = [&](int hq, int qt, uint32_t slot_off) {
     const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + (int64_t)hq * p.q_hs;
     const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + (int64_t)hq * P.do_hs;
+    const int64_t q0r = min(qt + row0, p.Sq - 1), q1r = min(qt + row1, p.Sq - 1);  // past Sq: lse2 = +inf
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(8 * w * 256));
+    lds_dma16(Q + q0r * p.q_ss + ch0 * 8, dst);
+    lds_dma16(dO + q0r * P.do_ss + ch0 * 8, dst + K2IMG);
+    lds_dma16(Q + q1r * p.q_ss + ch1 * 8, dst + 1024);
+    lds_dma16(dO + q1r * P.do_ss + ch1 * 8, dst + K2IMG + 1024);
+    const int64_t ri = ((int64_t)b * p.Hq + hq) * Sqp + qt;
+    lds_dma16(P.delta + st_lane + ri,
+              __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(2 * K2IMG + w * 1024)));
+  };
+  auto wait_dma = [&](int pending_tiles) {  // 5 DMA instructions per tile
+    if (pending_tiles >= 2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (pending_tiles == 1) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // S and dP of the tile at query qt in slot SL (query rows in registers, key on the lane)
+  auto sdp = [&](int qt, auto slot_c, f32x16& s, f32x16& dp) {
+    constexpr int SL = decltype(slot_c)::value;
+    const char* qi = smem + SL * K2SLOT;
+    s = f32x16{};
+    if (qt < qmask) {  // wave-uniform: the tile touches the diagonal / key padding
 #pragma unroll
-    for (int r = 0; r < LD; ++r) {
-      const int i = tid + BNT * r, row = i / kChunks, ch = i % kChunks, q = qt + row;
-      if (q < p.Sq) {
-        qreg[r] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)q * p.q_ss + ch * 8);
-        oreg[r] = *reinterpret_cast<const bf16x8*>(dO + (int64_t)q * P.do_ss + ch * 8);
-      } else {
-        qreg[r] = bf16x8{};
-        oreg[r] = bf16x8{};
-      }
+      for (int r = 0; r < 16; ++r) s[r] = qt + acc_row(r, h) >= qlim ? 0.f : -INFINITY;
     }
-    if (tid < TM) {
-      const int q = qt + tid;
-      const int64_t ri = ((int64_t)b * p.Hq + hq) * p.Sq + q;
-      lse_r = q < p.Sq ? p.lse[ri] * kLog2e : INFINITY;
-      del_r = q < p.Sq ? P.delta[ri] : 0.f;
+    dp = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      s = mfma32(lds_row_read(qi, l32, 2 * ks + h), kf[ks], s);
+      dp = mfma32(lds_row_read(qi + K2IMG, l32, 2 * ks + h), vf[ks], dp);
     }
   };
-  auto store_q = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < LD; ++r) {
-      const int i = tid + BNT * r, row = i / kChunks, ch = i % kChunks;
-      *reinterpret_cast<bf16x8*>(Ql(buf) + img_off(row, ch)) = qreg[r];
-      *reinterpret_cast<bf16x8*>(dOl(buf) + img_off(row, ch)) = oreg[r];
-    }
-    if (tid < TM) { lsel[buf * TM + tid] = lse_r; dell[buf * TM + tid] = del_r; }
+
+  // tile cursors (query head, query start): the tile being consumed, the next one, the DMA one
+  int cur_h = 0, cur_q = qstart;
+  auto advance = [&](int& hh, int& qq) {
+    qq += K2M;
+    if (qq >= p.Sq) { qq = qstart; ++hh; }
   };
+  int nxt_h = cur_h, nxt_q = cur_q;
+  advance(nxt_h, nxt_q);
+  int dma_h = 0, dma_q = qstart;
 
-  if (total > 0) { load_q(0); store_q(0); }
-  __syncthreads();
+  auto step = [&](int t, auto slot_c, f32x16& s_c, f32x16& dp_c, f32x16& s_n, f32x16& dp_n) {
+    constexpr int SL = decltype(slot_c)::value;
+    // tile t+1 landed for every wave, and every wave is done with tile t-1 (its slot is refilled)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + 1 < total) wait_dma(min(total, t + K2NSLOT - 1) - (t + 2));
+    __builtin_amdgcn_s_barrier();
+    if (t + K2NSLOT - 1 < total) {
+      dma_tile(hkv * grp + dma_h, dma_q, (uint32_t)(((SL + K2NSLOT - 1) % K2NSLOT) * K2SLOT));
+      advance(dma_h, dma_q);
+    }
 
-  for (int it = 0; it < total; ++it) {
-    const int cur = it & 1;
-    const int qt = qstart + (it % nqt) * TM;
-    if (it + 1 < total) load_q(it + 1);
-    if (!(p.causal && (kw0 > qt + TM - 1 + off))) {  // else: all 32 keys after every row of the tile
-      f32x16 s[NQ], dp[NQ];
+    sdp(nxt_q, std::integral_constant<int, (SL + 1) % K2NSLOT>{}, s_n, dp_n);  // past the end: dropped
+
+    const char* qi = smem + SL * K2SLOT;
+    const float* st = reinterpret_cast<const float*>(qi + 2 * K2IMG + w * 1024);
+    bf16x8 pb[2], sb[2];
 #pragma unroll
-      for (int n = 0; n < NQ; ++n) { s[n] = f32x16{}; dp[n] = f32x16{}; }
+    for (int gg = 0; gg < 4; ++gg) {
+      const f32x4 ls = *reinterpret_cast<const f32x4*>(st + 8 * gg + 4 * h);
+      const f32x4 de = *reinterpret_cast<const f32x4*>(st + 32 + 8 * gg + 4 * h);
 #pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks)
-#pragma unroll
-        for (int n = 0; n < NQ; ++n) {
-          s[n] = mfma32(lds_row_read(Ql(cur), n * 32 + l32, 2 * ks + h), kf[ks], s[n]);
-          dp[n] = mfma32(lds_row_read(dOl(cur), n * 32 + l32, 2 * ks + h), vf[ks], dp[n]);
-        }
-#pragma unroll
-      for (int n = 0; n < NQ; ++n) {
-        const int qn = qt + n * 32;
-        const bool need_mask = (k0 + BBN > sk) || (p.causal && kw0 + 31 > qn + off) || (qn + 32 > p.Sq);
-#pragma unroll
-        for (int gg = 0; gg < 4; ++gg) {
-          const f32x4 ls = *reinterpret_cast<const f32x4*>(lsel + cur * TM + n * 32 + 8 * gg + 4 * h);
-          const f32x4 de = *reinterpret_cast<const f32x4*>(dell + cur * TM + n * 32 + 8 * gg + 4 * h);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int r = 4 * gg + j;
-            const int q = qn + 8 * gg + 4 * h + j;
-            float pv = fast_exp2(s[n][r] * c - ls[j]);
-            if (need_mask && (mykey >= sk || q >= p.Sq || (p.causal && mykey > q + off))) pv = 0.f;
-            if (DROP) {
-              const uint32_t bhq = (uint32_t)(b * p.Hq + hkv * grp + it / nqt);
-              const float z = drop_factor(p, bhq, q, mykey);
-              s[n][r] = pv * z;                   // dV uses the dropped probabilities
-              dp[n][r] = pv * (dp[n][r] * z - de[j]);
-            } else {
-              s[n][r] = pv;
-              dp[n][r] = pv * (dp[n][r] - de[j]);
-            }
-          }
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * gg + j;
+        const float pv = fast_exp2(fmaf(s_c[r], c, -ls[j]));
+        if (DROP) {
+          const float z = drop_factor(p, (uint32_t)(b * p.Hq + hkv * grp + cur_h), cur_q + 8 * gg + 4 * h + j, mykey);
+          s_c[r] = pv * z;                  // dV uses the dropped probabilities
+          dp_c[r] = pv * (dp_c[r] * z - de[j]);
+        } else {
+          s_c[r] = pv;
+          dp_c[r] = pv * (dp_c[r] - de[j]);
         }
       }
-#pragma unroll
-      for (int n = 0; n < NQ; ++n)
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8 pb = pack8(s[n], 8 * st);
-          const bf16x8 sb = pack8(dp[n], 8 * st);
-          const int kk = n * 32 + 16 * st + 4 * h;
-#pragma unroll
-          for (int db = 0; db < 4; ++db) {
-            const int c0 = db * 32 + (g & 1) * 16;
-            const bf16x8 oa = cat(lds_tr_read(dOl(cur), kk, c0, l16), lds_tr_read(dOl(cur), kk + 8, c0, l16));
-            dv[db] = mfma32(oa, pb, dv[db]);
-            const bf16x8 qa = cat(lds_tr_read(Ql(cur), kk, c0, l16), lds_tr_read(Ql(cur), kk + 8, c0, l16));
-            dk[db] = mfma32(qa, sb, dk[db]);
-          }
-        }
     }
-    if (it + 1 < total) store_q(cur ^ 1);
-    __syncthreads();
+    pb[0] = pack8(s_c, 0);
+    pb[1] = pack8(s_c, 8);
+    sb[0] = pack8(dp_c, 0);
+    sb[1] = pack8(dp_c, 8);
+    // dV^T += dO^T P, dK^T += Q^T dS (transposed reads of tile t's images)
+#pragma unroll
+    for (int stp = 0; stp < 2; ++stp) {
+      const int kk = 16 * stp + 4 * h;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int c0 = db * 32 + (g & 1) * 16;
+        const bf16x8 oa = cat(lds_tr_read(qi + K2IMG, kk, c0, l16), lds_tr_read(qi + K2IMG, kk + 8, c0, l16));
+        dv[db] = mfma32(oa, pb[stp], dv[db]);
+        const bf16x8 qa = cat(lds_tr_read(qi, kk, c0, l16), lds_tr_read(qi, kk + 8, c0, l16));
+        dk[db] = mfma32(qa, sb[stp], dk[db]);
+      }
+    }
+    cur_h = nxt_h;
+    cur_q = nxt_q;
+    advance(nxt_h, nxt_q);
+  };
+
+  if (total > 0) {
+    const int pre = min(total, K2NSLOT - 1);
+    for (int j = 0; j < pre; ++j) {
+      dma_tile(hkv * grp + dma_h, dma_q, (uint32_t)(j * K2SLOT));
+      advance(dma_h, dma_q);
+    }
+    wait_dma(pre - 1);
+    __builtin_amdgcn_s_barrier();
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    f32x16 sA, dpA, sB, dpB;
+    sdp(cur_q, I0{}, sA, dpA);
+    int t = 0;
+    for (; t + K2NSLOT <= total; t += K2NSLOT) {  // one ring revolution: slots 0..3, register sets A/B
+      step(t, I0{}, sA, dpA, sB, dpB);
+      step(t + 1, I1{}, sB, dpB, sA, dpA);
+      step(t + 2, I2{}, sA, dpA, sB, dpB);
+      step(t + 3, I3{}, sB, dpB, sA, dpA);
+    }
+    if (t < total) step(t, I0{}, sA, dpA, sB, dpB);
+    if (t + 1 < total) step(t + 1, I1{}, sB, dpB, sA, dpA);
+    if (t + 2 < total) step(t + 2, I2{}, sA, dpA, sB, dpB);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   if (mykey < p.Sk) {
     bf16* dK = (bf16*)P.dk + (int64_t)b * P.dk_bs + (int64_t)hkv * P.dk_hs + (int64_t)mykey * P.dk_ss;
@@ -454,30 +557,33 @@ __global__ __launch_bounds__(BNT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPara
   }
 }
 
-// dQ kernel: the forward's structure (32 query rows per wave, query on the MFMA lane, K/V tiles of
-// 64 keys double-buffered in LDS). S^T = K Q^T and dP^T = V dO^T are recomputed, dS^T stays in
-// registers and feeds dQ^T += K^T dS^T as the B operand (K^T by transposed reads of the same K
-// tile). lse and delta are lane-local. No atomics, dQ written once in bf16.
-template <bool DROP>
-__global__ __launch_bounds__(FNT, 2) void attn_bwd_dq_kernel(const AttnBwdParams P) {
-  const AttnParams& p = P.f;
-  __shared__ __attribute__((aligned(16))) char smem[4 * kTileBytes];  // K[2], V[2]
-  auto Kl = [&](int buf) -> char* { return smem + buf * kTileBytes; };
-  auto Vl = [&](int buf) -> char* { return smem + (2 + buf) * kTileBytes; };
+// dQ: the forward's mapping (32 query rows per wave on the MFMA lane, 4 waves = 128 rows) over
+// 32-key K / V tiles through the ring; S^T / dP^T are recomputed and dS^T feeds dQ^T += K^T dS^T.
+// 24 MFMAs per tile and wave; two workgroups per CU (64 KiB LDS each). Masking: -inf in the S^T
+// accumulator's initial value on the diagonal / padding tiles.
+constexpr int Q2M = 128, Q2N = 32, Q2NT = 256, Q2NSLOT = 4;
+constexpr int Q2IMG = Q2N * D * 2;   // one 32-key image: 8 KiB
+constexpr int Q2SLOT = 2 * Q2IMG;    // K, V
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+template <bool DROP>
+__global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParams P) {
+  const AttnParams& p = P.f;
+  __shared__ __attribute__((aligned(16))) char smem[Q2NSLOT * Q2SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
   const int g = lane >> 4, l16 = lane & 15;
-  const int nqb = (p.Sq + FBM - 1) / FBM;
+  const int nqb = (p.Sq + Q2M - 1) / Q2M;
   const int BH = p.B * p.Hq;
-  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);
+  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) blocks first
   const int bh = blockIdx.x % BH;
   const int b = bh / p.Hq, hq = bh % p.Hq;
   const int hkv = hq / (p.Hq / p.Hkv);
   const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
   const int off = p.Sk - p.Sq;
-  const int q0 = qblk * FBM, qw0 = q0 + w * 32;
+  const int q0 = qblk * Q2M, qw0 = q0 + w * 32;
   const int myq = qw0 + l32;
   const bool qok = myq < p.Sq;
+  const int Sqp = sq_pad(p.Sq);
 
   const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + (int64_t)hq * p.q_hs;
   const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + (int64_t)hq * P.do_hs;
@@ -495,35 +601,52 @@ __global__ __launch_bounds__(FNT, 2) void attn_bwd_dq_kernel(const AttnBwdParams
       of[ks] = bf16x8{};
     }
   }
-  const int64_t ri = ((int64_t)b * p.Hq + hq) * p.Sq + (qok ? myq : 0);
-  const float lse2 = qok ? p.lse[ri] * kLog2e : INFINITY;
-  const float dlt = qok ? P.delta[ri] : 0.f;
+  const int64_t ri = (int64_t)bh * Sqp + min(myq, Sqp - 1);
+  const float lse2 = P.delta[(int64_t)BH * Sqp + ri];  // +inf on padding rows: p = 0
+  const float dlt = P.delta[ri];
   const float c = p.scale * kLog2e;
+  // per-lane mask: key kept iff key < sk and (non-causal or key <= myq + off)
+  const int klim = p.causal ? min(sk - 1, myq + off) : sk - 1;
+  // first key past which a tile needs the mask for some lane of this wave
+  const int kmask = p.causal ? min(sk, qw0 + off + 1) : sk;
 
   int kend = sk;
-  if (p.causal) kend = min(kend, q0 + FBM + off);
-  const int nt = kend > 0 ? (kend + FBN - 1) / FBN : 0;
+  if (p.causal) kend = min(kend, q0 + Q2M + off);
+  const int nt = kend > 0 ? (kend + Q2N - 1) / Q2N : 0;
 
-  bf16x8 kreg[4], vreg[4];
-  auto load_tile = [&](int t) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = tid + FNT * r, row = i / kChunks, ch = i % kChunks, key = t * FBN + row;
-      if (key < sk) {
-        kreg[r] = *reinterpret_cast<const bf16x8*>(K + (int64_t)key * p.k_ss + ch * 8);
-        vreg[r] = *reinterpret_cast<const bf16x8*>(Vg + (int64_t)key * p.v_ss + ch * 8);
-      } else {
-        kreg[r] = bf16x8{};
-        vreg[r] = bf16x8{};
-      }
-    }
+  // LDS-DMA of tile t into slot t % Q2NSLOT: wave w fills image rows 8w .. 8w+7 of K and V.
+  // Per-lane source offsets are fixed (row 8w + 4k + g, swizzled chunk); only the key base moves.
+  const uint32_t smem0 = lds_u32(smem);
+  const int row0 = 8 * w + g, row1 = row0 + 4;
+  const int ch0 = l16 ^ img_swz(row0), ch1 = l16 ^ img_swz(row1);
+  auto dma_tile = [&](int t, uint32_t slot_off) {
+    const int64_t k0r = min(t * Q2N + row0, p.Sk - 1), k1r = min(t * Q2N + row1, p.Sk - 1);  // past Sk: masked
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(8 * w * 256));
+    lds_dma16(K + k0r * p.k_ss + ch0 * 8, dst);
+    lds_dma16(Vg + k0r * p.v_ss + ch0 * 8, dst + Q2IMG);
+    lds_dma16(K + k1r * p.k_ss + ch1 * 8, dst + 1024);
+    lds_dma16(Vg + k1r * p.v_ss + ch1 * 8, dst + Q2IMG + 1024);
   };
-  auto store_tile = [&](int buf) {
+  auto wait_dma = [&](int pending_tiles) {  // 4 DMA instructions per tile
+    if (pending_tiles >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (pending_tiles == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // S^T and dP^T of tile t from slot SL; masked keys enter as -inf through the initial accumulator
+  auto sdp = [&](int t, auto slot_c, f32x16& s, f32x16& dp) {
+    constexpr int SL = decltype(slot_c)::value;
+    const char* ki = smem + SL * Q2SLOT;
+    const int kb = t * Q2N;
+    s = f32x16{};
+    if (kb + Q2N > kmask) {  // wave-uniform: the tile touches the diagonal / key padding
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = tid + FNT * r, row = i / kChunks, ch = i % kChunks;
-      *reinterpret_cast<bf16x8*>(Kl(buf) + img_off(row, ch)) = kreg[r];
-      *reinterpret_cast<bf16x8*>(Vl(buf) + img_off(row, ch)) = vreg[r];
+      for (int r = 0; r < 16; ++r) s[r] = kb + acc_row(r, h) <= klim ? 0.f : -INFINITY;
+    }
+    dp = f32x16{};
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      s = mfma32(lds_row_read(ki, l32, 2 * ks + h), qf[ks], s);
+      dp = mfma32(lds_row_read(ki + Q2IMG, l32, 2 * ks + h), of[ks], dp);
     }
   };
 
@@ -531,49 +654,55 @@ __global__ __launch_bounds__(FNT, 2) void attn_bwd_dq_kernel(const AttnBwdParams
 #pragma unroll
   for (int i = 0; i < 4; ++i) dq[i] = f32x16{};
 
-  if (nt > 0) { load_tile(0); store_tile(0); }
-  __syncthreads();
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    const int kb = t * FBN;
-    if (t + 1 < nt) load_tile(t + 1);
-    const bool skip = p.causal && (kb > qw0 + 31 + off);
-    if (!skip) {
-      const bool need_mask = (kb + FBN > sk) || (p.causal && kb + FBN - 1 > qw0 + off);
+  using I0 = std::integral_constant<int, 0>;
+  auto step = [&](int t, auto slot_c, f32x16& s_c, f32x16& dp_c, f32x16& s_n, f32x16& dp_n) {
+    constexpr int SL = decltype(slot_c)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (t + 1 < nt) wait_dma(min(nt, t + Q2NSLOT - 1) - (t + 2));
+    __builtin_amdgcn_s_barrier();
+    if (t + Q2NSLOT - 1 < nt) dma_tile(t + Q2NSLOT - 1, (uint32_t)(((SL + Q2NSLOT - 1) % Q2NSLOT) * Q2SLOT));
+
+    sdp(t + 1, std::integral_constant<int, (SL + 1) % Q2NSLOT>{}, s_n, dp_n);  // past the end: dropped
+
 #pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        f32x16 s = f32x16{}, dp = f32x16{};
+    for (int r = 0; r < 16; ++r) {
+      const float pv = fast_exp2(fmaf(s_c[r], c, -lse2));
+      const float z = DROP ? drop_factor(p, (uint32_t)bh, myq, t * Q2N + acc_row(r, h)) : 1.f;
+      s_c[r] = pv * (dp_c[r] * z - dlt);
+    }
+    const char* ki = smem + SL * Q2SLOT;
 #pragma unroll
-        for (int ks = 0; ks < D / 16; ++ks) {
-          s = mfma32(lds_row_read(Kl(cur), n * 32 + l32, 2 * ks + h), qf[ks], s);
-          dp = mfma32(lds_row_read(Vl(cur), n * 32 + l32, 2 * ks + h), of[ks], dp);
-        }
+    for (int stp = 0; stp < 2; ++stp) {
+      const bf16x8 sb = pack8(s_c, 8 * stp);
+      const int kk = 16 * stp + 4 * h;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          float pv = fast_exp2(s[r] * c - lse2);
-          const int key = kb + n * 32 + acc_row(r, h);
-          if (need_mask) {
-            if (key >= sk || (p.causal && key > myq + off)) pv = 0.f;
-          }
-          const float z = DROP ? drop_factor(p, (uint32_t)bh, myq, key) : 1.f;
-          s[r] = pv * (dp[r] * z - dlt);
-        }
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const bf16x8 sb = pack8(s, 8 * st);
-          const int kk = n * 32 + 16 * st + 4 * h;
-#pragma unroll
-          for (int db = 0; db < 4; ++db) {
-            const int c0 = db * 32 + (g & 1) * 16;
-            const bf16x8 a = cat(lds_tr_read(Kl(cur), kk, c0, l16), lds_tr_read(Kl(cur), kk + 8, c0, l16));
-            dq[db] = mfma32(a, sb, dq[db]);
-          }
-        }
+      for (int db = 0; db < 4; ++db) {
+        const int c0 = db * 32 + (g & 1) * 16;
+        const bf16x8 a = cat(lds_tr_read(ki, kk, c0, l16), lds_tr_read(ki, kk + 8, c0, l16));
+        dq[db] = mfma32(a, sb, dq[db]);
       }
     }
-    if (t + 1 < nt) store_tile(cur ^ 1);
-    __syncthreads();
+  };
+
+  if (nt > 0) {
+    const int pre = min(nt, Q2NSLOT - 1);
+    for (int t = 0; t < pre; ++t) dma_tile(t, (uint32_t)(t * Q2SLOT));
+    wait_dma(pre - 1);
+    __builtin_amdgcn_s_barrier();
+    f32x16 sA, dpA, sB, dpB;
+    sdp(0, I0{}, sA, dpA);
+    int t = 0;
+    for (; t + Q2NSLOT <= nt; t += Q2NSLOT) {  // one ring revolution: slots 0..3, register sets A/B
+      step(t, I0{}, sA, dpA, sB, dpB);
+      step(t + 1, std::integral_constant<int, 1>{}, sB, dpB, sA, dpA);
+      step(t + 2, std::integral_constant<int, 2>{}, sA, dpA, sB, dpB);
+      step(t + 3, std::integral_constant<int, 3>{}, sB, dpB, sA, dpA);
+    }
+    if (t < nt) step(t, I0{}, sA, dpA, sB, dpB);
+    if (t + 1 < nt) step(t + 1, std::integral_constant<int, 1>{}, sB, dpB, sA, dpA);
+    if (t + 2 < nt) step(t + 2, std::integral_constant<int, 2>{}, sA, dpA, sB, dpB);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   if (qok) {
     bf16* dQ = (bf16*)P.dq + (int64_t)b * P.dq_bs + (int64_t)hq * P.dq_hs + (int64_t)myq * P.dq_ss;
@@ -592,32 +721,28 @@ __global__ __launch_bounds__(FNT, 2) void attn_bwd_dq_kernel(const AttnBwdParams
 }  // namespace
 
 void attn_fwd(const AttnParams& p, hipStream_t s) {
-  const int nqb = (p.Sq + FBM - 1) / FBM;
-  const dim3 grid((unsigned)(nqb * p.B * p.Hq));
-  if (p.drop_thresh) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(FNT), 0, s, p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(FNT), 0, s, p);
+  const dim3 grid((unsigned)(((p.Sq + F3M - 1) / F3M) * p.B * p.Hq));
+  if (p.drop_thresh) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(F3NT), 0, s, p);
+  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(F3NT), 0, s, p);
 }
 
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
   (void)Dh;
-  return (int64_t)B * Hq * Sq;  // delta
+  return 2 * (int64_t)B * Hq * sq_pad(Sq);  // delta and lse2, rows padded to 32
 }
 
 void attn_bwd(const AttnBwdParams& p, hipStream_t s) {
-  const int64_t rows = (int64_t)p.f.B * p.f.Hq * p.f.Sq;
+  const int64_t rows = (int64_t)p.f.B * p.f.Hq * sq_pad(p.f.Sq);
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
-  const int nkb = (p.f.Sk + BBN - 1) / BBN;
-  const int nqb = (p.f.Sq + FBM - 1) / FBM;
+  const int nkb = (p.f.Sk + K2N - 1) / K2N;
+  const int nqb = (p.f.Sq + Q2M - 1) / Q2M;
   const dim3 g1((unsigned)(nkb * p.f.B * p.f.Hkv)), g2((unsigned)(nqb * p.f.B * p.f.Hq));
-  static const int nq = [] { const char* e = getenv("GRT_ATTN_BWD_NQ"); return e ? atoi(e) : 2; }();
   if (p.f.drop_thresh) {
-    if (nq == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 1>), g1, dim3(BNT), 0, s, p);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, 2>), g1, dim3(BNT), 0, s, p);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(FNT), 0, s, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(Q2NT), 0, s, p);
   } else {
-    if (nq == 1) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 1>), g1, dim3(BNT), 0, s, p);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, 2>), g1, dim3(BNT), 0, s, p);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(FNT), 0, s, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(K2NT), 0, s, p);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(Q2NT), 0, s, p);
   }
 }
 

@@ -23,9 +23,10 @@ from collections import defaultdict
 
 def short(name):
     n = name.replace("void ", "").replace("grt::(anonymous namespace)::", "")
-    m = re.match(r"_ZN3grt12_GLOBAL__N_1\d+(\w+?)I", n)
-    if m:
-        return m.group(1)
+    m = re.match(r"_ZN3grt12_GLOBAL__N_1\d+(\w+?)I(\w*?)EE", n)
+    if m:  # keep the template arguments (Lb0E = false, Lb1E = true, Li2E = 2) to tell variants apart
+        args = re.sub(r"L[bi](\d+)E?", r"\1,", m.group(2)).rstrip(",")
+        return f"{m.group(1)}<{args}>"
     return re.sub(r"\(.*", "", n)[:60]
 
 
