@@ -264,6 +264,61 @@ void dropout_bwd_seeded(const Tensor& dy, const Tensor& dx, double p, int64_t se
                    (uint64_t)seed, (uint64_t)offset, accumulate);
 }
 
+// ------------------------------------------------------------------ LoRA adapter
+// (h, xd) = lora_down(x [M, K], a [R, K]): h = (x * keep / (1-p)) a^T, xd = x * keep / (1-p) when
+// want_xd (same keep mask as dropout_fwd_seeded(x, p, seed, offset)). Returns {} when the shape is
+// not supported by the kernel (the caller falls back to the torch path).
+std::vector<Tensor> lora_down(const Tensor& x, const Tensor& a, double p, int64_t seed, int64_t offset,
+                              bool want_xd) {
+  check_cuda(x, "x");
+  check_contig(a, "a");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && a.dim() == 2 && a.size(1) == x.size(1), "lora_down: shapes");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && a.scalar_type() == at::kBFloat16, "lora_down: bf16");
+  check_drop_p(p);
+  const int64_t M = x.size(0);
+  const int K = (int)x.size(1), R = (int)a.size(0);
+  if (!grt::lora_down_supported(M, K, R, (int)x.stride(0), (uint64_t)offset) ||
+      reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 || reinterpret_cast<uintptr_t>(a.data_ptr()) % 16)
+    return {};
+  c10::OptionalDeviceGuard g(x.device());
+  auto h = at::empty({M, R}, x.options());
+  Tensor xd;
+  if (want_xd) xd = at::empty({M, K}, x.options());
+  grt::LoraDownParams lp{};
+  lp.x = x.data_ptr(); lp.a = a.data_ptr(); lp.h = h.data_ptr(); lp.xd = want_xd ? xd.data_ptr() : nullptr;
+  lp.M = M; lp.K = K; lp.R = R; lp.ldx = (int)x.stride(0);
+  lp.p = (float)p; lp.seed = (uint64_t)seed; lp.offset = (uint64_t)offset;
+  grt::lora_down(lp, cur_stream(x));
+  if (want_xd) return {h, xd};
+  return {h};
+}
+
+// dx [M, K] (+)= keep / (1-p) * (g [M, R] @ at^T), at = A^T [K, R]; returns false (nothing done)
+// when the shape is not supported by the kernel.
+bool lora_dx(const Tensor& g, const Tensor& at, const Tensor& dx, double p, int64_t seed, int64_t offset,
+             bool accumulate) {
+  check_contig(g, "g");
+  check_contig(at, "at");
+  check_contig(dx, "dx");
+  TORCH_CHECK(g.dim() == 2 && at.dim() == 2 && dx.dim() == 2 && g.size(0) == dx.size(0) &&
+                  at.size(0) == dx.size(1) && at.size(1) == g.size(1), "lora_dx: shapes");
+  TORCH_CHECK(g.scalar_type() == at::kBFloat16 && at.scalar_type() == at::kBFloat16 &&
+                  dx.scalar_type() == at::kBFloat16, "lora_dx: bf16");
+  check_drop_p(p);
+  const int64_t M = dx.size(0);
+  const int K = (int)dx.size(1), R = (int)g.size(1);
+  if (!grt::lora_dx_supported(M, K, R, (uint64_t)offset) || reinterpret_cast<uintptr_t>(dx.data_ptr()) % 16 ||
+      reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 || reinterpret_cast<uintptr_t>(at.data_ptr()) % 16)
+    return false;
+  c10::OptionalDeviceGuard dg(dx.device());
+  grt::LoraDxParams lp{};
+  lp.g = g.data_ptr(); lp.at = at.data_ptr(); lp.dx = dx.data_ptr();
+  lp.M = M; lp.K = K; lp.R = R;
+  lp.p = (float)p; lp.seed = (uint64_t)seed; lp.offset = (uint64_t)offset; lp.accumulate = accumulate ? 1 : 0;
+  grt::lora_dx(lp, cur_stream(dx));
+  return true;
+}
+
 // ------------------------------------------------------------------ cross entropy
 std::vector<Tensor> ce_fwd(const Tensor& logits, const Tensor& labels, int64_t ignore_index) {
   check_cuda(logits, "logits");
@@ -707,6 +762,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("dropout_fwd_seeded", &dropout_fwd_seeded);
+  m.def("lora_down", &lora_down);
+  m.def("lora_dx", &lora_dx);
   m.def("dropout_bwd_seeded", &dropout_bwd_seeded);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

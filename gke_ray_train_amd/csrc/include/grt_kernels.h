@@ -81,6 +81,25 @@ void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v
 // Scale in place: x *= a (device scalar pointer or host value when a_ptr == null).
 void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s);
 
+// ---------------- LoRA adapter (lora.hip) ----------------
+// h[M][R] = (x ⊙ keep/(1-p)) · A^T, A [R][K]; keep = the element-dropout hash of x's element index
+// (offset + row*K + col, as dropout_fwd_seeded); xd (optional) receives x ⊙ keep/(1-p).
+struct LoraDownParams {
+  const void* x; const void* a; void* h; void* xd;
+  int64_t M; int K; int R; int ldx;
+  float p; uint64_t seed; uint64_t offset;
+};
+bool lora_down_supported(int64_t M, int K, int R, int ldx, uint64_t offset);
+void lora_down(const LoraDownParams& p, hipStream_t s);
+// dX[M][K] (+)= keep/(1-p) ⊙ (g[M][R] · A[R][K]), given A^T = at [K][R] (same keep mask as lora_down)
+struct LoraDxParams {
+  const void* g; const void* at; void* dx;
+  int64_t M; int K; int R;
+  float p; uint64_t seed; uint64_t offset; int accumulate;
+};
+bool lora_dx_supported(int64_t M, int K, int R, uint64_t offset);
+void lora_dx(const LoraDxParams& p, hipStream_t s);
+
 // ---------------- attention (attention.hip) ----------------
 struct AttnParams {
   const void* q; const void* k; const void* v; void* o; float* lse;

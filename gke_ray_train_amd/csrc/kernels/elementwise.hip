@@ -184,25 +184,7 @@ __global__ __launch_bounds__(kNT) void scale_add_pe_kernel(const T* __restrict__
 }
 
 // ------------------------------- dropout -------------------------------------
-__device__ __forceinline__ uint64_t hash_u64(uint64_t x) {
-  // splitmix64 finaliser: counter-based, stateless, graph-replay safe (seed/offset are args)
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
-// The keep decision of element idx is a pure function of (seed, idx), so a backward regenerates
-// it instead of reading a stored mask: 16 bits of hash(key ^ (idx / 4)) against p in 1/65536
-// units, key = hash(seed) (all 64 seed bits matter; computed once per thread). One hash per 4
-// elements: the 64-bit multiplies of the hash are emulated with 32-bit ones on CDNA, and one hash
-// per element made the kernel VALU-bound; per group it streams at memory speed. Keep probability
-// 1 - round(p * 65536) / 65536. ops/_ref.py::dropout_keep_mask is the host reimplementation.
-__device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 65536.0f + 0.5f); }
-__device__ __forceinline__ bool drop_keep(uint64_t key, uint64_t idx, uint32_t thr) {
-  const uint64_t h = hash_u64(key ^ (idx >> 2));
-  return ((uint32_t)(h >> (16 * (idx & 3))) & 0xffffu) >= thr;
-}
+// keep-mask hash (hash_u64 / drop_thr / drop_keep): grt_common.h, shared with lora.hip
 // V consecutive decisions from idx0; one hash per 4 elements when idx0 is 4-aligned
 template <int V>
 __device__ __forceinline__ void drop_keep_vec(uint64_t key, uint64_t idx0, uint32_t thr, bool (&keep)[V]) {

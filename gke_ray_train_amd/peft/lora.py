@@ -57,6 +57,11 @@ class LoraConfig:
         return d
 
 
+# LoRA adapter kernels (csrc/kernels/lora.hip): dropout + down-projection in one pass over x, and
+# the adapter's dX contribution accumulated in one pass over dX. GRT_LORA_KERNELS=0 -> torch path.
+_LORA_KERNELS = os.environ.get("GRT_LORA_KERNELS", "1") != "0"
+
+
 def _base_weight(base: nn.Module) -> torch.Tensor:
     return base.dequantize() if isinstance(base, NF4Linear) else base.weight
 
@@ -85,9 +90,15 @@ class _LoraFn(torch.autograd.Function):
         bias = getattr(base, "bias", None)
         y = F.linear(x2, w, bias)
         del w
-        xd = C.dropout_fwd_seeded(x2, p, seed, offset) if p > 0 else x2
         acat = torch.cat(As, 0) if k > 1 else As[0]
-        h = xd @ acat.t()                                   # [M, r * k]
+        # h = dropout(x) A^T in one pass over x (lora.hip); x_d is kept for the dA GEMM
+        res = C.lora_down(x2, acat, p, seed, offset, p > 0) if _LORA_KERNELS else []
+        if res:
+            h = res[0]
+            xd = res[1] if p > 0 else x2
+        else:
+            xd = C.dropout_fwd_seeded(x2, p, seed, offset) if p > 0 else x2
+            h = xd @ acat.t()                               # [M, r * k]
         for i, (off, n) in enumerate(spec):                 # GEMM epilogue accumulates into y
             y[:, off:off + n].addmm_(h[:, i * r:(i + 1) * r], Bs[i].t(), alpha=scaling)
         ctx.base, ctx.spec, ctx.r, ctx.scaling, ctx.p, ctx.seed, ctx.offset = base, spec, r, scaling, p, seed, offset
@@ -114,10 +125,12 @@ class _LoraFn(torch.autograd.Function):
         g = torch.cat(gs, 1) if len(gs) > 1 else gs[0]       # [M, r * k]
         dacat = g.t() @ xd                                   # [r * k, in]
         if dx is not None:
-            if ctx.p > 0:
-                C.dropout_bwd_seeded(g @ acat, dx, ctx.p, ctx.seed, ctx.offset, True)  # dx += drop'(g A)
-            else:
-                dx.addmm_(g, acat)
+            # dx += drop'(g A): one read-modify-write of dx (lora.hip), else GEMM + dropout backward
+            if not (_LORA_KERNELS and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
+                if ctx.p > 0:
+                    C.dropout_bwd_seeded(g @ acat, dx, ctx.p, ctx.seed, ctx.offset, True)
+                else:
+                    dx.addmm_(g, acat)
             dx = dx.view(ctx.xshape)
         dAs = [dacat[i * r:(i + 1) * r] for i in range(len(spec))]
         return (dx, None, None, None, None, None, None, None, *dAs, *dBs)

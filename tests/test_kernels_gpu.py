@@ -527,6 +527,49 @@ def test_fused_lora_matches_reference(nf4, p, targets):
             assert rel < 2e-2, f"lora {what} {n}: rel err {rel.item():.3g}"
 
 
+@pytest.mark.parametrize("M,K,R,p,offset,strided", [
+    (256, 256, 32, 0.0, 0, False), (200, 512, 64, 0.1, 0, False), (77, 1024, 192, 0.1, 8, True),
+    (1024, 4096, 128, 0.1, 0, False), (33, 128, 256, 0.5, 4, False)])
+def test_lora_down_kernel(M, K, R, p, offset, strided):
+    """lora.hip lora_down: h = drop(x) A^T (mask = the host hash, ops/_ref.py) and the x_d side output."""
+    from gke_ray_train_amd.ops import _ref
+    C = _C()
+    torch.manual_seed(1)
+    xs = torch.randn(M, K + (64 if strided else 0), device=DEV, dtype=torch.bfloat16)
+    x = xs[:, :K]
+    a = (torch.randn(R, K, device=DEV) / math.sqrt(K)).to(torch.bfloat16)
+    seed = 0x1234_5678_9abc
+    res = C.lora_down(x, a, p, seed, offset, True)
+    assert len(res) == 2, "kernel path not taken"
+    h, xd = res
+    keep = _ref.dropout_keep_mask(seed, offset, M * K, p).to(DEV).view(M, K).float() if p > 0 else 1.0
+    xr = x.float() * keep / (1 - p)
+    _close(xd, xr, 1e-2, 1e-2, "lora_down xd")
+    _close(h, xr @ a.float().t(), 2e-2, 2e-2, "lora_down h")
+    assert len(C.lora_down(x, a, p, seed, offset, False)) == 1
+    assert C.lora_down(x[:, :K - 32], a[:, :K - 32].contiguous(), p, seed, offset, True) == []  # K % 64
+
+
+@pytest.mark.parametrize("M,K,R,p,offset,acc", [
+    (256, 256, 32, 0.0, 0, True), (200, 512, 48, 0.1, 0, True), (77, 1024, 192, 0.1, 8, False),
+    (1024, 4096, 128, 0.1, 0, True), (65, 128, 256, 0.5, 4, True), (100, 384, 16, 0.1, 0, True)])
+def test_lora_dx_kernel(M, K, R, p, offset, acc):
+    """lora.hip lora_dx: dx (+)= keep/(1-p) * (g A), A^T given as [K, R]."""
+    from gke_ray_train_amd.ops import _ref
+    C = _C()
+    torch.manual_seed(2)
+    g = torch.randn(M, R, device=DEV, dtype=torch.bfloat16)
+    a = (torch.randn(R, K, device=DEV) / math.sqrt(R)).to(torch.bfloat16)
+    dx = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+    dx0 = dx.float().clone()
+    seed = 987654321
+    assert C.lora_dx(g, a.t().contiguous(), dx, p, seed, offset, acc), "kernel path not taken"
+    keep = _ref.dropout_keep_mask(seed, offset, M * K, p).to(DEV).view(M, K).float() if p > 0 else 1.0
+    ref = (g.float() @ a.float()) * keep / (1 - p) + (dx0 if acc else 0)
+    _close(dx, ref, 2e-2, 2e-2, "lora_dx")
+    assert not C.lora_dx(g, a.t().contiguous()[:64].contiguous(), dx[:, :64].contiguous(), p, seed, offset, acc)
+
+
 def test_transpose_and_nf4_dequant_t():
     """HIP transpose and transposing NF4 dequant match torch exactly."""
     from gke_ray_train_amd import ops

@@ -16,8 +16,9 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--out", default="gpurun_out/tunableop_lora.csv")
 ap.add_argument("--model", default="llama2-7b")
 ap.add_argument("--peft", default="lora", choices=["lora", "qlora"])
-ap.add_argument("--tokens", type=int, default=8192)
-ap.add_argument("--seq", type=int, default=1024)
+ap.add_argument("--rows", type=int, default=8, help="sequences per step (SFT: batch 2 x accumulation 4 fused)")
+ap.add_argument("--seqs", default="1024", help="padded sequence lengths to tune at (M = rows x seq)")
+ap.add_argument("--duration", type=int, default=20, help="max tuning ms per shape")
 a = ap.parse_args()
 
 from gke_ray_train_amd.models import build_llama, get_config  # noqa: E402
@@ -28,7 +29,7 @@ tun = torch.cuda.tunable
 tun.enable(True)
 tun.read_file(str(RESULTS))
 tun.tuning_enable(True)
-tun.set_max_tuning_duration(20)
+tun.set_max_tuning_duration(a.duration)
 tun.set_max_tuning_iterations(30)
 os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
 tun.set_filename(a.out)
@@ -40,14 +41,14 @@ if a.peft == "qlora":
     quantize_model_(model, BitsAndBytesConfig(bnb_4bit_compute_dtype=torch.bfloat16))
 pm = get_peft_model(model, LoraConfig(r=64, lora_alpha=16, lora_dropout=0.1))
 ddp = DistributedDataParallel(pm)
-ids = torch.randint(0, cfg.vocab_size, (a.tokens // a.seq, a.seq), device=dev)
-for i in range(2):
+for L in [int(x) for x in a.seqs.split(",")]:
+    ids = torch.randint(0, cfg.vocab_size, (a.rows, L), device=dev)
     loss = pm(ids, labels=ids)["loss"]
     loss.backward()
     ddp.finish_gradient_sync()
     ddp.zero_grad()
     torch.cuda.synchronize()
-    print(f"pass {i} done", flush=True)
+    print(f"M = {a.rows * L} tuned", flush=True)
 tun.tuning_enable(False)
 with open(a.out, "w") as fh:
     for k, v in tun.get_validators():
