@@ -58,8 +58,11 @@ class LoraConfig:
 
 
 # LoRA adapter kernels (csrc/kernels/lora.hip): dropout + down-projection in one pass over x, and
-# the adapter's dX contribution accumulated in one pass over dX. GRT_LORA_KERNELS=0 -> torch path.
-_LORA_KERNELS = os.environ.get("GRT_LORA_KERNELS", "1") != "0"
+# the adapter's dX contribution accumulated in one pass over dX. GRT_LORA_KERNELS=0 -> torch path
+# (=down / =dx: only that kernel).
+_LORA_KERNELS_ENV = os.environ.get("GRT_LORA_KERNELS", "1")
+_LORA_DOWN = _LORA_KERNELS_ENV in ("1", "down")
+_LORA_DX = _LORA_KERNELS_ENV in ("1", "dx")
 
 
 def _base_weight(base: nn.Module) -> torch.Tensor:
@@ -92,7 +95,7 @@ class _LoraFn(torch.autograd.Function):
         del w
         acat = torch.cat(As, 0) if k > 1 else As[0]
         # h = dropout(x) A^T in one pass over x (lora.hip); x_d is kept for the dA GEMM
-        res = C.lora_down(x2, acat, p, seed, offset, p > 0) if _LORA_KERNELS else []
+        res = C.lora_down(x2, acat, p, seed, offset, p > 0) if _LORA_DOWN else []
         if res:
             h = res[0]
             xd = res[1] if p > 0 else x2
@@ -126,7 +129,7 @@ class _LoraFn(torch.autograd.Function):
         dacat = g.t() @ xd                                   # [r * k, in]
         if dx is not None:
             # dx += drop'(g A): one read-modify-write of dx (lora.hip), else GEMM + dropout backward
-            if not (_LORA_KERNELS and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
+            if not (_LORA_DX and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
                 if ctx.p > 0:
                     C.dropout_bwd_seeded(g @ acat, dx, ctx.p, ctx.seed, ctx.offset, True)
                 else:

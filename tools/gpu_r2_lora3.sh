@@ -1,0 +1,11 @@
+#!/bin/bash
+# LoRA kernels v2: numerics, LoRA bench A/B, kernel-time profile
+set -o pipefail
+export TMPDIR=/tmp
+O=gpurun_out/r2lora3
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_kernels_gpu.py \
+  -k "lora" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+bash tools/gpu_ab_env.sh r2lora3/ab "GRT_LORA_KERNELS=0" "GRT_LORA_KERNELS=1" 2 --peft lora || exit 1
+bash tools/gpu_prof_bench.sh r2lora3/prof --peft lora
