@@ -14,13 +14,12 @@
 //               targets); the dropout keep-mask is the element-dropout hash of x's element index
 //               (grt_common.h drop_keep, the same mask dropout_fwd/bwd_seeded use), applied in
 //               registers; x_d is optionally written as a side output (the dA GEMM reads it).
-//               MFMA D[R][token] = A · x_d^T: one wave = 32 tokens x R, the workgroup's four waves
-//               split K and reduce through LDS. Grid = tokens / 32 (256 workgroups at 8192 tokens).
-//   lora_dx:    dX[M][K] (+)= keep / (1-p) ⊙ (g[M][R] · A[R][K]) from A^T = [K][R]: MFMA
-//               D[k][token] = A^T · g^T over R, epilogue applies the mask and accumulates into dX
-//               with 8-byte row chunks — one read-modify-write of dX, no temporary.
-// v_mfma_f32_32x32x16_bf16 throughout; operands are 16-byte row fragments loaded straight from
-// global memory (A / A^T / g are small and L2-resident; x is streamed once).
+//   lora_dx:    dX[M][K] (+)= keep / (1-p) ⊙ (g[M][R] · A[R][K]) from A^T = [K][R] — one
+//               read-modify-write of dX, no [M][K] temporary.
+// v_mfma_f32_32x32x16_bf16 throughout. Every global access is a full-row coalesced 16 B/lane load
+// or store; MFMA fragments are read from padded LDS images (a first version loaded the fragments
+// straight from global memory — 32 rows x 32 B per instruction, address-unit bound, 2-4x slower:
+// profiles/r2_perf_experiments.md).
 #include "grt_common.h"
 #include "grt_kernels.h"
 
@@ -42,51 +41,122 @@ __device__ __forceinline__ void keep8(uint64_t key, uint64_t idx0, uint32_t thr,
   }
 }
 
+// ---- lora_down: 32 tokens per workgroup, K streamed in 128-column chunks. x: each thread loads 32 B
+// of one row per chunk (8 threads cover a row's 256 B: coalesced), LD_PF chunks in flight in a
+// register ring; the mask is applied in registers, x_d is stored from them (coalesced 16 B stores).
+// A's [R][128] chunk is loaded coalesced one chunk ahead in registers. Both go to double-buffered
+// LDS images (one barrier per chunk) from which each wave feeds two 16-wide k-steps of MFMAs
+// D[R row][token] = A · x_d^T. (MFMA fragments straight from global memory touch 32 rows x 32 B
+// per instruction — address-unit bound; the LDS images make every global access a full row.)
+constexpr int LD_KC = 128;          // K chunk
+constexpr int LD_XS = LD_KC + 8;    // LDS row (bf16): +16 B so b128 fragment reads of 32 rows spread over banks
+constexpr int LD_PF = 4;            // x chunks in flight per thread
+
+__device__ __forceinline__ void drop8(bf16x8& v, uint64_t key, uint64_t idx0, uint32_t thr, float sc) {
+  bool kp[8];
+  keep8(key, idx0, thr, kp);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = static_cast<bf16>(kp[e] ? static_cast<float>(v[e]) * sc : 0.f);
+}
+
+template <int RB>
+constexpr int lora_down_lds_bytes() {
+  return 2 * 32 * LD_XS * 2 + 2 * 32 * RB * LD_XS * 2;  // x images + A images (the reduction aliases A)
+}
+
 template <int RB>  // R = 32 * RB
 __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) {
   constexpr int R = 32 * RB;
-  __shared__ float red[3][RB * 16 * 64];  // waves 1-3 park their partial accumulators
+  constexpr int AIMG = R * LD_XS;  // elements per A image
+  static_assert(3 * RB * 16 * 64 * 4 <= 2 * AIMG * 2, "reduction scratch must fit in the A images");
+  __shared__ __attribute__((aligned(16))) char smem[lora_down_lds_bytes<RB>()];
+  bf16* xs = reinterpret_cast<bf16*>(smem);                       // [2][32][LD_XS]
+  bf16* as = reinterpret_cast<bf16*>(smem + 2 * 32 * LD_XS * 2);  // [2][R][LD_XS]
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t t0 = (int64_t)blockIdx.x * 32;
-  const int64_t tok = t0 + l32;
-  const bool tok_ok = tok < P.M;
-  const bf16* xrow = static_cast<const bf16*>(P.x) + (tok_ok ? tok : P.M - 1) * (int64_t)P.ldx;
-  const int kq = P.K / 4, kbeg = w * kq;
+  const int lr = tid >> 3, lc = (tid & 7) * 16;  // x loader: row, first of 16 columns
+  const int64_t ltok = t0 + lr;
+  const bool lok = ltok < P.M;
+  const bf16* src = static_cast<const bf16*>(P.x) + (lok ? ltok : P.M - 1) * (int64_t)P.ldx + lc;
+  bf16* xdst = (P.xd != nullptr && lok) ? static_cast<bf16*>(P.xd) + ltok * (int64_t)P.K + lc : nullptr;
+  const int ar = tid >> 4, ac = (tid & 15) * 8;  // A loader: rows ar + 16 j, 8 columns from ac
+  const bf16* asrc = static_cast<const bf16*>(P.a) + (int64_t)ar * P.K + ac;
+  const int nch = P.K / LD_KC;
   const bool drop = P.p > 0.f;
   const uint32_t thr = drop_thr(P.p);
   const float sc = drop ? 1.f / (1.f - P.p) : 1.f;
   const uint64_t key = hash_u64(P.seed);
-  const uint64_t eidx = P.offset + (uint64_t)tok * (uint64_t)P.K;  // element index of x[tok][0]
+  const uint64_t eidx = P.offset + (uint64_t)ltok * (uint64_t)P.K + lc;  // element index of x[ltok][lc]
 
+  bf16x8 ring[LD_PF][2];
+#pragma unroll
+  for (int i = 0; i < LD_PF; ++i)
+    if (i < nch) {
+      ring[i][0] = *reinterpret_cast<const bf16x8*>(src + i * LD_KC);
+      ring[i][1] = *reinterpret_cast<const bf16x8*>(src + i * LD_KC + 8);
+    }
+  bf16x8 areg[2 * RB];
+#pragma unroll
+  for (int j = 0; j < 2 * RB; ++j) areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * 16 * P.K);
   f32x16 acc[RB];
 #pragma unroll
   for (int i = 0; i < RB; ++i) acc[i] = f32x16{};
-  for (int k = kbeg; k < kbeg + kq; k += 16) {
-    const int kk = k + 8 * h;
-    bf16x8 xf = *reinterpret_cast<const bf16x8*>(xrow + kk);
-    if (drop) {
-      bool kp[8];
-      keep8(key, eidx + (uint64_t)kk, thr, kp);
+  for (int c0 = 0; c0 < nch; c0 += LD_PF) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) xf[e] = static_cast<bf16>(kp[e] ? static_cast<float>(xf[e]) * sc : 0.f);
-    }
-    if (P.xd != nullptr && tok_ok) *reinterpret_cast<bf16x8*>(static_cast<bf16*>(P.xd) + tok * (int64_t)P.K + kk) = xf;
+    for (int i = 0; i < LD_PF; ++i) {
+      const int c = c0 + i;
+      if (c < nch) {  // block-uniform
+        bf16x8 v0 = ring[i][0], v1 = ring[i][1];
+        if (c + LD_PF < nch) {
+          ring[i][0] = *reinterpret_cast<const bf16x8*>(src + (c + LD_PF) * LD_KC);
+          ring[i][1] = *reinterpret_cast<const bf16x8*>(src + (c + LD_PF) * LD_KC + 8);
+        }
+        // buffer c & 1 (c0 is a multiple of LD_PF); the previous reader of this buffer was chunk
+        // c - 2, which every wave finished before the barrier of chunk c - 1
+        bf16* xt = xs + (i & 1) * 32 * LD_XS;
+        bf16* at = as + (i & 1) * AIMG;
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) {
-      const bf16x8 af = *reinterpret_cast<const bf16x8*>(static_cast<const bf16*>(P.a) + (int64_t)(rb * 32 + l32) * P.K + kk);
-      acc[rb] = mfma32x32x16(af, xf, acc[rb]);  // D[R row][token]
+        for (int j = 0; j < 2 * RB; ++j) *reinterpret_cast<bf16x8*>(at + (ar + 16 * j) * LD_XS + ac) = areg[j];
+        if (c + 1 < nch) {
+#pragma unroll
+          for (int j = 0; j < 2 * RB; ++j)
+            areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * 16 * P.K + (c + 1) * LD_KC);
+        }
+        if (drop) {
+          drop8(v0, key, eidx + (uint64_t)c * LD_KC, thr, sc);
+          drop8(v1, key, eidx + (uint64_t)c * LD_KC + 8, thr, sc);
+        }
+        if (xdst != nullptr) {
+          *reinterpret_cast<bf16x8*>(xdst + c * LD_KC) = v0;
+          *reinterpret_cast<bf16x8*>(xdst + c * LD_KC + 8) = v1;
+        }
+        *reinterpret_cast<bf16x8*>(xt + lr * LD_XS + lc) = v0;
+        *reinterpret_cast<bf16x8*>(xt + lr * LD_XS + lc + 8) = v1;
+        __syncthreads();
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          const int kk = (2 * w + s2) * 16 + 8 * h;
+          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xt + l32 * LD_XS + kk);
+#pragma unroll
+          for (int rb = 0; rb < RB; ++rb)
+            acc[rb] = mfma32x32x16(*reinterpret_cast<const bf16x8*>(at + (rb * 32 + l32) * LD_XS + kk), xf, acc[rb]);
+        }
+      }
     }
   }
-  // reduce the four K quarters: waves 1-3 -> LDS, wave 0 sums and stores
+  // reduce the four waves' k-step partial sums: waves 1-3 -> LDS (over the A images), wave 0 sums
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(as);  // [3][RB * 16 * 64]
   if (w > 0) {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[w - 1][(rb * 16 + r) * 64 + lane] = acc[rb][r];
+      for (int r = 0; r < 16; ++r) red[(w - 1) * RB * 1024 + (rb * 16 + r) * 64 + lane] = acc[rb][r];
   }
   __syncthreads();
-  if (w == 0 && tok_ok) {
+  const int64_t tok = t0 + l32;
+  if (w == 0 && tok < P.M) {
     bf16* hrow = static_cast<bf16*>(P.h) + tok * (int64_t)R;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -95,76 +165,113 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
         bf16x4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int r = 4 * q + j, ix = (rb * 16 + r) * 64 + lane;
-          v[j] = static_cast<bf16>(acc[rb][r] + red[0][ix] + red[1][ix] + red[2][ix]);
+          const int ix = (rb * 16 + 4 * q + j) * 64 + lane;
+          v[j] = static_cast<bf16>(acc[rb][4 * q + j] + red[ix] + red[RB * 1024 + ix] + red[2 * RB * 1024 + ix]);
         }
         *reinterpret_cast<bf16x4*>(hrow + rb * 32 + 8 * q + 4 * h) = v;
       }
   }
 }
 
+// ---- lora_dx: one workgroup = 64 tokens x 128 columns of dX. The dX tile's 16 B chunks are loaded
+// first (coalesced, in flight during the rest); g [64][R] and A^T [128][R] are loaded with full-row
+// coalesced loads into padded LDS images; each wave computes a 32-token x 64-column block
+// D[k][token] = A^T · g^T over R from them, parks it in a padded fp32 LDS tile (over the images),
+// and every thread then finishes four 8-column chunks: mask, scale, add, 16 B store.
+constexpr int DX_TS = 132;  // fp32 tile row: 128 + 4 so the f32x4 writes of 32 rows spread over banks
+
+template <int RS>
+constexpr int lora_dx_lds_bytes() {
+  return (192 * (16 * RS + 8) * 2) > (64 * DX_TS * 4) ? (192 * (16 * RS + 8) * 2) : (64 * DX_TS * 4);
+}
+
 template <int RS>  // R = 16 * RS
 __global__ __launch_bounds__(256) void lora_dx_kernel(const LoraDxParams P) {
+  constexpr int R = 16 * RS, RP = R + 8;  // padded image row (bf16)
+  __shared__ __attribute__((aligned(16))) char smem[lora_dx_lds_bytes<RS>()];
+  bf16* gimg = reinterpret_cast<bf16*>(smem);  // [64][RP]
+  bf16* aimg = gimg + 64 * RP;                 // [128][RP]
+  float* tile = reinterpret_cast<float*>(smem);  // [64][DX_TS], after the images are consumed
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nkb = P.K / 128;
   const int64_t tb = blockIdx.x / nkb;
   const int kb = blockIdx.x % nkb;
-  const int64_t t0 = tb * 64 + (w & 1) * 32;
-  const int c0 = kb * 128 + (w >> 1) * 64;
-  const int64_t tok = t0 + l32;
-  const bool tok_ok = tok < P.M;
-  const bf16* grow = static_cast<const bf16*>(P.g) + (tok_ok ? tok : P.M - 1) * (int64_t)(16 * RS);
-  bf16x8 gf[RS];
+  bf16* dx = static_cast<bf16*>(P.dx);
+  bf16x8 old[4];
 #pragma unroll
-  for (int s = 0; s < RS; ++s) gf[s] = *reinterpret_cast<const bf16x8*>(grow + 16 * s + 8 * h);
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, row = c >> 4, col = (c & 15) * 8;
+    const int64_t tok = tb * 64 + row;
+    old[i] = bf16x8{};
+    if (P.accumulate && tok < P.M) old[i] = *reinterpret_cast<const bf16x8*>(dx + tok * (int64_t)P.K + kb * 128 + col);
+  }
+  // images: R / 8 chunks of 16 B per row
+  constexpr int CPR = R / 8;
+  const bf16* g = static_cast<const bf16*>(P.g);
+  const bf16* at = static_cast<const bf16*>(P.at) + (int64_t)kb * 128 * R;
+#pragma unroll
+  for (int c = tid; c < 64 * CPR; c += 256) {
+    const int row = c / CPR, col = (c % CPR) * 8;
+    const int64_t tok = tb * 64 + row;
+    *reinterpret_cast<bf16x8*>(gimg + row * RP + col) =
+        *reinterpret_cast<const bf16x8*>(g + (tok < P.M ? tok : P.M - 1) * (int64_t)R + col);
+  }
+#pragma unroll
+  for (int c = tid; c < 128 * CPR; c += 256) {
+    const int row = c / CPR, col = (c % CPR) * 8;
+    *reinterpret_cast<bf16x8*>(aimg + row * RP + col) = *reinterpret_cast<const bf16x8*>(at + (int64_t)row * R + col);
+  }
+  __syncthreads();
+  const int tl = (w & 1) * 32 + l32;  // this lane's token row within the tile (MFMA B operand)
+  f32x16 acc[2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int kl = (w >> 1) * 64 + cb * 32;  // column block within the tile
+    acc[cb] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < RS; ++s)
+      acc[cb] = mfma32x32x16(*reinterpret_cast<const bf16x8*>(aimg + (kl + l32) * RP + 16 * s + 8 * h),
+                             *reinterpret_cast<const bf16x8*>(gimg + tl * RP + 16 * s + 8 * h), acc[cb]);  // D[k][token]
+  }
+  __syncthreads();  // images consumed; the fp32 tile reuses the space
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int kl = (w >> 1) * 64 + cb * 32;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      *reinterpret_cast<f32x4*>(&tile[tl * DX_TS + kl + 8 * q + 4 * h]) =
+          f32x4{acc[cb][4 * q], acc[cb][4 * q + 1], acc[cb][4 * q + 2], acc[cb][4 * q + 3]};
+  }
+  __syncthreads();
   const bool drop = P.p > 0.f;
   const uint32_t thr = drop_thr(P.p);
   const float sc = drop ? 1.f / (1.f - P.p) : 1.f;
   const uint64_t key = hash_u64(P.seed);
-  const uint64_t eidx = P.offset + (uint64_t)tok * (uint64_t)P.K;
-  bf16* dxrow = static_cast<bf16*>(P.dx) + tok * (int64_t)P.K;
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    const int cc = c0 + cb * 32;
-    f32x16 acc = f32x16{};
-    const bf16* arow = static_cast<const bf16*>(P.at) + (int64_t)(cc + l32) * (16 * RS);
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i, row = c >> 4, col = (c & 15) * 8;
+    const int64_t t = tb * 64 + row;
+    if (t >= P.M) continue;
+    const f32x4 a0 = *reinterpret_cast<const f32x4*>(&tile[row * DX_TS + col]);
+    const f32x4 a1 = *reinterpret_cast<const f32x4*>(&tile[row * DX_TS + col + 4]);
+    const float d[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+    bool kp[8];
+    if (drop) keep8(key, P.offset + (uint64_t)t * (uint64_t)P.K + kb * 128 + col, thr, kp);
+    bf16x8 o;
 #pragma unroll
-    for (int s = 0; s < RS; ++s)
-      acc = mfma32x32x16(*reinterpret_cast<const bf16x8*>(arow + 16 * s + 8 * h), gf[s], acc);  // D[k][token]
-    if (tok_ok) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int kc = cc + 8 * q + 4 * h;  // 4 consecutive columns kc .. kc+3 (4-aligned)
-        float d[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d[j] = acc[4 * q + j] * sc;
-        if (drop) {
-          const uint64_t hv = hash_u64(key ^ ((eidx + (uint64_t)kc) >> 2));
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (((uint32_t)(hv >> (16 * j)) & 0xffffu) < thr) d[j] = 0.f;
-        }
-        bf16x4* dst = reinterpret_cast<bf16x4*>(dxrow + kc);
-        bf16x4 o;
-        if (P.accumulate) {
-          const bf16x4 old = *dst;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = static_cast<bf16>(static_cast<float>(old[j]) + d[j]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = static_cast<bf16>(d[j]);
-        }
-        *dst = o;
-      }
+    for (int e = 0; e < 8; ++e) {
+      const float v = (drop && !kp[e]) ? 0.f : d[e] * sc;
+      o[e] = static_cast<bf16>(static_cast<float>(old[i][e]) + v);
     }
+    *reinterpret_cast<bf16x8*>(dx + t * (int64_t)P.K + kb * 128 + col) = o;
   }
 }
 
 }  // namespace
 
 bool lora_down_supported(int64_t M, int K, int R, int ldx, uint64_t offset) {
-  return M > 0 && K % 64 == 0 && R % 32 == 0 && R >= 32 && R <= 256 && ldx % 8 == 0 && offset % 4 == 0;
+  return M > 0 && K % 128 == 0 && R % 32 == 0 && R >= 32 && R <= 256 && ldx % 8 == 0 && offset % 4 == 0;
 }
 
 void lora_down(const LoraDownParams& p, hipStream_t s) {
