@@ -24,7 +24,12 @@ constexpr int kNT = 256;          // 4 waves per workgroup
 constexpr int kRowsPerBlock = kNT / kWave;
 constexpr int kBwdMaxBlocks = 512;  // measured best for d=4096 rows=8192 (256: 89 us, 512: 74 us, 1024: 81 us)
 
-template <typename T, int MAXC, bool RMS>
+// Forward: every load of the row (x, residual, weight) is issued before the first use, so a wave
+// has the whole row in flight at once. (A per-chunk `if (ch < nchunk)` around load -> add -> store
+// made hipcc close every chunk with vmcnt(0): one 16 B load pair in flight per wave, 2.6 TB/s.)
+// FULL: d / V is exactly MAXC x 64 chunks (every Llama / BasicLLM width) -> no guards at all;
+// otherwise loads are clamped to the last chunk and the stores are guarded.
+template <typename T, int MAXC, bool RMS, bool RES, bool FULL>
 __global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ res,
                                                        const T* __restrict__ w,
@@ -33,28 +38,38 @@ __global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
                                                        float* __restrict__ rstd_out, int64_t rows,
                                                        int d, float eps) {
   constexpr int V = Vec16<T>::N;
+  typedef typename Vec16<T>::type VT;
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int nchunk = d / V;
   const T* xr = x + row * d;
+  const T* rr = RES ? res + row * d : nullptr;
+  VT xv[MAXC], rv[MAXC], wvv[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = FULL ? lane + c * kWave : min(lane + c * kWave, nchunk - 1);
+    xv[c] = *reinterpret_cast<const VT*>(xr + ch * V);
+    if (RES) rv[c] = *reinterpret_cast<const VT*>(rr + ch * V);
+  }
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = FULL ? lane + c * kWave : min(lane + c * kWave, nchunk - 1);
+    wvv[c] = *reinterpret_cast<const VT*>(w + ch * V);
+  }
   float hv[MAXC][V];
   float s1 = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int ch = lane + c * kWave;
-    if (ch < nchunk) {
-      load16(xr + ch * V, hv[c]);
-      if (res != nullptr) {
-        float rv[V];
-        load16(res + row * d + ch * V, rv);
+    const bool ok = FULL || lane + c * kWave < nchunk;
 #pragma unroll
-        for (int i = 0; i < V; ++i) hv[c][i] = to_f(from_f<T>(hv[c][i] + rv[i]));  // round like torch
-        store16(h_out + row * d + ch * V, hv[c]);
-      }
-#pragma unroll
-      for (int i = 0; i < V; ++i) s1 += RMS ? hv[c][i] * hv[c][i] : hv[c][i];
+    for (int i = 0; i < V; ++i) {
+      float t = to_f(xv[c][i]);
+      if (RES) t = to_f(from_f<T>(t + to_f(rv[c][i])));  // round like torch
+      hv[c][i] = ok ? t : 0.f;
+      s1 += RMS ? hv[c][i] * hv[c][i] : hv[c][i];
     }
+    if (RES && ok) store16(h_out + row * d + (lane + c * kWave) * V, hv[c]);
   }
   s1 = wave_sum(s1);
   float mu = 0.f, rstd;
@@ -65,11 +80,9 @@ __global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
     float s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      const int ch = lane + c * kWave;
-      if (ch < nchunk) {
+      const bool ok = FULL || lane + c * kWave < nchunk;
 #pragma unroll
-        for (int i = 0; i < V; ++i) { const float t = hv[c][i] - mu; s2 += t * t; }
-      }
+      for (int i = 0; i < V; ++i) { const float t = hv[c][i] - mu; s2 += ok ? t * t : 0.f; }
     }
     s2 = wave_sum(s2);
     rstd = rsqrtf(s2 / d + eps);
@@ -77,17 +90,16 @@ __global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = lane + c * kWave;
-    if (ch < nchunk) {
-      float wv[V], o[V];
-      load16(w + ch * V, wv);
+    if (FULL || ch < nchunk) {
+      float o[V];
       if (!RMS && b != nullptr) {
         float bv[V];
         load16(b + ch * V, bv);
 #pragma unroll
-        for (int i = 0; i < V; ++i) o[i] = (hv[c][i] - mu) * rstd * wv[i] + bv[i];
+        for (int i = 0; i < V; ++i) o[i] = (hv[c][i] - mu) * rstd * to_f(wvv[c][i]) + bv[i];
       } else {
 #pragma unroll
-        for (int i = 0; i < V; ++i) o[i] = (hv[c][i] - mu) * rstd * wv[i];
+        for (int i = 0; i < V; ++i) o[i] = (hv[c][i] - mu) * rstd * to_f(wvv[c][i]);
       }
       store16(y + row * d + ch * V, o);
     }
@@ -100,8 +112,10 @@ __global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
 
 // Backward: one 256-thread workgroup per row (grid-strided), each thread owns MAXC 16-byte
 // column chunks, so the dw/db partial sums stay in a handful of VGPRs per thread for every
-// row the workgroup visits and are written once as this workgroup's fp32 slab.
-template <typename T, int MAXC, bool RMS>
+// row the workgroup visits and are written once as this workgroup's fp32 slab. The next row's
+// h / dy / residual-gradient chunks are loaded (clamped, unconditional) before this row's
+// reduction barriers, so a row's loads are always in flight behind the previous row's math.
+template <typename T, int MAXC, bool RMS, bool RES>
 __global__ __launch_bounds__(kNT) void norm_bwd_kernel(const T* __restrict__ dy,
                                                        const T* __restrict__ h,
                                                        const T* __restrict__ w,
@@ -110,38 +124,51 @@ __global__ __launch_bounds__(kNT) void norm_bwd_kernel(const T* __restrict__ dy,
                                                        const T* __restrict__ dres, T* __restrict__ dx,
                                                        float* __restrict__ ws, int64_t rows, int d) {
   constexpr int V = Vec16<T>::N;
+  typedef typename Vec16<T>::type VT;
   __shared__ float red[2 * kRowsPerBlock];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nchunk = d / V;
   float dwp[MAXC][V], dbp[MAXC][V], wv[MAXC][V];
+  int chs[MAXC];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int ch = tid + c * kNT;
+    chs[c] = min(tid + c * kNT, nchunk - 1);
 #pragma unroll
-    for (int i = 0; i < V; ++i) { dwp[c][i] = 0.f; dbp[c][i] = 0.f; wv[c][i] = 0.f; }
-    if (ch < nchunk) load16(w + ch * V, wv[c]);
+    for (int i = 0; i < V; ++i) { dwp[c][i] = 0.f; dbp[c][i] = 0.f; }
+    load16(w + chs[c] * V, wv[c]);
   }
+  VT hn[MAXC], dn[MAXC], rn[MAXC];
+  auto load_row = [&](int64_t rr) {
+    rr = rr < rows ? rr : rows - 1;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      hn[c] = *reinterpret_cast<const VT*>(h + rr * d + chs[c] * V);
+      dn[c] = *reinterpret_cast<const VT*>(dy + rr * d + chs[c] * V);
+      if (RES) rn[c] = *reinterpret_cast<const VT*>(dres + rr * d + chs[c] * V);
+    }
+  };
+  load_row(blockIdx.x);
   for (int64_t row = blockIdx.x; row < rows; row += gridDim.x) {
+    VT hc[MAXC], dc[MAXC], rc[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) { hc[c] = hn[c]; dc[c] = dn[c]; if (RES) rc[c] = rn[c]; }
+    load_row(row + gridDim.x);
     const float r = rstd[row];
     const float mu = RMS ? 0.f : mean[row];
     float xh[MAXC][V], g[MAXC][V];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
-      const int ch = tid + c * kNT;
-      if (ch < nchunk) {
-        float dv[V];
-        load16(h + row * d + ch * V, xh[c]);
-        load16(dy + row * d + ch * V, dv);
+      const bool ok = tid + c * kNT < nchunk;
 #pragma unroll
-        for (int i = 0; i < V; ++i) {
-          xh[c][i] = (xh[c][i] - mu) * r;
-          g[c][i] = dv[i] * wv[c][i];
-          sg += g[c][i];
-          sgx += g[c][i] * xh[c][i];
-          dwp[c][i] += dv[i] * xh[c][i];
-          if (!RMS) dbp[c][i] += dv[i];
-        }
+      for (int i = 0; i < V; ++i) {
+        const float dv = ok ? to_f(dc[c][i]) : 0.f;
+        xh[c][i] = (to_f(hc[c][i]) - mu) * r;
+        g[c][i] = dv * wv[c][i];
+        sg += g[c][i];
+        sgx += g[c][i] * xh[c][i];
+        dwp[c][i] += dv * xh[c][i];
+        if (!RMS) dbp[c][i] += dv;
       }
     }
     // two-value block reduction, one barrier pair per row
@@ -160,14 +187,8 @@ __global__ __launch_bounds__(kNT) void norm_bwd_kernel(const T* __restrict__ dy,
       const int ch = tid + c * kNT;
       if (ch < nchunk) {
         float o[V];
-        if (dres != nullptr) {
-          load16(dres + row * d + ch * V, o);
-        } else {
 #pragma unroll
-          for (int i = 0; i < V; ++i) o[i] = 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < V; ++i) o[i] += r * (g[c][i] - tsg - xh[c][i] * tsgx);
+        for (int i = 0; i < V; ++i) o[i] = (RES ? to_f(rc[c][i]) : 0.f) + r * (g[c][i] - tsg - xh[c][i] * tsgx);
         store16(dx + row * d + ch * V, o);
       }
     }
@@ -221,10 +242,16 @@ void launch_fwd(const void* x, const void* res, const void* w, const void* b, vo
   constexpr int V = Vec16<T>::N;
   const int per_lane = (d / V + kWave - 1) / kWave;
   const dim3 grid((unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock));
-#define GRT_NF(MC)                                                                              \
-  hipLaunchKernelGGL((norm_fwd_kernel<T, MC, RMS>), grid, dim3(kNT), 0, s, (const T*)x,          \
-                     (const T*)res, (const T*)w, (const T*)b, (T*)y, (T*)h_out, mean, rstd, rows, \
+#define GRT_NF4(MC, RES, FULL)                                                                  \
+  hipLaunchKernelGGL((norm_fwd_kernel<T, MC, RMS, RES, FULL>), grid, dim3(kNT), 0, s, (const T*)x, \
+                     (const T*)res, (const T*)w, (const T*)b, (T*)y, (T*)h_out, mean, rstd, rows,     \
                      d, eps)
+#define GRT_NF(MC)                                                     \
+  do {                                                                 \
+    const bool full = (d / V) == (MC) * kWave;                         \
+    if (res != nullptr) { if (full) GRT_NF4(MC, true, true); else GRT_NF4(MC, true, false); }   \
+    else { if (full) GRT_NF4(MC, false, true); else GRT_NF4(MC, false, false); }              \
+  } while (0)
   if (per_lane <= 1) GRT_NF(1);
   else if (per_lane <= 2) GRT_NF(2);
   else if (per_lane <= 4) GRT_NF(4);
@@ -232,6 +259,7 @@ void launch_fwd(const void* x, const void* res, const void* w, const void* b, vo
   else if (per_lane <= 16) GRT_NF(16);
   else GRT_NF(32);
 #undef GRT_NF
+#undef GRT_NF4
 }
 
 int bwd_max_blocks() {
@@ -257,14 +285,20 @@ void launch_bwd(const void* dy, const void* h, const void* w, const float* mean,
   const int per_thr = (d / V + kNT - 1) / kNT;
   const int nb = bwd_blocks(rows);
   const size_t lds = 0;
-#define GRT_NB(MC)                                                                             \
-  hipLaunchKernelGGL((norm_bwd_kernel<T, MC, RMS>), dim3(nb), dim3(kNT), lds, s, (const T*)dy, \
+#define GRT_NB2(MC, RES)                                                                            \
+  hipLaunchKernelGGL((norm_bwd_kernel<T, MC, RMS, RES>), dim3(nb), dim3(kNT), lds, s, (const T*)dy, \
                      (const T*)h, (const T*)w, mean, rstd, (const T*)dres, (T*)dx, ws, rows, d)
+#define GRT_NB(MC)                                      \
+  do {                                                  \
+    if (dres != nullptr) GRT_NB2(MC, true);             \
+    else GRT_NB2(MC, false);                            \
+  } while (0)
   if (per_thr <= 1) GRT_NB(1);
   else if (per_thr <= 2) GRT_NB(2);
   else if (per_thr <= 4) GRT_NB(4);
   else GRT_NB(8);
 #undef GRT_NB
+#undef GRT_NB2
   const int ncols = RMS ? d : 2 * d;
   hipLaunchKernelGGL(colsum_kernel, dim3((ncols + 63) / 64), dim3(kNT), 0, s, ws, nb, d, ncols, dw, db);
 }
