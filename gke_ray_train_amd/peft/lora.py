@@ -19,6 +19,7 @@ Documented deviation: one dropout mask per fused input (HF draws separate masks 
 """
 from __future__ import annotations
 
+import functools
 import json
 import math
 import os
@@ -65,6 +66,11 @@ _LORA_DOWN = _LORA_KERNELS_ENV in ("1", "down")
 _LORA_DX = _LORA_KERNELS_ENV in ("1", "dx")
 
 
+@functools.lru_cache(maxsize=None)
+def _num_cus(dev: torch.device) -> int:
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
 def _base_weight(base: nn.Module) -> torch.Tensor:
     return base.dequantize() if isinstance(base, NF4Linear) else base.weight
 
@@ -94,8 +100,11 @@ class _LoraFn(torch.autograd.Function):
         y = F.linear(x2, w, bias)
         del w
         acat = torch.cat(As, 0) if k > 1 else As[0]
-        # h = dropout(x) A^T in one pass over x (lora.hip); x_d is kept for the dA GEMM
-        res = C.lora_down(x2, acat, p, seed, offset, p > 0) if _LORA_DOWN else []
+        # h = dropout(x) A^T in one pass over x (lora.hip); x_d is kept for the dA GEMM. The kernel
+        # runs one workgroup per 32 tokens, so below 32 tokens per CU (the SFT job's ~2 K-token
+        # steps) the dropout pass + library GEMM fill the chip better.
+        res = (C.lora_down(x2, acat, p, seed, offset, p > 0)
+               if _LORA_DOWN and x2.shape[0] >= 32 * _num_cus(x2.device) else [])
         if res:
             h = res[0]
             xd = res[1] if p > 0 else x2

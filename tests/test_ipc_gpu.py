@@ -48,7 +48,7 @@ def _worker(rank, world, port, q):
             for rep in range(3):  # repeated calls exercise both staging parities
                 x = t.clone()
                 c.all_reduce(x, average=(rep == 2))
-            out[i] = x.float().cpu()
+            out[i] = x.float().cpu().numpy()  # by value: a shared-fd tensor dies with this process
         c = comms[None]
         c.barrier()
         torch.cuda.synchronize()
@@ -99,8 +99,8 @@ def test_ipc_allreduce_matches_host_sum(world):
         exp = sum(_inp(r, i, n, dt).float() for r in range(world)) / world
         tol = 1e-6 if dt == torch.float32 else 1e-2
         for r in range(world):
-            got = res[r][i]
+            got = torch.from_numpy(res[r][i])
             assert torch.allclose(got, exp, atol=tol * 4, rtol=tol), (world, i, r, (got - exp).abs().max())
         for r in range(1, world):  # fixed reduction order: bit-identical on every rank
-            assert torch.equal(res[r][i], res[0][i])
+            assert torch.equal(torch.from_numpy(res[r][i]), torch.from_numpy(res[0][i]))
     print(f"world {world}: 4-byte all-reduce {res[0]['us']:.1f} us")
