@@ -23,6 +23,10 @@ MI355X design (not a translation of torch's C++ Reducer):
   traffic shrink by world), and the updated shards are ALL-GATHERED back into the flat parameter
   buffer asynchronously, bucket by bucket in forward order, each bucket waited for by a forward
   pre-hook of the first module that uses it — the gather overlaps the next step's forward.
+* one GPU: the gradient-norm reduction of each bucket (sum of squares, HBM-bound) runs on a side
+  stream as soon as the bucket's last gradient is written, under the remaining backward GEMMs;
+  ``clip_grad_norm_`` then only combines the per-bucket partial sums (``GRT_EARLY_GRAD_NORM=0``
+  computes the norm after backward instead).
 """
 from __future__ import annotations
 
@@ -86,6 +90,8 @@ class _Bucket:
     work: Optional[object] = None
     shard_off: int = 0        # ZeRO: offset of this bucket's chunk in the rank's shard buffers
     ag_work: Optional[object] = None
+    norm_slot: int = -1       # one GPU: this bucket's slot in the early grad-norm workspace
+    normed: bool = False      # its sum of squares was launched for the current step
 
 
 @dataclass
@@ -146,7 +152,15 @@ class DistributedDataParallel(nn.Module):
                 seen.add(id(p))
                 named.append((n, p))
         total_bytes = sum(p.numel() * p.element_size() for _, p in named)
-        self.bucket_bytes = int(bucket_cap_mb * 2 ** 20) if bucket_cap_mb else plan_bucket_bytes(total_bytes, self.world_size)
+        dev0 = named[0][1].device if named else torch.device("cpu")
+        self._early_norm = (self.world_size == 1 and dev0.type == "cuda"
+                            and os.environ.get("GRT_EARLY_GRAD_NORM", "1") != "0")
+        if bucket_cap_mb:
+            self.bucket_bytes = int(bucket_cap_mb * 2 ** 20)
+        elif self._early_norm and not os.environ.get("GRT_BUCKET_MB"):
+            self.bucket_bytes = 256 * 2 ** 20  # norm granularity only: no collectives on one GPU
+        else:
+            self.bucket_bytes = plan_bucket_bytes(total_bytes, self.world_size)
         # group by (dtype, decay), reverse registration order inside each group
         groups: Dict[tuple, List[tuple]] = {}
         for n, p in named:
@@ -176,6 +190,19 @@ class DistributedDataParallel(nn.Module):
         self._register_hooks()
         if self.zero:
             self._setup_shards()
+        self._norm_ws = None
+        self._norm_stream = None
+        self._norm_bad = False  # a step whose early norm cannot be trusted (fall back)
+        if self._early_norm:
+            from .. import _native
+            C = _native.kernels()
+            nslots = 0
+            for g in self.groups:
+                for b in g.buckets:
+                    b.norm_slot = nslots
+                    nslots += 1
+            self._norm_ws = torch.zeros(nslots * C.sumsq_blocks(), device=dev0, dtype=torch.float32)
+            self._norm_stream = torch.cuda.Stream(dev0)
 
     # ------------------------------------------------------------------ layout
     def _flatten(self, items, dtype, decay, grad_dtype) -> _FlatGroup:
@@ -275,13 +302,31 @@ class DistributedDataParallel(nn.Module):
         self._mark_ready(g, b)
 
     def _mark_ready(self, g, b):
-        if not self._sync or self.world_size == 1:
+        if not self._sync:
+            return
+        if self.world_size == 1:
+            if self._early_norm:
+                b.ready += 1
+                if b.ready > len(b.params):
+                    self._norm_bad = True
+                elif b.ready == len(b.params):
+                    self._launch_norm(g, b)
             return
         b.ready += 1
         if b.ready > len(b.params):  # a parameter announced twice would launch a bucket early
             raise RuntimeError("DDP bucket readiness over-counted (gradient announced twice)")
         if b.ready == len(b.params):
             self._launch(g, b)
+
+    def _launch_norm(self, g: _FlatGroup, b: _Bucket):
+        """Sum of squares of a finished bucket's gradient on the side stream (ordered after the
+        kernels that wrote it)."""
+        from .. import _native
+        cur = torch.cuda.current_stream(g.grad.device)
+        self._norm_stream.wait_stream(cur)
+        with torch.cuda.stream(self._norm_stream):
+            _native.kernels().sumsq(g.grad[b.start:b.end], self._norm_ws, b.norm_slot)
+        b.normed = True
 
     def _launch(self, g: _FlatGroup, b: _Bucket):
         if b.work is not None:
@@ -313,6 +358,12 @@ class DistributedDataParallel(nn.Module):
                 self._slots[p].fresh = False
                 p.grad = self._slots[p].view
         if self.world_size == 1:
+            if self._early_norm and self._sync:
+                for g in self.groups:
+                    for b in g.buckets:
+                        if not b.normed:  # no gradient announced (unused params) or partial bucket
+                            self._launch_norm(g, b)
+                        b.ready = 0
             return
         for g in self.groups:
             for b in g.buckets:
@@ -339,6 +390,21 @@ class DistributedDataParallel(nn.Module):
         host sync); the 1/world averaging is folded into the coefficient consumed by FusedAdamW."""
         from ..ops import clip_grad_norm_ as _clip
         W = self.world_size
+        if self._early_norm:
+            done = all(b.normed for g in self.groups for b in g.buckets)
+            bad = self._norm_bad
+            for g in self.groups:
+                for b in g.buckets:
+                    b.normed = False
+            self._norm_bad = False
+            if done and not bad:
+                from .. import _native
+                from ..ops import GradClipState
+                cur = torch.cuda.current_stream(self._norm_ws.device)
+                cur.wait_stream(self._norm_stream)
+                st = GradClipState(self._norm_ws.device)
+                _native.kernels().clip_finalize(self._norm_ws, self._norm_ws.numel(), float(max_norm), 1.0, st.buf)
+                return st
         if not self.zero:
             return _clip(self.grad_buffers(), max_norm, prescale=1.0 / W)
         st = _clip(self.grad_buffers(), 0.0, prescale=1.0)
@@ -377,6 +443,12 @@ class DistributedDataParallel(nn.Module):
         for p, sl in self._slots.items():
             sl.fresh = True
             p.grad = None
+        for g in self.groups:
+            for b in g.buckets:
+                b.normed = False
+                if self.world_size == 1:
+                    b.ready = 0
+        self._norm_bad = False
 
     def optimizer_param_groups(self, weight_decay: float = 0.0):
         """One flat Parameter per (dtype, decay) group; its .grad is the flat gradient buffer

@@ -168,3 +168,32 @@ def test_llama3_70b_shapes_fsdp_offload_step():
         losses.append(loss)
     assert all(l == l and l < 20 for l in losses), losses
     assert losses[-1] < losses[0], losses
+
+
+@pytest.mark.parametrize("accum,bucket_mb", [(1, 0.25), (2, 0.25), (1, None)])
+def test_ddp_early_grad_norm_matches_full_norm(accum, bucket_mb):
+    """One GPU: per-bucket sums of squares launched on a side stream as buckets finish during
+    backward (parallel/ddp.py) give the same global norm / clip coefficient as the norm of the
+    final gradient buffers computed after backward, over several steps (flags reset per step)."""
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.ops import clip_grad_norm_
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    m = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=3)
+    ddp = DistributedDataParallel(m, bucket_cap_mb=bucket_mb)
+    assert ddp._early_norm
+    if bucket_mb:
+        assert ddp.num_buckets() > 2
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for step in range(3):
+        for j in range(accum):
+            ids = torch.randint(0, 512, (2, 128), device="cuda", generator=g)
+            with ddp.no_sync(j < accum - 1):
+                (ddp(ids, labels=ids)["loss"] / accum).backward()
+        ddp.finish_gradient_sync()
+        st = ddp.clip_grad_norm_(0.3)
+        ref = clip_grad_norm_(ddp.grad_buffers(), 0.3)
+        full = torch.sqrt(sum((b.float() ** 2).sum() for b in ddp.grad_buffers()))
+        torch.cuda.synchronize()
+        assert abs(float(st.buf[0]) - float(full)) <= 1e-3 * float(full), (step, float(st.buf[0]), float(full))
+        assert abs(float(st.buf[1]) - float(ref.buf[1])) <= 1e-3 * float(ref.buf[1])
+        ddp.zero_grad()
