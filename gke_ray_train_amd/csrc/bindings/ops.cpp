@@ -365,7 +365,8 @@ void clip_finalize(const Tensor& ws, int64_t nparts, double max_norm, double pre
                           cur_stream(ws));
 }
 void adamw(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const optional<Tensor>& master, const Tensor& hyper,
-           const optional<Tensor>& gscale, int64_t max_blocks) {
+           const optional<Tensor>& gscale, int64_t max_blocks, int64_t index_offset) {
+  TORCH_CHECK(index_offset >= 0 && index_offset % 4 == 0, "adamw: index_offset must be a multiple of 4");
   check_contig(p, "p");
   check_contig(gr, "g");
   check_contig(m, "m");
@@ -373,7 +374,8 @@ void adamw(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const optional<Ten
   const int64_t n = p.numel();
   TORCH_CHECK(gr.numel() == n && m.numel() == n && v.numel() == n, "adamw size mismatch");
   TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat, "adam state must be fp32");
-  TORCH_CHECK(hyper.scalar_type() == at::kFloat && hyper.numel() >= 8 && hyper.is_cuda(), "hyper fp32[8] on device");
+  TORCH_CHECK(hyper.scalar_type() == at::kFloat && hyper.numel() >= 10 && hyper.is_cuda(),
+              "hyper fp32[10] on device: lr, b1, b2, eps, wd, bc1, bc2, gscale, stochastic_rounding, step");
   for (const Tensor* t : std::initializer_list<const Tensor*>{&p, &gr, &m, &v})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0 ||
                     (t->element_size() == 2 && reinterpret_cast<uintptr_t>(t->data_ptr()) % 8 == 0),
@@ -385,7 +387,8 @@ void adamw(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const optional<Ten
   c10::OptionalDeviceGuard g(p.device());
   grt::adamw_step(dtype_of(p), dtype_of(gr), p.data_ptr(), gr.data_ptr(), m.data_ptr<float>(), v.data_ptr<float>(),
                   master.has_value() ? master->data_ptr<float>() : nullptr, n, hyper.data_ptr<float>(),
-                  gscale.has_value() ? gscale->data_ptr<float>() : nullptr, cur_stream(p), (int)max_blocks);
+                  gscale.has_value() ? gscale->data_ptr<float>() : nullptr, cur_stream(p), (int)max_blocks,
+                  index_offset);
 }
 void scale_(Tensor& x, double a, const optional<Tensor>& a_ptr) {
   check_contig(x, "x");
@@ -771,7 +774,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sumsq", &sumsq);
   m.def("clip_finalize", &clip_finalize);
   m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("master"),
-        py::arg("hyper"), py::arg("gscale"), py::arg("max_blocks") = 0);
+        py::arg("hyper"), py::arg("gscale"), py::arg("max_blocks") = 0, py::arg("index_offset") = 0);
   m.def("scale_", &scale_);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("scale"),
         py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);

@@ -77,7 +77,8 @@ void clip_coef_finalize(const float* ws, int nparts, float max_norm, float presc
 // max_blocks > 0 caps the grid (grid-stride loop): a bandwidth-throttled update that can run
 // beside compute-bound kernels on another stream without starving them (parallel/overlap.py).
 void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
-                int64_t n, const float* hyper, const float* grad_scale_ptr, hipStream_t s, int max_blocks = 0);
+                int64_t n, const float* hyper, const float* grad_scale_ptr, hipStream_t s, int max_blocks = 0,
+                int64_t index_offset = 0);  // element index of p[0] in its flat buffer (stochastic rounding)
 // Scale in place: x *= a (device scalar pointer or host value when a_ptr == null).
 void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s);
 

@@ -59,18 +59,33 @@ __global__ __launch_bounds__(kNT) void clip_finalize_kernel(const float* __restr
   }
 }
 
+// fp32 -> bf16 with stochastic rounding: add 16 random bits below the bf16 mantissa, truncate.
+__device__ __forceinline__ bf16 sr_bf16(float x, uint32_t r16) {
+  const uint32_t u = __float_as_uint(x);
+  if ((u & 0x7f800000u) == 0x7f800000u) return static_cast<bf16>(x);  // inf / nan unchanged
+  const uint32_t t = (u + r16) & 0xffff0000u;
+  return static_cast<bf16>(__uint_as_float(t));  // exact: the low 16 bits are zero
+}
+
 template <typename P, typename G>
 __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     float* __restrict__ master, int64_t n,
                                                     const float* __restrict__ hyper,
-                                                    const float* __restrict__ gsp) {
+                                                    const float* __restrict__ gsp, uint64_t ioff) {
   const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float bc1 = hyper[5], bc2 = hyper[6];
   const float gs = hyper[7] * (gsp ? gsp[1] : 1.f);
   const float step = lr / bc1;
   const float rbc2 = rsqrtf(bc2);
   const float decay = 1.f - lr * wd;
+  // bf16 parameters without an fp32 master copy: stochastic rounding of the updated value
+  // (hyper[8] != 0; hyper[9] = step). Updates below half a bf16 ulp (lr 2e-5 on |w| ~ 1e-2) would
+  // otherwise round away entirely; SR keeps every update in expectation.
+  // The random bits are a hash of (step, element index + ioff): a launch over a slice of a flat
+  // buffer (the overlapped optimizer's per-module chunks) rounds exactly like one over the whole.
+  const bool sr = sizeof(P) == 2 && master == nullptr && hyper[8] != 0.f;
+  const uint64_t srkey = hash_u64(0x5352ull ^ ((uint64_t)hyper[9] << 20));
   const int64_t n4 = n / 4;
   const int64_t stride = (int64_t)gridDim.x * kNT;
   for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n4; i += stride) {
@@ -117,8 +132,14 @@ __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* 
     }
     if constexpr (sizeof(P) == 2) {
       bf16x4 t;
+      if (sr) {
+        const uint64_t h = hash_u64(srkey ^ ((ioff + (uint64_t)o) >> 2));
 #pragma unroll
-      for (int k = 0; k < 4; ++k) t[k] = from_f<bf16>(pf[k]);
+        for (int k = 0; k < 4; ++k) t[k] = sr_bf16(pf[k], (uint32_t)(h >> (16 * k)) & 0xffffu);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = from_f<bf16>(pf[k]);
+      }
       *reinterpret_cast<bf16x4*>(p + o) = t;
     } else {
       f32x4 t;
@@ -135,7 +156,12 @@ __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* 
     v[j] = b2 * v[j] + (1.f - b2) * gf * gf;
     pf = pf * decay - step * m[j] / (sqrtf(v[j]) * rbc2 + eps);
     if (master) master[j] = pf;
-    p[j] = from_f<P>(pf);
+    if constexpr (sizeof(P) == 2) {
+      p[j] = sr ? sr_bf16(pf, (uint32_t)(hash_u64(srkey ^ ((ioff + (uint64_t)j) >> 2)) >> (16 * ((ioff + j) & 3))) & 0xffffu)
+                : from_f<P>(pf);
+    } else {
+      p[j] = from_f<P>(pf);
+    }
   }
 }
 
@@ -171,18 +197,18 @@ void clip_coef_finalize(const float* ws, int nparts, float max_norm, float presc
 }
 
 void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
-                int64_t n, const float* hyper, const float* gsp, hipStream_t s, int max_blocks) {
+                int64_t n, const float* hyper, const float* gsp, hipStream_t s, int max_blocks, int64_t ioff) {
   unsigned nb = grid_for(n / 4 + 1);
   if (max_blocks > 0 && nb > (unsigned)max_blocks) nb = (unsigned)max_blocks;
   const dim3 grid(nb);
   if (pdt == DType::BF16 && gdt == DType::BF16)
-    hipLaunchKernelGGL((adamw_kernel<bf16, bf16>), grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, master, n, hyper, gsp);
+    hipLaunchKernelGGL((adamw_kernel<bf16, bf16>), grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, master, n, hyper, gsp, (uint64_t)ioff);
   else if (pdt == DType::BF16)
-    hipLaunchKernelGGL((adamw_kernel<bf16, float>), grid, dim3(kNT), 0, s, (bf16*)p, (const float*)g, m, v, master, n, hyper, gsp);
+    hipLaunchKernelGGL((adamw_kernel<bf16, float>), grid, dim3(kNT), 0, s, (bf16*)p, (const float*)g, m, v, master, n, hyper, gsp, (uint64_t)ioff);
   else if (gdt == DType::BF16)
-    hipLaunchKernelGGL((adamw_kernel<float, bf16>), grid, dim3(kNT), 0, s, (float*)p, (const bf16*)g, m, v, master, n, hyper, gsp);
+    hipLaunchKernelGGL((adamw_kernel<float, bf16>), grid, dim3(kNT), 0, s, (float*)p, (const bf16*)g, m, v, master, n, hyper, gsp, (uint64_t)ioff);
   else
-    hipLaunchKernelGGL((adamw_kernel<float, float>), grid, dim3(kNT), 0, s, (float*)p, (const float*)g, m, v, master, n, hyper, gsp);
+    hipLaunchKernelGGL((adamw_kernel<float, float>), grid, dim3(kNT), 0, s, (float*)p, (const float*)g, m, v, master, n, hyper, gsp, (uint64_t)ioff);
 }
 
 void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s) {

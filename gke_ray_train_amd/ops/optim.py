@@ -13,6 +13,7 @@ ray-jobs/fine_tune_config.json:19).
 from __future__ import annotations
 
 import math
+import os
 from typing import Iterable, Optional
 
 import torch
@@ -90,18 +91,26 @@ class FusedAdamW(torch.optim.Optimizer):
     """
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01,
-                 master_weights: bool = False):
+                 master_weights: bool = False, stochastic_rounding: Optional[bool] = None):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.master_weights = master_weights
+        # bf16 params without a master copy (the reference's paged_adamw_32bit on a bf16 model):
+        # stochastic rounding of the update by default (GRT_ADAMW_SR=0 -> round to nearest)
+        if stochastic_rounding is None:
+            stochastic_rounding = os.environ.get("GRT_ADAMW_SR", "1") != "0"
+        self.stochastic_rounding = bool(stochastic_rounding)
         self._hyper = {}
 
     def _hyper_buf(self, dev, key):
         hb = self._hyper.get((dev, key))
         if hb is None:
-            hb = torch.empty(8, dtype=torch.float32, device=dev)
+            hb = torch.empty(10, dtype=torch.float32, device=dev)
             self._hyper[(dev, key)] = hb
         return hb
+
+    def _sr(self) -> float:
+        return 1.0 if self.stochastic_rounding and not self.master_weights else 0.0
 
     def _init_state(self, p):
         st = self.state[p]
@@ -129,7 +138,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 step = float(st["step"])
                 hb = self._hyper_buf(p.device, (gi,))
                 hb.copy_(torch.tensor([group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** step,
-                                       1.0 - b2 ** step, 1.0], dtype=torch.float32), non_blocking=True)
+                                       1.0 - b2 ** step, 1.0, self._sr(), step], dtype=torch.float32),
+                         non_blocking=True)
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 out.append((p, g, st["exp_avg"], st["exp_avg_sq"], st.get("master"), hb))
         return out
@@ -155,8 +165,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 master = st.get("master")
                 if p.is_cuda:
                     hb = self._hyper_buf(p.device, (gi,))
-                    hb.copy_(torch.tensor([lr, b1, b2, eps, wd, bc1, bc2, 1.0], dtype=torch.float32),
-                             non_blocking=True)
+                    hb.copy_(torch.tensor([lr, b1, b2, eps, wd, bc1, bc2, 1.0, self._sr(), step],
+                                          dtype=torch.float32), non_blocking=True)
                     g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                     _native.kernels().adamw(p.data, g, st["exp_avg"], st["exp_avg_sq"], master, hb,
                                             None if grad_scale is None else grad_scale.buf)
@@ -181,7 +191,7 @@ class OffloadedAdamW(FusedAdamW):
 
     def __init__(self, params, chunk_elems: int = 1 << 26, **kw):
         super().__init__(params, **kw)
-        self.chunk = int(chunk_elems)
+        self.chunk = max(64, int(chunk_elems) // 64 * 64)  # aligned chunks (vector kernel, SR stream)
         self._stage = None
         self._copy_stream = None
 
@@ -205,7 +215,8 @@ class OffloadedAdamW(FusedAdamW):
                 st["step"] += 1
                 step = float(st["step"])
                 hb = self._hyper_buf(p.device, (gi,))
-                hb.copy_(torch.tensor([lr, b1, b2, eps, wd, 1.0 - b1 ** step, 1.0 - b2 ** step, 1.0]), non_blocking=True)
+                hb.copy_(torch.tensor([lr, b1, b2, eps, wd, 1.0 - b1 ** step, 1.0 - b2 ** step, 1.0, self._sr(), step]),
+                         non_blocking=True)
                 self._stream_update(p, st, hb, grad_scale)
 
     NSLOT = 3
@@ -251,7 +262,7 @@ class OffloadedAdamW(FusedAdamW):
             comp.wait_event(up_done[i])
             mb, vb = self._stage[i % self.NSLOT]
             C.adamw(pf[s:e], gf[s:e], mb[: e - s], vb[: e - s], None, hb,
-                    None if grad_scale is None else grad_scale.buf)
+                    None if grad_scale is None else grad_scale.buf, 0, s)
             upd_done[i].record(comp)
             with torch.cuda.stream(down):
                 down.wait_event(upd_done[i])

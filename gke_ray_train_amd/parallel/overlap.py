@@ -123,7 +123,7 @@ class OverlappedOptimizer:
                 for gi, lo, hi in rs:
                     p, g, ea, eas, master, hb = per_group[gi]
                     C.adamw(p.data[lo:hi], g[lo:hi], ea[lo:hi], eas[lo:hi],
-                            None if master is None else master[lo:hi], hb, gs, self.max_blocks)
+                            None if master is None else master[lo:hi], hb, gs, self.max_blocks, lo)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
                 self._events[m] = ev

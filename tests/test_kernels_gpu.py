@@ -283,6 +283,28 @@ def test_adamw_and_clip(pdt):
     _close(opt.state[P]["exp_avg"], m, 1e-6, 1e-4, "adamw m")
 
 
+@pytest.mark.parametrize("sr", [False, True])
+def test_adamw_bf16_stochastic_rounding(sr):
+    """bf16 params without a master copy: an update of 1/4 of the bf16 spacing below 1.0 (lr 2^-10
+    on p = 1, first Adam step |update| = lr) rounds away under round-to-nearest but is kept in
+    expectation under stochastic rounding (mean within a few sigma, values only the two neighbours)."""
+    from gke_ray_train_amd.ops import FusedAdamW
+    n = 1 << 20
+    P = torch.nn.Parameter(torch.ones(n, device=DEV, dtype=torch.bfloat16))
+    P.grad = torch.ones(n, device=DEV, dtype=torch.bfloat16)
+    opt = FusedAdamW([P], lr=2.0 ** -10, weight_decay=0.0, stochastic_rounding=sr)
+    opt.step()
+    x = P.data.float()
+    if not sr:
+        assert torch.equal(x, torch.ones_like(x))
+        return
+    lo = 1.0 - 2.0 ** -8
+    assert bool(((x == 1.0) | (x == lo)).all())
+    mean = x.mean().item()
+    sigma = 2.0 ** -8 * (0.25 * 0.75) ** 0.5 / n ** 0.5
+    assert abs(mean - (1.0 - 2.0 ** -10)) < 6 * sigma, (mean, 1.0 - 2.0 ** -10)
+
+
 def test_nf4_roundtrip():
     from gke_ray_train_amd import ops
     from gke_ray_train_amd.ops import _ref

@@ -44,7 +44,10 @@ def test_offloaded_adamw_matches_fused():
 
 
 @pytest.mark.parametrize("offload", [False, True])
-def test_fsdp_world1_matches_ddp_on_gpu(offload):
+def test_fsdp_world1_matches_ddp_on_gpu(offload, monkeypatch):
+    # the two engines lay parameters out differently; compare with round-to-nearest updates
+    # (stochastic rounding draws its bits by flat-buffer index)
+    monkeypatch.setenv("GRT_ADAMW_SR", "0")
     from gke_ray_train_amd.models import build_llama
     from gke_ray_train_amd.models.llama import LlamaForCausalLM, RMSNorm, get_config
     from gke_ray_train_amd.ops import FusedAdamW

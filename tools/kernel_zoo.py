@@ -76,7 +76,7 @@ p = torch.randn(n, device=dev, dtype=bf)
 g = torch.randn(n, device=dev, dtype=bf)
 m = torch.zeros(n, device=dev)
 vv = torch.zeros(n, device=dev)
-hyper = torch.tensor([1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, 1.0], device=dev)
+hyper = torch.tensor([1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, 1.0, 0.0, 1.0], device=dev)
 rep(lambda: C.adamw(p, g, m, vv, None, hyper, None))
 del p, g, m, vv
 

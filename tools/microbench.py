@@ -108,7 +108,7 @@ def memops(T=8192, d=4096, f=11008):
     g = torch.randn(n, device=dev, dtype=torch.bfloat16)
     m = torch.zeros(n, device=dev)
     vv = torch.zeros(n, device=dev)
-    hyper = torch.tensor([1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, 1.0], device=dev)
+    hyper = torch.tensor([1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, 1.0, 0.0, 1.0], device=dev)
     t = timeit(lambda: C.adamw(p, g, m, vv, None, hyper, None), iters=10)
     out.append(dict(op="adamw_bf16", ms=t * 1e3, gbs=n * 22 / t / 1e9))
     logits = torch.randn(T, 32000, device=dev, dtype=torch.bfloat16)
