@@ -265,6 +265,18 @@ void dropout_bwd_seeded(const Tensor& dy, const Tensor& dx, double p, int64_t se
 }
 
 // ------------------------------------------------------------------ LoRA adapter
+// compute units of a device (cached)
+static int device_cus(int dev) {
+  static int cache[64] = {0};
+  if (dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    cache[dev] = v;
+  }
+  return cache[dev];
+}
+
 // (h, xd) = lora_down(x [M, K], a [R, K]): h = (x * keep / (1-p)) a^T, xd = x * keep / (1-p) when
 // want_xd (same keep mask as dropout_fwd_seeded(x, p, seed, offset)). Returns {} when the shape is
 // not supported by the kernel (the caller falls back to the torch path).
@@ -288,6 +300,13 @@ std::vector<Tensor> lora_down(const Tensor& x, const Tensor& a, double p, int64_
   lp.x = x.data_ptr(); lp.a = a.data_ptr(); lp.h = h.data_ptr(); lp.xd = want_xd ? xd.data_ptr() : nullptr;
   lp.M = M; lp.K = K; lp.R = R; lp.ldx = (int)x.stride(0);
   lp.p = (float)p; lp.seed = (uint64_t)seed; lp.offset = (uint64_t)offset;
+  static const int split_env = [] { const char* e = getenv("GRT_LORA_DOWN_SPLIT"); return e ? atoi(e) : 0; }();
+  lp.ksplit = split_env > 0 ? std::min(split_env, K / 128) : grt::lora_down_splits(M, K, device_cus(x.device().index()));
+  Tensor hpart;
+  if (lp.ksplit > 1) {
+    hpart = at::empty({(int64_t)lp.ksplit, M, R}, x.options().dtype(at::kFloat));
+    lp.hpart = hpart.data_ptr<float>();
+  }
   grt::lora_down(lp, cur_stream(x));
   if (want_xd) return {h, xd};
   return {h};

@@ -89,7 +89,9 @@ struct LoraDownParams {
   const void* x; const void* a; void* h; void* xd;
   int64_t M; int K; int R; int ldx;
   float p; uint64_t seed; uint64_t offset;
+  int ksplit = 1; float* hpart = nullptr;  // split-K: fp32 partials [ksplit][M][R], summed into h
 };
+int lora_down_splits(int64_t M, int K, int cus);
 bool lora_down_supported(int64_t M, int K, int R, int ldx, uint64_t offset);
 void lora_down(const LoraDownParams& p, hipStream_t s);
 // dX[M][K] (+)= keep/(1-p) ⊙ (g[M][R] · A[R][K]), given A^T = at [K][R] (same keep mask as lora_down)

@@ -48,8 +48,6 @@ __device__ __forceinline__ void keep8(uint64_t key, uint64_t idx0, uint32_t thr,
 // LDS images (one barrier per chunk) from which each wave feeds two 16-wide k-steps of MFMAs
 // D[R row][token] = A · x_d^T. (MFMA fragments straight from global memory touch 32 rows x 32 B
 // per instruction — address-unit bound; the LDS images make every global access a full row.)
-constexpr int LD_KC = 128;          // K chunk
-constexpr int LD_XS = LD_KC + 8;    // LDS row (bf16): +16 B so b128 fragment reads of 32 rows spread over banks
 constexpr int LD_PF = 4;            // x chunks in flight per thread
 
 __device__ __forceinline__ void drop8(bf16x8& v, uint64_t key, uint64_t idx0, uint32_t thr, float sc) {
@@ -59,46 +57,58 @@ __device__ __forceinline__ void drop8(bf16x8& v, uint64_t key, uint64_t idx0, ui
   for (int e = 0; e < 8; ++e) v[e] = static_cast<bf16>(kp[e] ? static_cast<float>(v[e]) * sc : 0.f);
 }
 
-template <int RB>
-constexpr int lora_down_lds_bytes() {
-  return 2 * 32 * LD_XS * 2 + 2 * 32 * RB * LD_XS * 2;  // x images + A images (the reduction aliases A)
+template <int RB, int KC>
+constexpr int lora_down_lds_bytes() {  // x images + A images; the final reduction reuses the space
+  return (2 * 32 * (KC + 8) * 2 + 2 * 32 * RB * (KC + 8) * 2) > 3 * RB * 16 * 64 * 4
+             ? (2 * 32 * (KC + 8) * 2 + 2 * 32 * RB * (KC + 8) * 2) : 3 * RB * 16 * 64 * 4;
 }
 
-template <int RB>  // R = 32 * RB
+// KC: K chunk (128, or 64 for half the LDS: two workgroups per CU at R = 192)
+template <int RB, int KC>  // R = 32 * RB
 __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) {
   constexpr int R = 32 * RB;
-  constexpr int AIMG = R * LD_XS;  // elements per A image
-  static_assert(3 * RB * 16 * 64 * 4 <= 2 * AIMG * 2, "reduction scratch must fit in the A images");
-  __shared__ __attribute__((aligned(16))) char smem[lora_down_lds_bytes<RB>()];
-  bf16* xs = reinterpret_cast<bf16*>(smem);                       // [2][32][LD_XS]
-  bf16* as = reinterpret_cast<bf16*>(smem + 2 * 32 * LD_XS * 2);  // [2][R][LD_XS]
+  constexpr int XS = KC + 8;         // LDS row (bf16): +16 B so b128 fragment reads of 32 rows spread over banks
+  constexpr int AIMG = R * XS;       // elements per A image
+  constexpr int NV = KC / 64;        // 16 B x vectors per thread per chunk (32 rows x KC / 256 threads / 8)
+  constexpr int TPA = KC / 8;        // A loader threads per row
+  constexpr int NA = R * TPA / 256;  // A vectors per thread per chunk
+  constexpr int KSW = KC / 64;       // 16-wide k-steps per wave per chunk
+  __shared__ __attribute__((aligned(16))) char smem[lora_down_lds_bytes<RB, KC>()];
+  bf16* xs = reinterpret_cast<bf16*>(smem);                    // [2][32][XS]
+  bf16* as = reinterpret_cast<bf16*>(smem + 2 * 32 * XS * 2);  // [2][R][XS]
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t t0 = (int64_t)blockIdx.x * 32;
-  const int lr = tid >> 3, lc = (tid & 7) * 16;  // x loader: row, first of 16 columns
+  // split-K: blockIdx = split * (token blocks) + token block; this workgroup reduces K chunks
+  // [c_lo, c_lo + nch) and writes an fp32 partial when the K range is split (lora_hsum adds them)
+  const int ntb = (int)((P.M + 31) / 32);
+  const int tb = blockIdx.x % ntb, ksi = blockIdx.x / ntb;
+  const int nch_all = P.K / KC;
+  const int c_lo = ksi * nch_all / P.ksplit;
+  const int nch = (ksi + 1) * nch_all / P.ksplit - c_lo;
+  const int64_t t0 = (int64_t)tb * 32;
+  const int lr = tid >> 3, lc = (tid & 7) * 8 * NV;  // x loader: row, first of 8 NV columns
   const int64_t ltok = t0 + lr;
   const bool lok = ltok < P.M;
-  const bf16* src = static_cast<const bf16*>(P.x) + (lok ? ltok : P.M - 1) * (int64_t)P.ldx + lc;
-  bf16* xdst = (P.xd != nullptr && lok) ? static_cast<bf16*>(P.xd) + ltok * (int64_t)P.K + lc : nullptr;
-  const int ar = tid >> 4, ac = (tid & 15) * 8;  // A loader: rows ar + 16 j, 8 columns from ac
-  const bf16* asrc = static_cast<const bf16*>(P.a) + (int64_t)ar * P.K + ac;
-  const int nch = P.K / LD_KC;
+  const bf16* src = static_cast<const bf16*>(P.x) + (lok ? ltok : P.M - 1) * (int64_t)P.ldx + c_lo * KC + lc;
+  bf16* xdst = (P.xd != nullptr && lok) ? static_cast<bf16*>(P.xd) + ltok * (int64_t)P.K + c_lo * KC + lc : nullptr;
+  const int ar = tid / TPA, ac = (tid % TPA) * 8;  // A loader: rows ar + (256 / TPA) j, 8 columns from ac
+  const bf16* asrc = static_cast<const bf16*>(P.a) + (int64_t)ar * P.K + c_lo * KC + ac;
   const bool drop = P.p > 0.f;
   const uint32_t thr = drop_thr(P.p);
   const float sc = drop ? 1.f / (1.f - P.p) : 1.f;
   const uint64_t key = hash_u64(P.seed);
-  const uint64_t eidx = P.offset + (uint64_t)ltok * (uint64_t)P.K + lc;  // element index of x[ltok][lc]
+  const uint64_t eidx = P.offset + (uint64_t)ltok * (uint64_t)P.K + c_lo * KC + lc;  // of this thread's first x element
 
-  bf16x8 ring[LD_PF][2];
+  bf16x8 ring[LD_PF][NV];
 #pragma unroll
   for (int i = 0; i < LD_PF; ++i)
     if (i < nch) {
-      ring[i][0] = *reinterpret_cast<const bf16x8*>(src + i * LD_KC);
-      ring[i][1] = *reinterpret_cast<const bf16x8*>(src + i * LD_KC + 8);
-    }
-  bf16x8 areg[2 * RB];
 #pragma unroll
-  for (int j = 0; j < 2 * RB; ++j) areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * 16 * P.K);
+      for (int v = 0; v < NV; ++v) ring[i][v] = *reinterpret_cast<const bf16x8*>(src + i * KC + 8 * v);
+    }
+  bf16x8 areg[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * (256 / TPA) * P.K);
   f32x16 acc[RB];
 #pragma unroll
   for (int i = 0; i < RB; ++i) acc[i] = f32x16{};
@@ -107,47 +117,45 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
     for (int i = 0; i < LD_PF; ++i) {
       const int c = c0 + i;
       if (c < nch) {  // block-uniform
-        bf16x8 v0 = ring[i][0], v1 = ring[i][1];
+        bf16x8 xv[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) xv[v] = ring[i][v];
         if (c + LD_PF < nch) {
-          ring[i][0] = *reinterpret_cast<const bf16x8*>(src + (c + LD_PF) * LD_KC);
-          ring[i][1] = *reinterpret_cast<const bf16x8*>(src + (c + LD_PF) * LD_KC + 8);
+#pragma unroll
+          for (int v = 0; v < NV; ++v) ring[i][v] = *reinterpret_cast<const bf16x8*>(src + (c + LD_PF) * KC + 8 * v);
         }
         // buffer c & 1 (c0 is a multiple of LD_PF); the previous reader of this buffer was chunk
         // c - 2, which every wave finished before the barrier of chunk c - 1
-        bf16* xt = xs + (i & 1) * 32 * LD_XS;
+        bf16* xt = xs + (i & 1) * 32 * XS;
         bf16* at = as + (i & 1) * AIMG;
 #pragma unroll
-        for (int j = 0; j < 2 * RB; ++j) *reinterpret_cast<bf16x8*>(at + (ar + 16 * j) * LD_XS + ac) = areg[j];
+        for (int j = 0; j < NA; ++j) *reinterpret_cast<bf16x8*>(at + (ar + (256 / TPA) * j) * XS + ac) = areg[j];
         if (c + 1 < nch) {
 #pragma unroll
-          for (int j = 0; j < 2 * RB; ++j)
-            areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * 16 * P.K + (c + 1) * LD_KC);
+          for (int j = 0; j < NA; ++j)
+            areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * (256 / TPA) * P.K + (c + 1) * KC);
         }
-        if (drop) {
-          drop8(v0, key, eidx + (uint64_t)c * LD_KC, thr, sc);
-          drop8(v1, key, eidx + (uint64_t)c * LD_KC + 8, thr, sc);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          if (drop) drop8(xv[v], key, eidx + (uint64_t)c * KC + 8 * v, thr, sc);
+          if (xdst != nullptr) *reinterpret_cast<bf16x8*>(xdst + c * KC + 8 * v) = xv[v];
+          *reinterpret_cast<bf16x8*>(xt + lr * XS + lc + 8 * v) = xv[v];
         }
-        if (xdst != nullptr) {
-          *reinterpret_cast<bf16x8*>(xdst + c * LD_KC) = v0;
-          *reinterpret_cast<bf16x8*>(xdst + c * LD_KC + 8) = v1;
-        }
-        *reinterpret_cast<bf16x8*>(xt + lr * LD_XS + lc) = v0;
-        *reinterpret_cast<bf16x8*>(xt + lr * LD_XS + lc + 8) = v1;
         __syncthreads();
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const int kk = (2 * w + s2) * 16 + 8 * h;
-          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xt + l32 * LD_XS + kk);
+        for (int s2 = 0; s2 < KSW; ++s2) {
+          const int kk = (KSW * w + s2) * 16 + 8 * h;
+          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xt + l32 * XS + kk);
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb)
-            acc[rb] = mfma32x32x16(*reinterpret_cast<const bf16x8*>(at + (rb * 32 + l32) * LD_XS + kk), xf, acc[rb]);
+            acc[rb] = mfma32x32x16(*reinterpret_cast<const bf16x8*>(at + (rb * 32 + l32) * XS + kk), xf, acc[rb]);
         }
       }
     }
   }
-  // reduce the four waves' k-step partial sums: waves 1-3 -> LDS (over the A images), wave 0 sums
+  // reduce the four waves' k-step partial sums: waves 1-3 -> LDS (over the images), wave 0 sums
   __syncthreads();
-  float* red = reinterpret_cast<float*>(as);  // [3][RB * 16 * 64]
+  float* red = reinterpret_cast<float*>(smem);  // [3][RB * 16 * 64]
   if (w > 0) {
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -156,7 +164,21 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
   }
   __syncthreads();
   const int64_t tok = t0 + l32;
-  if (w == 0 && tok < P.M) {
+  if (w == 0 && tok < P.M && P.ksplit > 1) {
+    float* prow = P.hpart + ((int64_t)ksi * P.M + tok) * R;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int ix = (rb * 16 + 4 * q + j) * 64 + lane;
+          v[j] = acc[rb][4 * q + j] + red[ix] + red[RB * 1024 + ix] + red[2 * RB * 1024 + ix];
+        }
+        *reinterpret_cast<f32x4*>(prow + rb * 32 + 8 * q + 4 * h) = v;
+      }
+  } else if (w == 0 && tok < P.M) {
     bf16* hrow = static_cast<bf16*>(P.h) + tok * (int64_t)R;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -170,6 +192,22 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
         }
         *reinterpret_cast<bf16x4*>(hrow + rb * 32 + 8 * q + 4 * h) = v;
       }
+  }
+}
+
+// h[M][R] = bf16(sum over the ksplit fp32 partials)
+__global__ __launch_bounds__(256) void lora_hsum_kernel(const float* __restrict__ part, bf16* __restrict__ h,
+                                                        int64_t n4, int ksplit, int64_t stride) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    f32x4 a = *reinterpret_cast<const f32x4*>(part + 4 * i);
+    for (int k = 1; k < ksplit; ++k) {
+      const f32x4 b = *reinterpret_cast<const f32x4*>(part + k * stride + 4 * i);
+      a += b;
+    }
+    bf16x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = static_cast<bf16>(a[j]);
+    *reinterpret_cast<bf16x4*>(h + 4 * i) = o;
   }
 }
 
@@ -274,17 +312,39 @@ bool lora_down_supported(int64_t M, int K, int R, int ldx, uint64_t offset) {
   return M > 0 && K % 128 == 0 && R % 32 == 0 && R >= 32 && R <= 256 && ldx % 8 == 0 && offset % 4 == 0;
 }
 
+int lora_down_splits(int64_t M, int K, int cus) {
+  // at least ~3 workgroups per CU (one workgroup = 32 tokens): a single 4-wave workgroup per CU
+  // leaves every per-chunk latency (A chunk from L2, barrier, LDS round trip) exposed
+  const int64_t ntb = (M + 31) / 32;
+  const int nch = K / 128;
+  int64_t ks = (3 * (int64_t)cus + ntb - 1) / ntb;
+  if (ks > nch) ks = nch;
+  if (ks > 16) ks = 16;
+  return ks < 1 ? 1 : (int)ks;
+}
+
 void lora_down(const LoraDownParams& p, hipStream_t s) {
-  const dim3 grid((unsigned)((p.M + 31) / 32)), block(256);
+  const dim3 grid((unsigned)(((p.M + 31) / 32) * p.ksplit)), block(256);
+  // GRT_LORA_DOWN_KC=64: half the LDS per workgroup (two workgroups per CU up to R = 192); measured
+  // neutral on the Llama-2-7B LoRA step (profiles/r2_perf_experiments.md), so 128 by default
+  static const int kc_env = [] { const char* e = getenv("GRT_LORA_DOWN_KC"); return e ? atoi(e) : 0; }();
+  const bool kc64 = kc_env == 64;
+#define GRT_LD(N)                                                                         \
+  case N:                                                                                 \
+    if (kc64) hipLaunchKernelGGL((lora_down_kernel<N, 64>), grid, block, 0, s, p);        \
+    else hipLaunchKernelGGL((lora_down_kernel<N, 128>), grid, block, 0, s, p);            \
+    break;
   switch (p.R / 32) {
-    case 1: hipLaunchKernelGGL(lora_down_kernel<1>, grid, block, 0, s, p); break;
-    case 2: hipLaunchKernelGGL(lora_down_kernel<2>, grid, block, 0, s, p); break;
-    case 3: hipLaunchKernelGGL(lora_down_kernel<3>, grid, block, 0, s, p); break;
-    case 4: hipLaunchKernelGGL(lora_down_kernel<4>, grid, block, 0, s, p); break;
-    case 5: hipLaunchKernelGGL(lora_down_kernel<5>, grid, block, 0, s, p); break;
-    case 6: hipLaunchKernelGGL(lora_down_kernel<6>, grid, block, 0, s, p); break;
-    case 7: hipLaunchKernelGGL(lora_down_kernel<7>, grid, block, 0, s, p); break;
-    default: hipLaunchKernelGGL(lora_down_kernel<8>, grid, block, 0, s, p); break;
+    GRT_LD(1) GRT_LD(2) GRT_LD(3) GRT_LD(4) GRT_LD(5) GRT_LD(6) GRT_LD(7)
+    default: GRT_LD(8)
+  }
+#undef GRT_LD
+  if (p.ksplit > 1) {
+    const int64_t n4 = p.M * (int64_t)p.R / 4;
+    int64_t g = (n4 + 255) / 256;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(lora_hsum_kernel, dim3((unsigned)g), dim3(256), 0, s, p.hpart, static_cast<bf16*>(p.h), n4,
+                       p.ksplit, p.M * (int64_t)p.R);
   }
 }
 

@@ -19,7 +19,6 @@ Documented deviation: one dropout mask per fused input (HF draws separate masks 
 """
 from __future__ import annotations
 
-import functools
 import json
 import math
 import os
@@ -60,15 +59,12 @@ class LoraConfig:
 
 # LoRA adapter kernels (csrc/kernels/lora.hip): dropout + down-projection in one pass over x, and
 # the adapter's dX contribution accumulated in one pass over dX. GRT_LORA_KERNELS=0 -> torch path
-# (=down / =dx: only that kernel).
+# (or a comma list of down, dx: only those kernels).
 _LORA_KERNELS_ENV = os.environ.get("GRT_LORA_KERNELS", "1")
-_LORA_DOWN = _LORA_KERNELS_ENV in ("1", "down")
-_LORA_DX = _LORA_KERNELS_ENV in ("1", "dx")
-
-
-@functools.lru_cache(maxsize=None)
-def _num_cus(dev: torch.device) -> int:
-    return torch.cuda.get_device_properties(dev).multi_processor_count
+_LORA_KINDS = ({"down", "dx"} if _LORA_KERNELS_ENV == "1" else
+               set() if _LORA_KERNELS_ENV == "0" else set(_LORA_KERNELS_ENV.split(",")))
+_LORA_DOWN = "down" in _LORA_KINDS
+_LORA_DX = "dx" in _LORA_KINDS
 
 
 def _base_weight(base: nn.Module) -> torch.Tensor:
@@ -100,11 +96,9 @@ class _LoraFn(torch.autograd.Function):
         y = F.linear(x2, w, bias)
         del w
         acat = torch.cat(As, 0) if k > 1 else As[0]
-        # h = dropout(x) A^T in one pass over x (lora.hip); x_d is kept for the dA GEMM. The kernel
-        # runs one workgroup per 32 tokens, so below 32 tokens per CU (the SFT job's ~2 K-token
-        # steps) the dropout pass + library GEMM fill the chip better.
-        res = (C.lora_down(x2, acat, p, seed, offset, p > 0)
-               if _LORA_DOWN and x2.shape[0] >= 32 * _num_cus(x2.device) else [])
+        # h = dropout(x) A^T in one pass over x (lora.hip; split over K when there are fewer than
+        # ~3 32-token workgroups per CU); x_d is kept for the dA GEMM
+        res = C.lora_down(x2, acat, p, seed, offset, p > 0) if _LORA_DOWN and x2.shape[0] >= 256 else []
         if res:
             h = res[0]
             xd = res[1] if p > 0 else x2
