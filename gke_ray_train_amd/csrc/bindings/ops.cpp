@@ -64,8 +64,10 @@ std::vector<Tensor> rmsnorm_fwd(const Tensor& x, const optional<Tensor>& residua
   return {y, residual.has_value() ? h : x, rstd};
 }
 
+// dw_out given: the weight gradient goes straight into it (parameter dtype, e.g. a data-parallel
+// gradient slot; accumulate adds) and the second result is dw_out itself.
 std::vector<Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& h, const Tensor& w, const Tensor& rstd,
-                                const optional<Tensor>& dres) {
+                                const optional<Tensor>& dres, const optional<Tensor>& dw_out, bool accumulate) {
   check_contig(dy, "dy");
   check_contig(h, "h");
   c10::OptionalDeviceGuard g(dy.device());
@@ -75,12 +77,17 @@ std::vector<Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& h, const Tensor&
     check_contig(*dres, "dres");
     TORCH_CHECK(dres->sizes() == h.sizes() && dres->scalar_type() == h.scalar_type(), "dres mismatch");
   }
+  if (dw_out.has_value()) {
+    check_contig(*dw_out, "dw_out");
+    TORCH_CHECK(dw_out->numel() == d && dw_out->scalar_type() == h.scalar_type(), "dw_out: [d] in the dtype of h");
+  }
   auto dx = at::empty_like(h);
-  auto dw = at::empty({d}, h.options().dtype(at::kFloat));
+  Tensor dw = dw_out.has_value() ? *dw_out : at::empty({d}, h.options().dtype(at::kFloat));
   auto ws = at::empty({grt::norm_bwd_workspace_floats(rows, (int)d)}, h.options().dtype(at::kFloat));
   grt::rmsnorm_bwd(dtype_of(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(),
-                   ptr_or_null(dres), dx.data_ptr(), dw.data_ptr<float>(), ws.data_ptr<float>(), rows,
-                   (int)d, cur_stream(h));
+                   ptr_or_null(dres), dx.data_ptr(), dw_out.has_value() ? nullptr : dw.data_ptr<float>(),
+                   ws.data_ptr<float>(), rows, (int)d, cur_stream(h),
+                   dw_out.has_value() ? dw.data_ptr() : nullptr, accumulate ? 1 : 0);
   return {dx, dw};
 }
 
@@ -771,7 +778,8 @@ void ipc_barrier(const std::vector<int64_t>& staging, const std::vector<int64_t>
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gke_ray_train_amd HIP kernels for gfx950 (MI355X)";
   m.def("rmsnorm_fwd", &rmsnorm_fwd);
-  m.def("rmsnorm_bwd", &rmsnorm_bwd);
+  m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("h"), py::arg("w"), py::arg("rstd"), py::arg("dres"),
+        py::arg("dw_out") = py::none(), py::arg("accumulate") = false);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("swiglu_fwd", &swiglu_fwd);

@@ -17,9 +17,11 @@ void rmsnorm_fwd(DType dt, const void* x, const void* residual, const void* w, v
                  float* rstd, int64_t rows, int d, float eps, hipStream_t s);
 // dx = d/dh (norm) + dres ; dw accumulated through fp32 partials (workspace of
 // rmsnorm_bwd_workspace(rows, d) floats).
+// dw_t != null: the weight gradient is written in the parameter dtype straight into dw_t (a
+// gradient-buffer slot; accumulate != 0 adds to it) instead of dw_f32.
 void rmsnorm_bwd(DType dt, const void* dy, const void* h, const void* w, const float* rstd,
                  const void* dres, void* dx, float* dw_f32, float* ws, int64_t rows, int d,
-                 hipStream_t s);
+                 hipStream_t s, void* dw_t = nullptr, int accumulate = 0);
 int64_t norm_bwd_workspace_floats(int64_t rows, int d);
 void layernorm_fwd(DType dt, const void* x, const void* residual, const void* w, const void* b,
                    void* y, void* h_out, float* mean, float* rstd, int64_t rows, int d, float eps,

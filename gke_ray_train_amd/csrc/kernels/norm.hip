@@ -210,8 +210,11 @@ __global__ __launch_bounds__(kNT) void norm_bwd_kernel(const T* __restrict__ dy,
 // dw[j] = sum_b ws[b][0][j], db[j] = sum_b ws[b][1][j] over ncols (= d for RMSNorm, 2d for
 // LayerNorm). One workgroup = 64 columns x 4 row phases; each thread keeps 4 independent
 // accumulators so the slab loads (256 contiguous bytes per wave) stay in flight.
+// GO: output type of dw / db (float, or bf16 written straight into a gradient buffer; ACC adds
+// to what the buffer holds).
+template <typename GO, bool ACC>
 __global__ __launch_bounds__(kNT) void colsum_kernel(const float* __restrict__ ws, int nb, int d, int ncols,
-                                                     float* __restrict__ dw, float* __restrict__ db) {
+                                                     GO* __restrict__ dw, GO* __restrict__ db) {
   __shared__ float red[4][64];
   const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + c;
@@ -231,8 +234,9 @@ __global__ __launch_bounds__(kNT) void colsum_kernel(const float* __restrict__ w
   __syncthreads();
   if (rg == 0 && j < ncols) {
     const float s = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
-    if (j < d) { if (dw) dw[j] = s; }
-    else { if (db) db[j - d] = s; }
+    GO* out = j < d ? dw : db;
+    const int jj = j < d ? j : j - d;
+    if (out) out[jj] = from_f<GO>(ACC ? to_f(out[jj]) + s : s);
   }
 }
 
@@ -280,7 +284,7 @@ int bwd_blocks(int64_t rows) {
 template <typename T, bool RMS>
 void launch_bwd(const void* dy, const void* h, const void* w, const float* mean, const float* rstd,
                 const void* dres, void* dx, float* dw, float* db, float* ws, int64_t rows, int d,
-                hipStream_t s) {
+                hipStream_t s, void* dw_t = nullptr, int accumulate = 0) {
   constexpr int V = Vec16<T>::N;
   const int per_thr = (d / V + kNT - 1) / kNT;
   const int nb = bwd_blocks(rows);
@@ -300,7 +304,15 @@ void launch_bwd(const void* dy, const void* h, const void* w, const float* mean,
 #undef GRT_NB
 #undef GRT_NB2
   const int ncols = RMS ? d : 2 * d;
-  hipLaunchKernelGGL(colsum_kernel, dim3((ncols + 63) / 64), dim3(kNT), 0, s, ws, nb, d, ncols, dw, db);
+  const dim3 cg((ncols + 63) / 64);
+  if (dw_t != nullptr && RMS) {  // weight gradient in T, straight into its gradient slot
+    if (accumulate)
+      hipLaunchKernelGGL((colsum_kernel<T, true>), cg, dim3(kNT), 0, s, ws, nb, d, ncols, (T*)dw_t, (T*)nullptr);
+    else
+      hipLaunchKernelGGL((colsum_kernel<T, false>), cg, dim3(kNT), 0, s, ws, nb, d, ncols, (T*)dw_t, (T*)nullptr);
+  } else {
+    hipLaunchKernelGGL((colsum_kernel<float, false>), cg, dim3(kNT), 0, s, ws, nb, d, ncols, dw, db);
+  }
 }
 
 }  // namespace
@@ -317,11 +329,11 @@ void rmsnorm_fwd(DType dt, const void* x, const void* residual, const void* w, v
 
 void rmsnorm_bwd(DType dt, const void* dy, const void* h, const void* w, const float* rstd,
                  const void* dres, void* dx, float* dw_f32, float* ws, int64_t rows, int d,
-                 hipStream_t s) {
+                 hipStream_t s, void* dw_t, int accumulate) {
   if (dt == DType::BF16)
-    launch_bwd<bf16, true>(dy, h, w, nullptr, rstd, dres, dx, dw_f32, nullptr, ws, rows, d, s);
+    launch_bwd<bf16, true>(dy, h, w, nullptr, rstd, dres, dx, dw_f32, nullptr, ws, rows, d, s, dw_t, accumulate);
   else
-    launch_bwd<float, true>(dy, h, w, nullptr, rstd, dres, dx, dw_f32, nullptr, ws, rows, d, s);
+    launch_bwd<float, true>(dy, h, w, nullptr, rstd, dres, dx, dw_f32, nullptr, ws, rows, d, s, dw_t, accumulate);
 }
 
 void layernorm_fwd(DType dt, const void* x, const void* residual, const void* w, const void* b,

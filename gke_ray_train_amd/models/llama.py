@@ -162,6 +162,9 @@ class LlamaMLP(nn.Module):
 
 
 class RMSNorm(nn.Module):
+    # the fused HIP backward (ops/fused.py) writes the weight gradient into the data-parallel slot
+    _grt_direct_grad = True
+
     def __init__(self, d, eps, device=None, dtype=None):
         super().__init__()
         self.weight = nn.Parameter(torch.ones(d, device=device, dtype=dtype))

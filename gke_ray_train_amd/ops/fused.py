@@ -7,6 +7,7 @@ missing ``_C.so`` raises, see ``_native.py``); CPU tensors use ``_ref`` so the w
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -32,8 +33,26 @@ class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, rstd = ctx.saved_tensors
-        dx, dw = _native.kernels().rmsnorm_bwd(dy.contiguous(), x, w, rstd, None)
-        return dx, dw.to(w.dtype), None
+        dx, dw = _norm_bwd_into_slot(w, lambda out, acc: _native.kernels().rmsnorm_bwd(
+            dy.contiguous(), x, w, rstd, None, out, acc))
+        return dx, dw, None
+
+
+_NORM_DIRECT_GRAD = os.environ.get("GRT_NORM_DIRECT_GRAD", "1") != "0"
+
+
+def _norm_bwd_into_slot(w, run):
+    """RMSNorm backward whose weight gradient the kernel writes in the parameter dtype straight into
+    the data-parallel gradient slot (``w._grt_slot``, parallel/ddp.py / fsdp.py) -> (dx, None);
+    without a slot -> (dx, dw)."""
+    slot = getattr(w, "_grt_slot", None) if _NORM_DIRECT_GRAD else None
+    if slot is None or not w.requires_grad or slot.view.dtype != w.dtype:
+        dx, dw = run(None, False)
+        return dx, dw.to(w.dtype)
+    res = []
+    slot.write(lambda v: res.append(run(v, False)[0]), lambda v: res.append(run(v, True)[0]))
+    slot.notify(w)
+    return res[0], None
 
 
 class _AddRMSNorm(torch.autograd.Function):
@@ -51,8 +70,8 @@ class _AddRMSNorm(torch.autograd.Function):
         h, w, rstd = ctx.saved_tensors
         dy = torch.zeros_like(h) if dy is None else dy.contiguous()
         dres = None if dh is None else dh.contiguous()
-        dx, dw = _native.kernels().rmsnorm_bwd(dy, h, w, rstd, dres)
-        return dx, dx, dw.to(w.dtype), None
+        dx, dw = _norm_bwd_into_slot(w, lambda out, acc: _native.kernels().rmsnorm_bwd(dy, h, w, rstd, dres, out, acc))
+        return dx, dx, dw, None
 
 
 def rms_norm(x, w, eps=1e-5):

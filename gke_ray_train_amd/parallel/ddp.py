@@ -141,6 +141,8 @@ class DistributedDataParallel(nn.Module):
         for m in module.modules():
             if isinstance(m, (_DirectLinear, _DirectEmbedding)) and m.weight.requires_grad:
                 self._direct.add(id(m.weight))
+            elif getattr(m, "_grt_direct_grad", False) and m.weight.requires_grad:
+                self._direct.add(id(m.weight))  # e.g. RMSNorm: the HIP backward writes the slot
         lm_head = getattr(module, "lm_head", None)
         if isinstance(lm_head, nn.Linear) and lm_head.weight.requires_grad:
             self._direct.add(id(lm_head.weight))
