@@ -416,6 +416,26 @@ void adamw(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const optional<Ten
                   gscale.has_value() ? gscale->data_ptr<float>() : nullptr, cur_stream(p), (int)max_blocks,
                   index_offset);
 }
+// AdamW on a bf16 weight [rows, cols] that also writes pt = W^T [cols, rows] (see optim.hip)
+void adamw_t(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const Tensor& hyper, const optional<Tensor>& gscale,
+             Tensor& pt, int64_t index_offset) {
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&p, &gr, &m, &v, &pt}) check_contig(*t, "adamw_t operand");
+  TORCH_CHECK(p.dim() == 2 && p.size(0) % 64 == 0 && p.size(1) % 64 == 0, "adamw_t: [rows, cols] multiples of 64");
+  TORCH_CHECK(p.scalar_type() == at::kBFloat16 && gr.scalar_type() == at::kBFloat16 && pt.scalar_type() == at::kBFloat16,
+              "adamw_t: bf16 param / grad / transpose");
+  TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat, "adamw_t: fp32 moments");
+  TORCH_CHECK(gr.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "adamw_t: sizes");
+  TORCH_CHECK(pt.dim() == 2 && pt.size(0) == p.size(1) && pt.size(1) == p.size(0), "adamw_t: pt must be [cols, rows]");
+  TORCH_CHECK(hyper.scalar_type() == at::kFloat && hyper.numel() >= 10 && hyper.is_cuda(), "hyper fp32[10] on device");
+  TORCH_CHECK(index_offset >= 0 && index_offset % 4 == 0, "adamw_t: index_offset must be a multiple of 4");
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&p, &gr, &m, &v, &pt})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "adamw_t operands must be 16-byte aligned");
+  c10::OptionalDeviceGuard g(p.device());
+  grt::adamw_t_step(p.data_ptr(), gr.data_ptr(), m.data_ptr<float>(), v.data_ptr<float>(), pt.data_ptr(), p.size(0),
+                    p.size(1), hyper.data_ptr<float>(), gscale.has_value() ? gscale->data_ptr<float>() : nullptr,
+                    cur_stream(p), index_offset);
+}
+
 void scale_(Tensor& x, double a, const optional<Tensor>& a_ptr) {
   check_contig(x, "x");
   c10::OptionalDeviceGuard g(x.device());
@@ -802,6 +822,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("clip_finalize", &clip_finalize);
   m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("master"),
         py::arg("hyper"), py::arg("gscale"), py::arg("max_blocks") = 0, py::arg("index_offset") = 0);
+  m.def("adamw_t", &adamw_t);
   m.def("scale_", &scale_);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("scale"),
         py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);

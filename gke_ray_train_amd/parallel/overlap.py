@@ -16,6 +16,11 @@ coefficient before step t+1 reads it, and ``synchronize()`` (or any device synch
 completes all pending updates, so a timed region that ends with ``torch.cuda.synchronize()``
 contains all of the optimizer work.
 
+The update of each bf16 projection weight (``ops.Linear`` / LM head, dims multiples of 64) also
+writes W^T (``adamw_t``: one extra 2-byte write per parameter inside the HBM-bound pass) and
+registers it, so the next backward's input-gradient GEMM runs in the faster TN form on it
+(``ops.linear.input_grad``); ``GRT_OPT_TRANSPOSE=0`` keeps the plain update.
+
 Ordering hazards and why they are safe:
 * the clip coefficient and gradients of step t are produced on the compute stream before the
   side stream's start event; the next backward overwrites a chunk's gradients only after that
@@ -62,6 +67,24 @@ class OverlappedOptimizer:
                 rng[gi] = [min(lo, off), max(hi, off + n)]
             self.chunks.append((m, [(gi, lo, hi) for gi, (lo, hi) in sorted(rng.items())]))
         self._check_disjoint()
+        # per chunk: the parameters in it, so weights with a transposed copy get their own launch
+        params_of = {id(p): p for g in engine.groups for p in g.params}
+        self._chunk_params: Dict[nn.Module, List[Tuple[int, int, int, torch.Tensor]]] = {}
+        for m, ids in waits.items():
+            self._chunk_params[m] = sorted((flat_ids[i] + (params_of[i],) for i in ids), key=lambda t: (t[0], t[1]))
+        self._wt: Dict[int, torch.Tensor] = {}
+        if os.environ.get("GRT_OPT_TRANSPOSE", "1") != "0" and not optimizer.master_weights:
+            from ..ops.linear import _TRANSPOSED_DGRAD, Linear as _DirectLinear
+            proj = {id(mm.weight) for mm in engine.module.modules() if isinstance(mm, _DirectLinear)}
+            head = getattr(engine.module, "lm_head", None)
+            if isinstance(head, nn.Linear):
+                proj.add(id(head.weight))
+            for g in engine.groups:
+                for p in g.params:
+                    if (_TRANSPOSED_DGRAD and id(p) in proj and p.is_cuda and p.dtype == torch.bfloat16
+                            and g.grad.dtype == torch.bfloat16 and p.dim() == 2 and p.shape[0] % 64 == 0
+                            and p.shape[1] % 64 == 0 and getattr(p, "_grt_slot", None) is not None):
+                        self._wt[id(p)] = torch.empty(p.shape[1], p.shape[0], device=p.device, dtype=p.dtype)
         self._events: Dict[nn.Module, torch.cuda.Event] = {}
         self._stream: Optional[torch.cuda.Stream] = None
         self._hooks = [m.register_forward_pre_hook(self._make_hook(m)) for m, _ in self.chunks]
@@ -117,16 +140,50 @@ class OverlappedOptimizer:
         start.record(cur)
         C = _native.kernels()
         gs = None if grad_scale is None else grad_scale.buf
+        from ..ops.linear import register_transposed
         with torch.cuda.stream(self._stream):
             self._stream.wait_event(start)
             for m, rs in self.chunks:
-                for gi, lo, hi in rs:
-                    p, g, ea, eas, master, hb = per_group[gi]
-                    C.adamw(p.data[lo:hi], g[lo:hi], ea[lo:hi], eas[lo:hi],
-                            None if master is None else master[lo:hi], hb, gs, self.max_blocks, lo)
+                if self._wt:
+                    self._launch_chunk_params(C, m, per_group, gs, register_transposed)
+                else:
+                    for gi, lo, hi in rs:
+                        p, g, ea, eas, master, hb = per_group[gi]
+                        C.adamw(p.data[lo:hi], g[lo:hi], ea[lo:hi], eas[lo:hi],
+                                None if master is None else master[lo:hi], hb, gs, self.max_blocks, lo)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
                 self._events[m] = ev
+
+    def _launch_chunk_params(self, C, m, per_group, gs, register_transposed):
+        """One launch per parameter of the chunk: projection weights through the transposing
+        update (W^T registered for the next backward), runs of the others through the flat one."""
+        run = None  # (gi, lo, hi) of consecutive plain parameters
+
+        def flush():
+            if run is not None:
+                gi, lo, hi = run
+                p, g, ea, eas, master, hb = per_group[gi]
+                C.adamw(p.data[lo:hi], g[lo:hi], ea[lo:hi], eas[lo:hi],
+                        None if master is None else master[lo:hi], hb, gs, self.max_blocks, lo)
+
+        for gi, off, n, prm in self._chunk_params[m]:
+            wt = self._wt.get(id(prm))
+            if wt is None:
+                if run is not None and run[0] == gi and run[2] <= off:
+                    run = (gi, run[1], off + n)
+                else:
+                    flush()
+                    run = (gi, off, off + n)
+                continue
+            flush()
+            run = None
+            p, g, ea, eas, master, hb = per_group[gi]
+            shape = prm.shape
+            C.adamw_t(p.data[off:off + n].view(shape), g[off:off + n].view(shape), ea[off:off + n].view(shape),
+                      eas[off:off + n].view(shape), hb, gs, wt, off)
+            register_transposed(prm, wt)
+        flush()
 
     def state_dict(self):
         self.synchronize()

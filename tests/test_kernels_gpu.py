@@ -305,6 +305,32 @@ def test_adamw_bf16_stochastic_rounding(sr):
     assert abs(mean - (1.0 - 2.0 ** -10)) < 6 * sigma, (mean, 1.0 - 2.0 ** -10)
 
 
+@pytest.mark.parametrize("sr", [0.0, 1.0])
+def test_adamw_t_matches_flat_update_and_transposes(sr):
+    """adamw_t (update of a [rows, cols] weight that also writes W^T) == the flat AdamW kernel on
+    the same data (same rounding stream for a matching index offset), and pt == p^T exactly."""
+    C = _C()
+    torch.manual_seed(8)
+    rows, cols, off = 192, 320, 128
+    p0 = torch.randn(rows, cols, device=DEV).bfloat16()
+    g = torch.randn(rows, cols, device=DEV).bfloat16()
+    m0 = torch.randn(rows, cols, device=DEV).abs() * 0.01
+    v0 = torch.rand(rows, cols, device=DEV) * 1e-3
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.01, 0.1, 0.001, 1.0, sr, 3.0], device=DEV)
+    gsc = torch.tensor([1.0, 0.5], device=DEV)
+    pa, ma, va = p0.clone(), m0.clone(), v0.clone()
+    C.adamw(pa.view(-1), g.view(-1), ma.view(-1), va.view(-1), None, hyper, gsc, 0, off)
+    pb, mb, vb = p0.clone(), m0.clone(), v0.clone()
+    pt = torch.empty(cols, rows, device=DEV, dtype=torch.bfloat16)
+    C.adamw_t(pb, g, mb, vb, hyper, gsc, pt, off)
+    torch.cuda.synchronize()
+    assert torch.equal(pt, pb.t()), "transpose"
+    _close(mb, ma, 1e-7, 1e-6, "adamw_t m")
+    _close(vb, va, 1e-9, 1e-6, "adamw_t v")
+    ulp = (pa.float() - pb.float()).abs() / pa.float().abs().clamp_min(1e-3)
+    assert (ulp > 1e-2).float().mean().item() < 1e-3, "adamw_t params"
+
+
 def test_nf4_roundtrip():
     from gke_ray_train_amd import ops
     from gke_ray_train_amd.ops import _ref

@@ -84,9 +84,13 @@ def test_fsdp_world1_matches_ddp_on_gpu(offload, monkeypatch):
         assert d < 5e-3, (k, d)
 
 
-def test_overlapped_optimizer_matches_serial():
+@pytest.mark.parametrize("transpose", ["0", "1"])
+def test_overlapped_optimizer_matches_serial(transpose, monkeypatch):
     """Chunked AdamW on a side stream, released to each module's forward pre-hook, gives
-    bit-identical parameters and losses to the serial end-of-step update."""
+    bit-identical parameters and losses to the serial end-of-step update. With the transposing
+    update (W^T for the next backward's TN dX GEMM) the input gradients round differently, so
+    losses / parameters agree to bf16 rounding instead of bit for bit."""
+    monkeypatch.setenv("GRT_OPT_TRANSPOSE", transpose)
     from gke_ray_train_amd.models import build_llama
     from gke_ray_train_amd.ops import FusedAdamW, clip_grad_norm_
     from gke_ray_train_amd.parallel import DistributedDataParallel
@@ -99,6 +103,7 @@ def test_overlapped_optimizer_matches_serial():
         if overlap:
             opt = OverlappedOptimizer(ddp, opt)
             assert len(opt.chunks) == m.config.num_hidden_layers + 3  # embed, layers, norm, head
+            assert bool(opt._wt) == (transpose == "1")
         g = torch.Generator(device="cuda").manual_seed(9)
         losses = []
         for _ in range(4):
@@ -114,9 +119,16 @@ def test_overlapped_optimizer_matches_serial():
             opt.synchronize()
         torch.cuda.synchronize()
         runs.append((losses, {k: v.clone() for k, v in m.state_dict().items()}))
-    assert runs[0][0] == runs[1][0]
-    for k, v in runs[0][1].items():
-        assert torch.equal(v, runs[1][1][k]), k
+    if transpose == "0":
+        assert runs[0][0] == runs[1][0]
+        for k, v in runs[0][1].items():
+            assert torch.equal(v, runs[1][1][k]), k
+    else:
+        for a, b in zip(runs[0][0], runs[1][0]):
+            assert abs(a - b) < 1e-3 * abs(a), (runs[0][0], runs[1][0])
+        for k, v in runs[0][1].items():
+            d = (v.float() - runs[1][1][k].float()).abs().max().item()
+            assert d < 2e-2 * max(1.0, v.float().abs().max().item()), (k, d)
 
 
 def test_sequence_parallel_single_rank_matches_plain_on_gpu():
