@@ -51,6 +51,8 @@ class GradSlot:
 
 
 _WGRAD_NATIVE = os.environ.get("GRT_WGRAD_GEMM", "1") != "0"
+# weight gradients with K <= N as transposes + TN library GEMM (see wgrad); GRT_WGRAD_TN=0 -> MFMA kernel
+_WGRAD_TN = os.environ.get("GRT_WGRAD_TN", "1") != "0"
 
 
 # dX = dY W through the TN library kernel on a contiguous W^T (13-15 % faster than the NN form on
@@ -149,7 +151,24 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor = None, accumul
     if _WGRAD_NATIVE and dy2.is_cuda and dy2.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 \
             and out.dtype == torch.bfloat16:
         from .. import _native
-        if _native.kernels().gemm_wgrad(dy2, x2, out, accumulate):
+        C = _native.kernels()
+        M, N, K = dy2.shape[0], dy2.shape[1], x2.shape[1]
+        if (_WGRAD_TN and K <= N and M % 64 == 0 and N % 64 == 0 and K % 64 == 0 and dy2.is_contiguous()
+                and x2.is_contiguous() and out.is_contiguous()):
+            # token-major operands are the layout every GEMM handles worst (~1.1 PF): transpose
+            # both (HIP, HBM-bound) and run the forward-like TN GEMM (~1.6 PF);
+            # tools/wgrad_transpose_ab.py: qkv 714 -> 617 us, o 242 -> 221, gate_up 1362 -> 1287,
+            # LM head 1880 -> 1594 incl. the transposes; down (K > N) stays on the MFMA kernel
+            dyt = torch.empty(N, M, device=dy2.device, dtype=dy2.dtype)
+            xt = torch.empty(K, M, device=x2.device, dtype=x2.dtype)
+            C.transpose_into(dy2, dyt)
+            C.transpose_into(x2, xt)
+            if accumulate:
+                out.addmm_(dyt, xt.t())
+            else:
+                torch.mm(dyt, xt.t(), out=out)
+            return out
+        if C.gemm_wgrad(dy2, x2, out, accumulate):
             return out
     if accumulate:
         out.addmm_(dy2.t(), x2)
