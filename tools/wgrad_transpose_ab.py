@@ -41,7 +41,7 @@ def time_it(fn, iters=6):
     return s.elapsed_time(e) / iters * 1000
 
 
-res = {n: {"grt": [], "tn": [], "tn+tr": [], "tr": []} for n in cases}
+res = {n: {"grt": [], "tn": [], "tn+tr": [], "tr": [], "dyT_only": [], "xT_only": []} for n in cases}
 for rnd in range(5):
     for n, c in cases.items():
         res[n]["grt"].append(time_it(lambda: C.gemm_wgrad(c["dy"], c["x"], c["out"], False)))
@@ -49,6 +49,8 @@ for rnd in range(5):
         C.transpose_into(c["x"], c["xt"])
         res[n]["tn"].append(time_it(lambda: torch.mm(c["dyt"], c["xt"].t(), out=c["out"])))
         res[n]["tr"].append(time_it(lambda: (C.transpose_into(c["dy"], c["dyt"]), C.transpose_into(c["x"], c["xt"]))))
+        res[n]["dyT_only"].append(time_it(lambda: torch.mm(c["dyt"], c["x"], out=c["out"])))
+        res[n]["xT_only"].append(time_it(lambda: torch.mm(c["dy"].t(), c["xt"].t(), out=c["out"])))
         res[n]["tn+tr"].append(time_it(lambda: (C.transpose_into(c["dy"], c["dyt"]), C.transpose_into(c["x"], c["xt"]),
                                                 torch.mm(c["dyt"], c["xt"].t(), out=c["out"]))))
 # numerics: both layouts give the same product
