@@ -420,7 +420,7 @@ void adamw(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const optional<Ten
 void adamw_t(Tensor& p, const Tensor& gr, Tensor& m, Tensor& v, const Tensor& hyper, const optional<Tensor>& gscale,
              Tensor& pt, int64_t index_offset) {
   for (const Tensor* t : std::initializer_list<const Tensor*>{&p, &gr, &m, &v, &pt}) check_contig(*t, "adamw_t operand");
-  TORCH_CHECK(p.dim() == 2 && p.size(0) % 64 == 0 && p.size(1) % 64 == 0, "adamw_t: [rows, cols] multiples of 64");
+  TORCH_CHECK(p.dim() == 2 && p.size(0) % 64 == 0 && p.size(1) % 128 == 0, "adamw_t: rows % 64 == 0, cols % 128 == 0");
   TORCH_CHECK(p.scalar_type() == at::kBFloat16 && gr.scalar_type() == at::kBFloat16 && pt.scalar_type() == at::kBFloat16,
               "adamw_t: bf16 param / grad / transpose");
   TORCH_CHECK(m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat, "adamw_t: fp32 moments");

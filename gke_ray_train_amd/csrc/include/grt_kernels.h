@@ -81,7 +81,7 @@ void clip_coef_finalize(const float* ws, int nparts, float max_norm, float presc
 void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
                 int64_t n, const float* hyper, const float* grad_scale_ptr, hipStream_t s, int max_blocks = 0,
                 int64_t index_offset = 0);  // element index of p[0] in its flat buffer (stochastic rounding)
-// AdamW of one bf16 weight [rows][cols] (bf16 grad, fp32 moments, no master; rows, cols % 64 == 0)
+// AdamW of one bf16 weight [rows][cols] (bf16 grad, fp32 moments, no master; rows % 64, cols % 128 == 0)
 // that also writes its transpose pt [cols][rows]; ioff = flat index of p[0] (stochastic rounding).
 void adamw_t_step(void* p, const void* g, float* m, float* v, void* pt, int64_t rows, int64_t cols,
                   const float* hyper, const float* grad_scale_ptr, hipStream_t s, int64_t ioff);

@@ -169,15 +169,21 @@ __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* 
 // writes W^T [cols][rows] — the operand of the next backward's TN input-gradient GEMM (13-15 %
 // faster than the NN form on the Llama shapes, profiles/r1_dgrad_layout_ab.jsonl) — so the
 // transpose costs one extra 2-byte write per parameter inside a pass that is HBM-bound anyway.
-// One workgroup = a 64 x 64 tile: 8 threads per 64-element row (full 128 B lines), the updated tile
-// is staged in LDS and written back transposed with 32 B row segments. Same update, stochastic
-// rounding and random stream (flat index ioff + row * cols + col) as adamw_kernel.
+// One workgroup = a 64 x 128 tile: 4 threads per 256-byte row segment, the updated tile staged in
+// LDS and written back transposed with 32 B row segments. Same update, stochastic rounding and
+// random stream (flat index ioff + row * cols + col) as adamw_kernel.
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_o;
+__device__ __forceinline__ int oswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int ooff(int row, int ch) { return row * 256 + 16 * (ch ^ oswz(row)); }
+
+// tile = 64 rows x 128 columns (cols % 128 == 0); the updated tile goes into the XOR-swizzled LDS
+// image of transpose.hip and is read back transposed with ds_read_b64_tr_b16.
 __global__ __launch_bounds__(kNT) void adamw_t_kernel(bf16* __restrict__ p, const bf16* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       bf16* __restrict__ pt, int64_t rows, int64_t cols,
                                                       const float* __restrict__ hyper,
                                                       const float* __restrict__ gsp, uint64_t ioff) {
-  __shared__ bf16 tile[64][64 + 8];
+  __shared__ __attribute__((aligned(16))) char img[64 * 256];
   const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float bc1 = hyper[5], bc2 = hyper[6];
   const float gs = hyper[7] * (gsp ? gsp[1] : 1.f);
@@ -186,13 +192,14 @@ __global__ __launch_bounds__(kNT) void adamw_t_kernel(bf16* __restrict__ p, cons
   const float decay = 1.f - lr * wd;
   const bool sr = hyper[8] != 0.f;
   const uint64_t srkey = hash_u64(0x5352ull ^ ((uint64_t)hyper[9] << 20));
-  const int64_t ntc = cols / 64;
+  const int64_t ntc = cols / 128;
   const int64_t tr = blockIdx.x / ntc, tc = blockIdx.x % ntc;
-  const int tid = threadIdx.x, rr = tid >> 3, cc = (tid & 7) * 8;
+  // 4 threads per 256-byte row; per k the 4 threads take 4 adjacent 16-byte chunks (coalesced)
+  const int tid = threadIdx.x, row = tid >> 2;
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    const int r = rr + 32 * pass;
-    const int64_t o = (tr * 64 + r) * cols + tc * 64 + cc;
+  for (int k = 0; k < 4; ++k) {
+    const int ch = (tid & 3) + 4 * k;
+    const int64_t o = (tr * 64 + row) * cols + tc * 128 + ch * 8;
     const bf16x8 pv = *reinterpret_cast<const bf16x8*>(p + o);
     const bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + o);
     f32x4 mv[2] = {*reinterpret_cast<const f32x4*>(m + o), *reinterpret_cast<const f32x4*>(m + o + 4)};
@@ -202,13 +209,13 @@ __global__ __launch_bounds__(kNT) void adamw_t_kernel(bf16* __restrict__ p, cons
     for (int hh = 0; hh < 2; ++hh) {
       const uint64_t hsh = hash_u64(srkey ^ ((ioff + (uint64_t)o + 4 * hh) >> 2));
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = 4 * hh + k;
+      for (int q = 0; q < 4; ++q) {
+        const int e = 4 * hh + q;
         const float gf = to_f(gv[e]) * gs;
-        mv[hh][k] = b1 * mv[hh][k] + (1.f - b1) * gf;
-        vv[hh][k] = b2 * vv[hh][k] + (1.f - b2) * gf * gf;
-        const float pf = to_f(pv[e]) * decay - step * mv[hh][k] / (sqrtf(vv[hh][k]) * rbc2 + eps);
-        out[e] = sr ? sr_bf16(pf, (uint32_t)(hsh >> (16 * k)) & 0xffffu) : from_f<bf16>(pf);
+        mv[hh][q] = b1 * mv[hh][q] + (1.f - b1) * gf;
+        vv[hh][q] = b2 * vv[hh][q] + (1.f - b2) * gf * gf;
+        const float pf = to_f(pv[e]) * decay - step * mv[hh][q] / (sqrtf(vv[hh][q]) * rbc2 + eps);
+        out[e] = sr ? sr_bf16(pf, (uint32_t)(hsh >> (16 * q)) & 0xffffu) : from_f<bf16>(pf);
       }
     }
     *reinterpret_cast<f32x4*>(m + o) = mv[0];
@@ -216,20 +223,25 @@ __global__ __launch_bounds__(kNT) void adamw_t_kernel(bf16* __restrict__ p, cons
     *reinterpret_cast<f32x4*>(v + o) = vv[0];
     *reinterpret_cast<f32x4*>(v + o + 4) = vv[1];
     *reinterpret_cast<bf16x8*>(p + o) = out;
-    *reinterpret_cast<bf16x8*>(&tile[r][cc]) = out;
+    *reinterpret_cast<bf16x8*>(img + ooff(row, ch)) = out;
   }
   __syncthreads();
-  // W^T tile: output row j (a column of W) = tile[0..63][j]; thread: row j = tid >> 2, 16 entries
-  const int j = tid >> 2, i0 = (tid & 3) * 16;
-  bf16x8 a, b;
+  // W^T: lane i of a 16-lane group gets column cb + i of 4 rows per transposed read
+  const int l16 = tid & 15, grp = tid >> 4;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    a[e] = tile[i0 + e][j];
-    b[e] = tile[i0 + 8 + e][j];
+  for (int pp = 0; pp < 2; ++pp) {
+    const int pr = grp + 16 * pp;
+    const int cb = 16 * (pr >> 2), rb = 16 * (pr & 3);
+    bf16x4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rr = rb + 4 * k + (l16 >> 2), col = cb + 4 * (l16 & 3);
+      q[k] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_o*)(img + ooff(rr, col >> 3) + 8 * ((col >> 2) & 1)));
+    }
+    bf16* d = pt + (tc * 128 + cb + l16) * rows + tr * 64 + rb;
+    *reinterpret_cast<bf16x8*>(d) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<bf16x8*>(d + 8) = __builtin_shufflevector(q[2], q[3], 0, 1, 2, 3, 4, 5, 6, 7);
   }
-  bf16* dst = pt + (tc * 64 + j) * rows + tr * 64 + i0;
-  *reinterpret_cast<bf16x8*>(dst) = a;
-  *reinterpret_cast<bf16x8*>(dst + 8) = b;
 }
 
 template <typename T>
@@ -280,7 +292,7 @@ void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v
 
 void adamw_t_step(void* p, const void* g, float* m, float* v, void* pt, int64_t rows, int64_t cols,
                   const float* hyper, const float* gsp, hipStream_t s, int64_t ioff) {
-  const dim3 grid((unsigned)((rows / 64) * (cols / 64)));
+  const dim3 grid((unsigned)((rows / 64) * (cols / 128)));
   hipLaunchKernelGGL(adamw_t_kernel, grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, (bf16*)pt, rows,
                      cols, hyper, gsp, (uint64_t)ioff);
 }

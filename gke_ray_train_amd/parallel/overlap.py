@@ -83,7 +83,7 @@ class OverlappedOptimizer:
                 for p in g.params:
                     if (_TRANSPOSED_DGRAD and id(p) in proj and p.is_cuda and p.dtype == torch.bfloat16
                             and g.grad.dtype == torch.bfloat16 and p.dim() == 2 and p.shape[0] % 64 == 0
-                            and p.shape[1] % 64 == 0 and getattr(p, "_grt_slot", None) is not None):
+                            and p.shape[1] % 128 == 0 and getattr(p, "_grt_slot", None) is not None):
                         self._wt[id(p)] = torch.empty(p.shape[1], p.shape[0], device=p.device, dtype=p.dtype)
         self._events: Dict[nn.Module, torch.cuda.Event] = {}
         self._stream: Optional[torch.cuda.Stream] = None

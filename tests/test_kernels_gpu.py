@@ -311,7 +311,7 @@ def test_adamw_t_matches_flat_update_and_transposes(sr):
     the same data (same rounding stream for a matching index offset), and pt == p^T exactly."""
     C = _C()
     torch.manual_seed(8)
-    rows, cols, off = 192, 320, 128
+    rows, cols, off = 192, 384, 128
     p0 = torch.randn(rows, cols, device=DEV).bfloat16()
     g = torch.randn(rows, cols, device=DEV).bfloat16()
     m0 = torch.randn(rows, cols, device=DEV).abs() * 0.01
