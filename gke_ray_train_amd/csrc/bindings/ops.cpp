@@ -793,6 +793,35 @@ void ipc_barrier(const std::vector<int64_t>& staging, const std::vector<int64_t>
   grt::ipc_barrier(p, (uint32_t)epoch, cur_stream(err));
 }
 
+// A HIP stream whose dispatches may only use the CUs set in `mask` (32 CUs per word). Used for
+// side-stream work (the overlapped optimizer) that must leave the other CUs to the compute
+// stream's GEMMs instead of filling every CU's wave slots. Returned as an integer handle for
+// torch.cuda.ExternalStream; it lives for the process (streams are few and reused).
+int64_t cu_masked_stream(const std::vector<int64_t>& mask, int64_t device) {
+  TORCH_CHECK(!mask.empty(), "cu_masked_stream: empty mask");
+  std::vector<uint32_t> words(mask.size());
+  bool any = false;
+  for (size_t i = 0; i < mask.size(); ++i) {
+    TORCH_CHECK(mask[i] >= 0 && mask[i] <= 0xffffffffLL, "cu_masked_stream: mask word out of range");
+    words[i] = (uint32_t)mask[i];
+    any = any || words[i] != 0;
+  }
+  TORCH_CHECK(any, "cu_masked_stream: mask selects no CU");
+  c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words.size(), words.data());
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+  return reinterpret_cast<int64_t>(s);
+}
+
+std::vector<int64_t> stream_cu_mask(int64_t stream, int64_t words) {
+  TORCH_CHECK(words > 0 && words <= 64, "stream_cu_mask: 1..64 words");
+  std::vector<uint32_t> w((size_t)words, 0u);
+  const hipError_t e = hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), (uint32_t)words, w.data());
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamGetCUMask: ", hipGetErrorString(e));
+  return std::vector<int64_t>(w.begin(), w.end());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -846,6 +875,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ipc_close", &ipc_close);
   m.def("ipc_allreduce", &ipc_allreduce);
   m.def("ipc_barrier", &ipc_barrier);
+  m.def("cu_masked_stream", &cu_masked_stream);
+  m.def("stream_cu_mask", &stream_cu_mask);
   m.attr("IPC_MAX_RANKS") = grt::kIpcMaxRanks;
   m.attr("IPC_SIGNAL_BYTES") = grt::kIpcSignalBytes;
 }

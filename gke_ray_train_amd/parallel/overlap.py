@@ -106,6 +106,16 @@ class OverlappedOptimizer:
                 torch.cuda.current_stream().wait_event(ev)
         return hook
 
+    @staticmethod
+    def _make_stream(dev):
+        """The update's side stream: confined to GRT_OPT_CUS CUs (``ops/streams.py``) so the
+        forward GEMMs keep the rest of the chip; 0 = an ordinary stream on every CU."""
+        n = int(os.environ.get("GRT_OPT_CUS", "0"))
+        if n > 0:
+            from ..ops.streams import cu_masked_stream
+            return cu_masked_stream(n, dev, os.environ.get("GRT_OPT_CU_PATTERN", "spread"))
+        return torch.cuda.Stream(dev)
+
     @property
     def param_groups(self):
         return self.opt.param_groups
@@ -135,7 +145,7 @@ class OverlappedOptimizer:
             per_group.append(w)
         cur = torch.cuda.current_stream(dev)
         if self._stream is None:
-            self._stream = torch.cuda.Stream(dev)
+            self._stream = self._make_stream(dev)
         start = torch.cuda.Event()
         start.record(cur)
         C = _native.kernels()
