@@ -257,7 +257,8 @@ def main():
     prof = None
     if a.profile_dir and rank == 0:
         from torch.profiler import ProfilerActivity, profile
-        prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA])
+        stacks = os.environ.get("GRT_PROFILE_STACKS", "0") == "1"  # attribute kernels to Python call sites
+        prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=stacks, with_stack=stacks)
         prof.__enter__()
     t0 = time.perf_counter()
     for i in range(a.steps):
@@ -277,6 +278,8 @@ def main():
         prof.export_chrome_trace(os.path.join(a.profile_dir, "trace.json"))
         with open(os.path.join(a.profile_dir, "kernels.txt"), "w") as f:
             f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=60))
+            if stacks:
+                f.write("\n\n" + prof.key_averages(group_by_stack_n=6).table(sort_by="cuda_time_total", row_limit=80))
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], device=dev if not cpu else "cpu", dtype=torch.float64)

@@ -143,6 +143,8 @@ class DistributedDataParallel(nn.Module):
                 self._direct.add(id(m.weight))
             elif getattr(m, "_grt_direct_grad", False) and m.weight.requires_grad:
                 self._direct.add(id(m.weight))  # e.g. RMSNorm: the HIP backward writes the slot
+            if hasattr(m, "direct_grad_params"):  # e.g. LoRA adapters (peft/lora.py)
+                self._direct.update(id(p) for p in m.direct_grad_params() if p.requires_grad)
         lm_head = getattr(module, "lm_head", None)
         if isinstance(lm_head, nn.Linear) and lm_head.weight.requires_grad:
             self._direct.add(id(lm_head.weight))

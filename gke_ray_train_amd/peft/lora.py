@@ -79,8 +79,43 @@ def _base_input_grad(base: nn.Module, dy2: torch.Tensor) -> torch.Tensor:
     return input_grad(dy2, base.weight)
 
 
+# LoRA gradients written by the adapter GEMMs straight into the data-parallel gradient slots
+# (``p._grt_slot``, parallel/ddp.py / fsdp.py) instead of returned to autograd (AccumulateGrad copy
+# + the engine's copy into the flat buffer, ~450 small kernels per Llama-2-7B step); the scaling is
+# folded into the GEMMs' alpha. GRT_LORA_DIRECT_GRAD=0 -> autograd accumulation.
+_LORA_DIRECT_GRAD = os.environ.get("GRT_LORA_DIRECT_GRAD", "1") != "0"
+
+
+def _packed(ts):
+    """(order, view) when the 2-D tensors ``ts`` (same shape[1]) lie back to back in one buffer:
+    ``view`` is their row concatenation in memory order ``order`` — no copy. Else None.
+    The data-parallel engines flatten parameters (and their gradient slots) contiguously, so the
+    A matrices of one adapted projection are normally adjacent (in reverse registration order)."""
+    if len(ts) == 1:
+        return [0], ts[0]
+    t0 = ts[0]
+    if any(t.dim() != 2 or t.shape[1] != t0.shape[1] or t.dtype != t0.dtype or not t.is_contiguous()
+           or t.untyped_storage().data_ptr() != t0.untyped_storage().data_ptr() for t in ts):
+        return None
+    order = sorted(range(len(ts)), key=lambda i: ts[i].data_ptr())
+    for i, j in zip(order, order[1:]):
+        if ts[j].data_ptr() != ts[i].data_ptr() + ts[i].numel() * ts[i].element_size():
+            return None
+    first = ts[order[0]]
+    rows = sum(t.shape[0] for t in ts)
+    return order, first.as_strided((rows, first.shape[1]), (first.shape[1], 1))
+
+
+def _slot_of(p):
+    return getattr(p, "_grt_slot", None) if _LORA_DIRECT_GRAD and p.requires_grad else None
+
+
 class _LoraFn(torch.autograd.Function):
-    """y = base(x) + scaling * sum_i  B_i A_i dropout(x)  (placed at target i's output columns)."""
+    """y = base(x) + scaling * sum_i  B_i A_i dropout(x)  (placed at target i's output columns).
+
+    Targets are processed in the memory order of their A matrices (``_packed``): A_cat is then a
+    view of the flat parameter buffer, h's column blocks follow that order, and dA_cat = g^T x_d is
+    one GEMM written into the (equally adjacent) gradient slots."""
 
     @staticmethod
     def forward(ctx, x, base, spec, r, scaling, p, seed, offset, *ab):
@@ -95,7 +130,11 @@ class _LoraFn(torch.autograd.Function):
         bias = getattr(base, "bias", None)
         y = F.linear(x2, w, bias)
         del w
-        acat = torch.cat(As, 0) if k > 1 else As[0]
+        pk = _packed(As)
+        if pk is None:
+            order, acat = list(range(k)), torch.cat(As, 0)
+        else:
+            order, acat = pk
         # h = dropout(x) A^T in one pass over x (lora.hip; split over K when there are fewer than
         # ~3 32-token workgroups per CU); x_d is kept for the dA GEMM
         res = C.lora_down(x2, acat, p, seed, offset, p > 0) if _LORA_DOWN and x2.shape[0] >= 256 else []
@@ -105,17 +144,21 @@ class _LoraFn(torch.autograd.Function):
         else:
             xd = C.dropout_fwd_seeded(x2, p, seed, offset) if p > 0 else x2
             h = xd @ acat.t()                               # [M, r * k]
-        for i, (off, n) in enumerate(spec):                 # GEMM epilogue accumulates into y
-            y[:, off:off + n].addmm_(h[:, i * r:(i + 1) * r], Bs[i].t(), alpha=scaling)
+        for j, i in enumerate(order):                       # GEMM epilogue accumulates into y
+            off, n = spec[i]
+            y[:, off:off + n].addmm_(h[:, j * r:(j + 1) * r], Bs[i].t(), alpha=scaling)
         ctx.base, ctx.spec, ctx.r, ctx.scaling, ctx.p, ctx.seed, ctx.offset = base, spec, r, scaling, p, seed, offset
+        ctx.order = order
         ctx.xshape = x.shape
-        ctx.save_for_backward(xd, h, acat, *Bs)
+        ctx.save_for_backward(xd, h, acat, *As, *Bs)
         return y.view(*x.shape[:-1], y.shape[-1])
 
     @staticmethod
     def backward(ctx, dy):
-        xd, h, acat, *Bs = ctx.saved_tensors
-        spec, r, s = ctx.spec, ctx.r, ctx.scaling
+        xd, h, acat, *ab = ctx.saved_tensors
+        spec, r, s, order = ctx.spec, ctx.r, ctx.scaling, ctx.order
+        k = len(spec)
+        As, Bs = ab[:k], ab[k:]
         C = _native.kernels()
         dy2 = dy.reshape(-1, dy.shape[-1])
         if dy2.dtype != acat.dtype:
@@ -123,13 +166,44 @@ class _LoraFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _base_input_grad(ctx.base, dy2)           # base dX (frozen weight)
-        gs, dBs = [], []
-        for i, (off, n) in enumerate(spec):
+        # g = dL/dh = s * dY_i B_i per target, into its column block (alpha = s, no scaled copy of B)
+        g = torch.zeros(dy2.shape[0], r * k, device=dy2.device, dtype=dy2.dtype)
+        dBs: List[Optional[torch.Tensor]] = [None] * k
+        for j, i in enumerate(order):
+            off, n = spec[i]
             dyi = dy2[:, off:off + n]
-            gs.append(dyi @ (Bs[i] * s))                     # dL/dh_i  [M, r]
-            dBs.append((dyi.t() @ h[:, i * r:(i + 1) * r]).mul_(s))
-        g = torch.cat(gs, 1) if len(gs) > 1 else gs[0]       # [M, r * k]
-        dacat = g.t() @ xd                                   # [r * k, in]
+            hj = h[:, j * r:(j + 1) * r]
+            g[:, j * r:(j + 1) * r].addmm_(dyi, Bs[i], alpha=s)
+            sl = _slot_of(Bs[i])
+            if sl is not None:                               # dB_i = s dY_i^T h_i into the slot
+                sl.write(lambda v: v.addmm_(dyi.t(), hj, beta=0.0, alpha=s), lambda v: v.addmm_(dyi.t(), hj, alpha=s))
+                sl.notify(Bs[i])
+            else:
+                dBs[i] = torch.mm(dyi.t(), hj).mul_(s)
+        dAs: List[Optional[torch.Tensor]] = [None] * k
+        aslots = [_slot_of(As[i]) for i in order]
+        pk = None
+        if all(sl is not None for sl in aslots) and len({sl.fresh for sl in aslots}) == 1:
+            pk = _packed([sl.view for sl in aslots])
+        if pk is not None and pk[0] == list(range(k)):      # slots adjacent in the same order
+            dst = pk[1]
+            if aslots[0].fresh:
+                dst.addmm_(g.t(), xd, beta=0.0)
+            else:
+                dst.addmm_(g.t(), xd)
+            for sl, i in zip(aslots, order):
+                sl.fresh, sl.direct = False, True
+                sl.notify(As[i])
+        else:
+            dacat = g.t() @ xd                               # [r * k, in]
+            for j, i in enumerate(order):
+                rows = dacat[j * r:(j + 1) * r]
+                sl = aslots[j]
+                if sl is not None:
+                    sl.write(lambda v: v.copy_(rows), lambda v: v.add_(rows))
+                    sl.notify(As[i])
+                else:
+                    dAs[i] = rows
         if dx is not None:
             # dx += drop'(g A): one read-modify-write of dx (lora.hip), else GEMM + dropout backward
             if not (_LORA_DX and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
@@ -138,7 +212,6 @@ class _LoraFn(torch.autograd.Function):
                 else:
                     dx.addmm_(g, acat)
             dx = dx.view(ctx.xshape)
-        dAs = [dacat[i * r:(i + 1) * r] for i in range(len(spec))]
         return (dx, None, None, None, None, None, None, None, *dAs, *dBs)
 
 
@@ -165,6 +238,10 @@ class LoraLinear(nn.Module):
             self.lora_B[name] = nn.Parameter(torch.zeros(n, cfg.r, device=dev, dtype=dt))
         self.full_cover = (len(self.targets) == 1 and self.targets[0][1] == 0 and
                            self.targets[0][2] == self.out_features)
+
+    def direct_grad_params(self) -> List[nn.Parameter]:
+        """Parameters whose gradient the GPU backward writes into the engine's slot itself."""
+        return list(self.lora_A.values()) + list(self.lora_B.values())
 
     def forward(self, x):
         if x.is_cuda:

@@ -1,4 +1,5 @@
 """Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op."""
+import contextlib
 import math
 
 import pytest
@@ -519,12 +520,18 @@ def test_embedding_module_autograd(monkeypatch):
     _close(e.weight.grad, ref, 2e-2, 2e-2, "Embedding module grad")
 
 
+@pytest.mark.parametrize("engine", ["none", "ddp", "ddp_accum"])
 @pytest.mark.parametrize("targets", ["qv", "qkv"])
 @pytest.mark.parametrize("nf4", [False, True])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_fused_lora_matches_reference(nf4, p, targets):
+def test_fused_lora_matches_reference(nf4, p, targets, engine):
     """The fused LoRA op (epilogue accumulation, seeded dropout regenerated in backward, in-place
-    dX accumulation) equals the unfused formula y = W x + s * B_i A_i drop(x) per target slice."""
+    dX accumulation) equals the unfused formula y = W x + s * B_i A_i drop(x) per target slice.
+    engine=ddp: the adapters sit in the DDP flat buffers, so A_cat is a view of them and dA / dB are
+    written by the GEMMs straight into the gradient slots; ddp_accum: two micro-steps (the first
+    under no_sync) accumulate into the slots."""
+    if engine == "ddp_accum" and p > 0:
+        pytest.skip("accumulation is checked without dropout (one mask per micro-step)")
     from gke_ray_train_amd.ops.linear import Linear
     from gke_ray_train_amd.peft.lora import LoraConfig, LoraLinear
     from gke_ray_train_amd.peft.quant import BitsAndBytesConfig, NF4Linear
@@ -543,10 +550,24 @@ def test_fused_lora_matches_reference(nf4, p, targets):
             mod.lora_B[n].normal_(0, 0.05)
     x = torch.randn(4, 64, 256, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     from gke_ray_train_amd.ops import _ref
+    fwd, eng, reps = mod, None, 1
+    if engine != "none":
+        from gke_ray_train_amd.parallel import DistributedDataParallel
+        fwd = eng = DistributedDataParallel(mod)
+        reps = 2 if engine == "ddp_accum" else 1
     rng = torch.get_rng_state()
-    y = mod(x)
-    dy = torch.randn_like(y)
-    (y.float() * dy.float()).sum().backward()
+    dy = None
+    for rep in range(reps):
+        ctx = eng.no_sync(rep < reps - 1) if eng is not None else contextlib.nullcontext()
+        with ctx:
+            y = fwd(x)
+            dy = torch.randn_like(y) if dy is None else dy
+            (y.float() * dy.float()).sum().backward()
+    if eng is not None:
+        eng.finish_gradient_sync()
+        assert all(getattr(q, "_grt_slot", None) is not None for q in mod.direct_grad_params())
+        from gke_ray_train_amd.peft.lora import _packed
+        assert _packed([mod.lora_A[n] for n in names]) is not None  # the no-copy A_cat view path ran
     # reference in fp32; the mask from the host reimplementation of the hash with the seed the op
     # drew from torch's CPU generator (ops/fused.py::dropout_seed_offset)
     torch.set_rng_state(rng)
@@ -566,11 +587,12 @@ def test_fused_lora_matches_reference(nf4, p, targets):
         yr[:, off:off + 256] = yr[:, off:off + 256] + cfg.scaling * (xd @ A[n].t()) @ B[n].t()
     (yr * dy.view(-1, 768).float()).sum().backward()
     _close(y.view(-1, 768), yr, 3e-2, 3e-2, "lora y")
-    _close(x.grad.view(-1, 256), x2.grad, 3e-2, 3e-2, "lora dx")
+    _close(x.grad.view(-1, 256), reps * x2.grad, 3e-2, 3e-2, "lora dx")
     for n in names:
         # adapter grads are reductions over all tokens of bf16 intermediates (as in PEFT under bf16):
         # compare by relative Frobenius error
         for got, ref, what in ((mod.lora_A[n].grad, A[n].grad, "dA"), (mod.lora_B[n].grad, B[n].grad, "dB")):
+            ref = reps * ref
             rel = (got.float() - ref).norm() / ref.norm().clamp_min(1e-6)
             assert rel < 2e-2, f"lora {what} {n}: rel err {rel.item():.3g}"
 
