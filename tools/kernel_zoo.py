@@ -78,7 +78,34 @@ m = torch.zeros(n, device=dev)
 vv = torch.zeros(n, device=dev)
 hyper = torch.tensor([1e-4, 0.9, 0.999, 1e-8, 0.0, 0.1, 0.001, 1.0, 0.0, 1.0], device=dev)
 rep(lambda: C.adamw(p, g, m, vv, None, hyper, None))
+# gradient sum of squares (grad-norm partials) over the same 512 M bf16 elements
+ws = torch.zeros(C.sumsq_blocks(), device=dev)
+rep(lambda: C.sumsq(g, ws, 0))
 del p, g, m, vv
+
+# transposing AdamW on one down-projection weight [4096, 11008] (+ W^T side output)
+pw = torch.randn(d, f, device=dev, dtype=bf)
+gw = torch.randn(d, f, device=dev, dtype=bf)
+mw, vw = torch.zeros(d, f, device=dev), torch.zeros(d, f, device=dev)
+wt = torch.empty(f, d, device=dev, dtype=bf)
+rep(lambda: C.adamw_t(pw, gw, mw, vw, hyper, None, wt, 0))
+del pw, gw, mw, vw, wt
+
+# weight-gradient operand transpose (down-projection input [8192, 11008])
+xs = torch.randn(T, f, device=dev, dtype=bf)
+xt = torch.empty(f, T, device=dev, dtype=bf)
+rep(lambda: C.transpose_into(xs, xt))
+del xs, xt
+
+# LoRA adapter kernels at the Llama-2-7B fused-qkv shape (r 64 x 3 targets, dropout 0.1)
+xl = torch.randn(T, d, device=dev, dtype=bf)
+al = torch.randn(192, d, device=dev, dtype=bf) * 0.02
+rep(lambda: C.lora_down(xl, al, 0.1, 1234, 0, True))
+gl = torch.randn(T, 192, device=dev, dtype=bf)
+dxl = torch.randn(T, d, device=dev, dtype=bf)
+alt = al.t().contiguous()
+rep(lambda: C.lora_dx(gl, alt, dxl, 0.1, 1234, 0, True))
+del xl, al, gl, dxl, alt
 
 # decode: GEMV (gate_up of Llama-3.1-8B, 1 token) and split-K decode attention (4K context)
 xw = torch.randn(1, 4096, device=dev, dtype=bf)
