@@ -199,6 +199,35 @@ std::vector<Tensor> rope_fwd(const Tensor& qkv, const Tensor& cos, const Tensor&
   return {q, k};
 }
 
+// decode: q = rope(q) [T, hq, D]; kc[t / tpr, pos[t]] = rope(k), vc[t / tpr, pos[t]] = v (caches
+// [B, L, hkv, D], last dim contiguous); a token whose position is outside [0, min(S, L)) is skipped
+// entirely by the kernel (no cache write, its q row left unwritten)
+Tensor rope_append(const Tensor& qkv, const Tensor& cos, const Tensor& sin, const Tensor& pos, int64_t hq, int64_t hkv,
+                   int64_t D, int64_t S, Tensor& kc, Tensor& vc, int64_t tpr) {
+  check_cuda(qkv, "qkv");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.stride(1) == 1 && qkv.scalar_type() == at::kBFloat16, "qkv must be bf16 [T, ld]");
+  c10::OptionalDeviceGuard g(qkv.device());
+  const int64_t T = qkv.size(0), ld = qkv.stride(0);
+  TORCH_CHECK(qkv.size(1) >= (hq + 2 * hkv) * D && D % 16 == 0, "qkv too narrow / head dim");
+  TORCH_CHECK(ld % 8 == 0 && reinterpret_cast<uintptr_t>(qkv.data_ptr()) % 16 == 0, "qkv alignment");
+  check_rope(cos, sin, pos, T, S, D);
+  for (const Tensor* c : {&kc, &vc}) {
+    check_cuda(*c, "cache");
+    TORCH_CHECK(c->dim() == 4 && c->size(2) == hkv && c->size(3) == D && c->stride(3) == 1 &&
+                c->scalar_type() == at::kBFloat16, "cache must be bf16 [B, L, hkv, D] with unit last stride");
+    TORCH_CHECK(c->stride(0) % 8 == 0 && c->stride(1) % 8 == 0 && c->stride(2) % 8 == 0 &&
+                reinterpret_cast<uintptr_t>(c->data_ptr()) % 16 == 0, "cache alignment");
+  }
+  TORCH_CHECK(tpr >= 1 && T % tpr == 0 && T / tpr == kc.size(0) && vc.sizes() == kc.sizes(),
+              "rope_append: T = B * tokens-per-row");
+  auto q = at::empty({T, hq, D}, qkv.options());
+  grt::rope_append(qkv.data_ptr(), ld, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), kc.stride(0), kc.stride(1),
+                   kc.stride(2), vc.stride(0), vc.stride(1), vc.stride(2), cos.data_ptr<float>(), sin.data_ptr<float>(),
+                   pos.data_ptr<int32_t>(), T, (int)tpr, (int)S, (int)kc.size(1), (int)hq, (int)hkv, (int)D,
+                   cur_stream(qkv));
+  return q;
+}
+
 void rope_bwd(const Tensor& dq, const Tensor& dk, Tensor& dqkv, const Tensor& cos, const Tensor& sin,
               const optional<Tensor>& pos, int64_t hq, int64_t hkv, int64_t D, int64_t S) {
   check_contig(dq, "dq");
@@ -642,10 +671,12 @@ void transpose_into(const Tensor& src, Tensor& dst) {
   grt::transpose_bf16(src.data_ptr(), dst.data_ptr(), (int)R, (int)Cc, cur_stream(src));
 }
 
-Tensor gemv(const Tensor& x, const Tensor& w) {
+// y = x W^T for 1-4 rows; swiglu: x = [gate | up] [M, 2K] -> y = (silu(gate) * up) W^T
+Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
   check_cuda(x, "x");
   check_contig(w, "w");
-  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "gemv: x [M, K], w [N, K]");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == (swiglu ? 2 : 1) * w.size(1),
+              swiglu ? "gemv_swiglu: gu [M, 2K], w [N, K]" : "gemv: x [M, K], w [N, K]");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "gemv: bf16");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
   TORCH_CHECK(M >= 1 && M <= 4, "gemv: 1..4 rows");
@@ -655,7 +686,8 @@ Tensor gemv(const Tensor& x, const Tensor& w) {
   TORCH_CHECK(N <= INT32_MAX && K <= INT32_MAX, "gemv: dims");
   c10::OptionalDeviceGuard g(x.device());
   Tensor y = at::empty({M, N}, x.options());
-  grt::gemv_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), N, (int)M, (int)N, (int)K, cur_stream(x));
+  grt::gemv_bf16(x.data_ptr(), x.stride(0), w.data_ptr(), y.data_ptr(), N, (int)M, (int)N, (int)K, cur_stream(x),
+                 swiglu);
   return y;
 }
 
@@ -837,6 +869,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd", &gelu_bwd);
   m.def("rope_fwd", &rope_fwd);
   m.def("rope_bwd", &rope_bwd);
+  m.def("rope_append", &rope_append);
   m.def("scale_add_pe", &scale_add_pe);
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
@@ -862,7 +895,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);
   m.def("transpose_into", &transpose_into);
-  m.def("gemv", &gemv);
+  m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("attn_decode", &attn_decode);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

@@ -44,6 +44,11 @@ void rope_fwd(DType dt, const void* qkv, int64_t ld, void* q_out, void* k_out, c
               const float* sin, const int32_t* pos, int64_t T, int S, int hq, int hkv, int D,
               hipStream_t s);
 // Inverse rotation of dq/dk, written into the q and k column ranges of dqkv (row stride ld).
+// decode: rotate q (-> q_out [T, hq, D]) and k of each token, write k and v at cache slot pos[t] of
+// row t / tpr of kc / vc (bf16)
+void rope_append(const void* qkv, int64_t ld, void* q_out, void* kc, void* vc, int64_t c_bs, int64_t c_ss,
+                 int64_t c_hs, int64_t v_bs, int64_t v_ss, int64_t v_hs, const float* cos, const float* sin,
+                 const int32_t* pos, int64_t T_, int tpr, int S, int L, int hq, int hkv, int D, hipStream_t s);
 void rope_bwd(DType dt, const void* dq, const void* dk, void* dqkv, int64_t ld, const float* cos,
               const float* sin, const int32_t* pos, int64_t T, int S, int hq, int hkv, int D,
               hipStream_t s);
@@ -190,7 +195,9 @@ void transpose_bf16(const void* src, void* dst, int rows, int cols, hipStream_t 
 
 // ---------------- decode GEMV (gemv.hip) ----------------
 // y[m][n] = sum_k x[m][k] * w[n][k] for m < M <= 4; bf16, K % 8 == 0, rows 16-byte aligned
-void gemv_bf16(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int M, int N, int K, hipStream_t s);
+// swiglu: x is the fused [gate | up] output [M, 2K] and the GEMV input is silu(gate) * up
+void gemv_bf16(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int M, int N, int K, hipStream_t s,
+               bool swiglu = false);
 
 // ---------------- xGMI peer-to-peer collectives (ipc_comm.hip) ----------------
 constexpr int kIpcMaxRanks = 8;

@@ -121,18 +121,37 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(const AttnDecode
   }
 }
 
+// One workgroup per (batch, query head), one thread per head dim. The NS <= 64 partial states are
+// loaded by the lanes of wave 0 in parallel (max / weight / sum by butterflies, weights to LDS),
+// then every thread sums its dimension over the splits with independent loads — two dependent
+// round trips instead of a serial NS-long chain.
 __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const AttnDecodeParams p) {
+  __shared__ float wts[64];
+  __shared__ float lsum;
   const int bhq = blockIdx.x, d = threadIdx.x;
   const int b = bhq / p.Hq, hq = bhq % p.Hq;
   const int64_t base = (int64_t)bhq * p.NS;
-  float mm = -INFINITY;
-  for (int s = 0; s < p.NS; ++s) mm = fmaxf(mm, p.part_m[base + s]);
-  float ll = 0.f, oo = 0.f;
-  for (int s = 0; s < p.NS; ++s) {
-    const float a = mm == -INFINITY ? 0.f : fast_exp2(p.part_m[base + s] - mm);
-    ll += p.part_l[base + s] * a;
-    oo += p.part_o[(base + s) * D + d] * a;
+  if (threadIdx.x < 64) {
+    const int s = threadIdx.x;
+    const bool ok = s < p.NS;
+    const float ms = ok ? p.part_m[base + s] : -INFINITY;
+    const float ls = ok ? p.part_l[base + s] : 0.f;
+    float mm = ms;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mm = fmaxf(mm, __shfl_xor(mm, off, 64));
+    const float a = (mm == -INFINITY || !ok) ? 0.f : fast_exp2(ms - mm);
+    float ll = ls * a;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ll += __shfl_xor(ll, off, 64);
+    wts[s] = a;
+    if (s == 0) lsum = ll;
   }
+  __syncthreads();
+  const float* po = p.part_o + base * D + d;
+  float oo = 0.f;
+#pragma unroll 8
+  for (int s = 0; s < p.NS; ++s) oo = fmaf(po[(int64_t)s * D], wts[s], oo);
+  const float ll = lsum;
   bf16* op = (bf16*)p.o + (int64_t)b * p.o_bs + (int64_t)hq * p.o_hs + d;
   *op = static_cast<bf16>(ll > 0.f ? oo / ll : 0.f);
 }

@@ -155,6 +155,57 @@ __global__ __launch_bounds__(kNT) void rope_kernel(const T* __restrict__ src_q, 
   }
 }
 
+// ------------------------- decode: RoPE + KV-cache append ------------------
+// The cached-decode step's q / k rotation and the cache writes in one launch: token t (batch row
+// t / tpr) at position pos[t] has its q heads rotated into q_out and its rotated k heads and raw v
+// heads written at cache slot pos[t] of kc / vc ([B, L, Hkv, D] with strides). A token whose position
+// is outside the rope table or the cache is skipped entirely (no write), so a bad position cannot
+// write out of bounds.
+template <typename T>
+__global__ __launch_bounds__(kNT) void rope_append_kernel(const T* __restrict__ qkv, int64_t ld, T* __restrict__ q_out,
+                                                          T* __restrict__ kc, T* __restrict__ vc, int64_t c_bs,
+                                                          int64_t c_ss, int64_t c_hs, int64_t v_bs, int64_t v_ss,
+                                                          int64_t v_hs, const float* __restrict__ cosb,
+                                                          const float* __restrict__ sinb, const int32_t* __restrict__ pos,
+                                                          int64_t T_, int tpr, int S, int L, int hq, int hkv, int D) {
+  const int half = D / 2;
+  const int gpp = half / 8;
+  const int heads = hq + 2 * hkv;
+  const int64_t total = T_ * heads * gpp;
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < total; i += (int64_t)gridDim.x * kNT) {
+    const int g = (int)(i % gpp);
+    const int64_t th = i / gpp;
+    const int h = (int)(th % heads);
+    const int64_t t = th / heads;
+    const int p = pos[t];
+    if (p < 0 || p >= S || p >= L) continue;
+    const int64_t b = t / tpr;
+    const T* src = qkv + t * ld + (int64_t)h * D;
+    const int c = g * 8;
+    float x1[8], x2[8], o1[8], o2[8];
+    load16(src + c, x1);
+    load16(src + half + c, x2);
+    T* dst;
+    if (h < hq + hkv) {
+      float cs[8], sn[8];
+      load16(cosb + (int64_t)p * half + c, cs); load16(cosb + (int64_t)p * half + c + 4, cs + 4);
+      load16(sinb + (int64_t)p * half + c, sn); load16(sinb + (int64_t)p * half + c + 4, sn + 4);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        o1[k] = x1[k] * cs[k] - x2[k] * sn[k];
+        o2[k] = x2[k] * cs[k] + x1[k] * sn[k];
+      }
+      dst = h < hq ? q_out + (t * hq + h) * (int64_t)D : kc + b * c_bs + (int64_t)p * c_ss + (int64_t)(h - hq) * c_hs;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { o1[k] = x1[k]; o2[k] = x2[k]; }
+      dst = vc + b * v_bs + (int64_t)p * v_ss + (int64_t)(h - hq - hkv) * v_hs;
+    }
+    store16(dst + c, o1);
+    store16(dst + half + c, o2);
+  }
+}
+
 // ------------------------- embedding scale + sinusoidal PE ------------------
 template <typename T>
 __global__ __launch_bounds__(kNT) void scale_add_pe_kernel(const T* __restrict__ emb, const float* __restrict__ pe,
@@ -311,6 +362,14 @@ void rope_fwd(DType dt, const void* qkv, int64_t ld, void* q_out, void* k_out, c
       (int64_t)hkv * D, cos, sin, pos, T_, S, hq, hkv, D)
   GRT_DISPATCH(dt, K, 0);
 #undef K
+}
+void rope_append(const void* qkv, int64_t ld, void* q_out, void* kc, void* vc, int64_t c_bs, int64_t c_ss,
+                 int64_t c_hs, int64_t v_bs, int64_t v_ss, int64_t v_hs, const float* cos, const float* sin,
+                 const int32_t* pos, int64_t T_, int tpr, int S, int L, int hq, int hkv, int D, hipStream_t s) {
+  const int64_t work = T_ * (hq + 2 * hkv) * (D / 16);
+  hipLaunchKernelGGL(rope_append_kernel<bf16>, dim3(grid_for(work)), dim3(kNT), 0, s, (const bf16*)qkv, ld,
+                     (bf16*)q_out, (bf16*)kc, (bf16*)vc, c_bs, c_ss, c_hs, v_bs, v_ss, v_hs, cos, sin, pos, T_, tpr,
+                     S, L, hq, hkv, D);
 }
 void rope_bwd(DType dt, const void* dq, const void* dk, void* dqkv, int64_t ld, const float* cos,
               const float* sin, const int32_t* pos, int64_t T_, int S, int hq, int hkv, int D,

@@ -47,21 +47,43 @@ def _layer_step(layer, h, residual, B, S, pos0, cos, sin, cache: KVCache, li: in
     qkv = attn.qkv_proj(x)
     hq, hkv, D = attn.hq, attn.hkv, attn.hd
     pos = torch.arange(pos0, pos0 + S, device=h.device, dtype=torch.int32).repeat(B)
-    if qkv.is_cuda and qkv.dtype == torch.bfloat16 and D == 128:
-        q, k = _native.kernels().rope_fwd(qkv.contiguous(), cos, sin, pos, hq, hkv, D, cos.shape[0])
+    if _fused_ok(qkv, cache, li):
+        # RoPE of q / k and the cache append of k / v in one kernel (rope_append, elementwise.hip)
+        q = _native.kernels().rope_append(qkv.contiguous(), cos, sin, pos, hq, hkv, D, cos.shape[0],
+                                          cache.k[li], cache.v[li], S)
     else:
         x3 = qkv.view(B * S, hq + 2 * hkv, D)
         q = _ref.apply_rope(x3[:, :hq], cos, sin, pos)
         k = _ref.apply_rope(x3[:, hq:hq + hkv], cos, sin, pos)
-    v = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:]
-    cache.k[li][:, pos0:pos0 + S] = k.view(B, S, hkv, D)
-    cache.v[li][:, pos0:pos0 + S] = v
+        v = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:]
+        cache.k[li][:, pos0:pos0 + S] = k.view(B, S, hkv, D)
+        cache.v[li][:, pos0:pos0 + S] = v
     kk = cache.k[li][:, :pos0 + S]
     vv = cache.v[li][:, :pos0 + S]
     o = ops.flash_attention(q.view(B, S, hq, D), kk, vv, causal=True)
     h = attn.o_proj(o.reshape(B * S, hq * D))
     x, residual = ops.add_rms_norm(h, residual, layer.post_attention_layernorm.weight, eps)
-    return layer.mlp(x), residual
+    return _mlp(layer.mlp, x), residual
+
+
+def _fused_ok(qkv, cache: KVCache, li: int) -> bool:
+    return (qkv.is_cuda and qkv.dtype == torch.bfloat16 and cache.k[li].dtype == torch.bfloat16
+            and qkv.shape[-1] % 8 == 0 and _native.kernels_available())
+
+
+def _mlp(mlp, x):
+    """Decode MLP: for 1-4 tokens the down projection is a GEMV whose input SwiGLU is computed on
+    the fly from the fused gate/up output (gemv.hip, one launch instead of SwiGLU + GEMV)."""
+    from ..ops import linear as _lin
+    down = mlp.down_proj
+    if (_lin._GEMV and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[0] <= 4 and type(down) is _lin.Linear
+            and down.bias is None and down.weight.dtype == torch.bfloat16 and down.weight.is_contiguous()
+            and down.in_features % 8 == 0 and not torch.is_grad_enabled()):
+        gu = mlp.gate_up_proj(x)
+        if gu.is_contiguous() and gu.data_ptr() % 16 == 0 and gu.shape[-1] == 2 * down.in_features:
+            return _native.kernels().gemv(gu, down.weight, swiglu=True)
+        return down(ops.swiglu(gu))
+    return mlp(x)
 
 
 @torch.no_grad()
@@ -91,14 +113,13 @@ def _graph_layer_step(layer, h, residual, B, cos, sin, cache: KVCache, li: int, 
         x, residual = ops.add_rms_norm(h, residual, layer.input_layernorm.weight, eps)
     qkv = attn.qkv_proj(x)
     hq, hkv, D = attn.hq, attn.hkv, attn.hd
-    q, k = _native.kernels().rope_fwd(qkv.contiguous(), cos, sin, pos_b, hq, hkv, D, cos.shape[0])
-    v = qkv.view(B, 1, hq + 2 * hkv, D)[:, :, hq + hkv:]
-    cache.k[li].index_copy_(1, pos_l, k.view(B, 1, hkv, D))
-    cache.v[li].index_copy_(1, pos_l, v)
+    # the new token's position is its cache slot (pos_b == pos_l for every row)
+    q = _native.kernels().rope_append(qkv.contiguous(), cos, sin, pos_b, hq, hkv, D, cos.shape[0],
+                                      cache.k[li], cache.v[li], 1)
     o = ops.flash_attention(q.view(B, 1, hq, D), cache.k[li], cache.v[li], causal=False, seqlens_k=lens)
     h = attn.o_proj(o.reshape(B, hq * D))
     x, residual = ops.add_rms_norm(h, residual, layer.post_attention_layernorm.weight, eps)
-    return layer.mlp(x), residual
+    return _mlp(layer.mlp, x), residual
 
 
 class GraphDecoder:

@@ -694,6 +694,54 @@ def test_gemv_decode(M, N, K):
     assert y2.shape == (M, 1, N) and torch.equal(y2.view(M, N), y)
 
 
+@pytest.mark.parametrize("M", [1, 3])
+@pytest.mark.parametrize("N,K", [(4096, 14336), (12288, 1024), (37, 264)])
+def test_gemv_swiglu_decode(M, N, K):
+    """Down-projection GEMV with the SwiGLU of the fused gate/up output folded in (both the
+    K-split (N <= 8192) and the one-wave-per-row variants) == swiglu kernel + GEMV == fp32 math."""
+    from gke_ray_train_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(M * N + K)
+    gu = torch.randn(M, 2 * K, device=DEV, dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16, generator=g) * 0.02
+    y = _C().gemv(gu, w, swiglu=True)
+    with torch.no_grad():
+        a = ops.swiglu(gu)
+    _close(y, _C().gemv(a, w), 1e-2, 1e-2, "gemv_swiglu vs swiglu + gemv")
+    gf = gu.float()
+    ref = (torch.nn.functional.silu(gf[:, :K]) * gf[:, K:]) @ w.float().t()
+    _close(y, ref, 2e-2, 2e-2, "gemv_swiglu vs fp32")
+
+
+@pytest.mark.parametrize("B,S,hq,hkv,L,start", [(1, 1, 32, 8, 64, 17), (2, 5, 8, 8, 40, 3), (3, 4, 4, 1, 10, 8)])
+def test_rope_append(B, S, hq, hkv, L, start):
+    """Decode RoPE + KV-cache append (rope_append, elementwise.hip) == rope_fwd + cache slice writes;
+    positions past the cache are skipped, every other slot is untouched."""
+    from gke_ray_train_amd.ops import _ref
+    C, D = _C(), 128
+    g = torch.Generator(device=DEV).manual_seed(B * S + hq)
+    qkv = torch.randn(B * S, (hq + 2 * hkv) * D, device=DEV, dtype=torch.bfloat16, generator=g)
+    # rope table longer than the cache: positions past the cache are valid rope positions (q is
+    # still rotated) whose k / v writes the kernel must skip
+    St = start + S + 4
+    cos, sin = _ref.rope_tables(St, D, 10000.0, device=DEV)
+    pos = torch.arange(start, start + S, device=DEV, dtype=torch.int32).repeat(B)
+    kc = torch.randn(B, L, hkv, D, device=DEV, dtype=torch.bfloat16, generator=g)
+    vc = torch.randn(B, L, hkv, D, device=DEV, dtype=torch.bfloat16, generator=g)
+    kc0, vc0 = kc.clone(), vc.clone()
+    q = C.rope_append(qkv, cos, sin, pos, hq, hkv, D, St, kc, vc, S)
+    x3 = qkv.view(B * S, hq + 2 * hkv, D)
+    qr = _ref.apply_rope(x3[:, :hq], cos, sin, pos)
+    kr = _ref.apply_rope(x3[:, hq:hq + hkv], cos, sin, pos)
+    n = max(0, min(S, L - start))  # slots written
+    qv = q.view(B, S, hq, D)[:, :n]  # q rows of skipped positions are not written
+    _close(qv, qr.view(B, S, hq, D)[:, :n], 1e-2, 1e-2, "rope_append q")
+    ke, ve = kc0.clone(), vc0.clone()
+    ke[:, start:start + n] = kr.view(B, S, hkv, D)[:, :n]
+    ve[:, start:start + n] = x3[:, hq + hkv:].reshape(B, S, hkv, D)[:, :n]
+    _close(kc, ke, 1e-2, 1e-2, "rope_append k cache")
+    assert torch.equal(vc, ve), "rope_append v cache"
+
+
 @pytest.mark.parametrize("B,Sk,hq,hkv,pad", [(1, 1, 4, 4, False), (1, 600, 32, 8, False), (3, 77, 8, 1, True),
                                              (2, 1300, 16, 8, True), (2, 33, 8, 4, False)])
 def test_decode_attention(B, Sk, hq, hkv, pad):
