@@ -13,6 +13,8 @@
 //      with the clip coefficient read from device memory.
 // Hyper-parameters come from a small device array so lr schedules do not bake into a captured
 // hipGraph. Optimizer state is always fp32 ("32-bit" AdamW); params may be bf16 or fp32.
+#include <cstdlib>
+
 #include "grt_common.h"
 #include "grt_kernels.h"
 
@@ -67,12 +69,26 @@ __device__ __forceinline__ bf16 sr_bf16(float x, uint32_t r16) {
   return static_cast<bf16>(__uint_as_float(t));  // exact: the low 16 bits are zero
 }
 
-template <typename P, typename G>
+// One AdamW element update with its fused multiply-adds spelled out, so every kernel variant (8- /
+// 4-wide, scalar tail, transposing) rounds identically whatever the compiler would contract.
+__device__ __forceinline__ float adam_elem(float p, float gf, float& m, float& v, float b1, float b2, float rbc2,
+                                           float eps, float decay, float step) {
+  m = fmaf(b1, m, (1.f - b1) * gf);
+  v = fmaf(b2, v, (1.f - b2) * gf * gf);
+  const float denom = fmaf(sqrtf(v), rbc2, eps);
+  return fmaf(p, decay, -(step * m / denom));
+}
+
+// V elements per thread and iteration: 8 (16-byte loads of bf16 p / g, two float4 of m / v; needs
+// 16-byte aligned operands) or 4 (the fallback for 8-byte aligned bf16 slices).
+template <typename P, typename G, int V>
 __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     float* __restrict__ master, int64_t n,
                                                     const float* __restrict__ hyper,
                                                     const float* __restrict__ gsp, uint64_t ioff) {
+  static_assert(V == 4 || V == 8, "V");
+  constexpr int Q = V / 4;  // float4 groups per iteration
   const float lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const float bc1 = hyper[5], bc2 = hyper[6];
   const float gs = hyper[7] * (gsp ? gsp[1] : 1.f);
@@ -82,79 +98,131 @@ __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* 
   // bf16 parameters without an fp32 master copy: stochastic rounding of the updated value
   // (hyper[8] != 0; hyper[9] = step). Updates below half a bf16 ulp (lr 2e-5 on |w| ~ 1e-2) would
   // otherwise round away entirely; SR keeps every update in expectation.
-  // The random bits are a hash of (step, element index + ioff): a launch over a slice of a flat
-  // buffer (the overlapped optimizer's per-module chunks) rounds exactly like one over the whole.
+  // The random bits are a hash of (step, element index + ioff), one 64-bit hash per 4 elements: a
+  // launch over a slice of a flat buffer (the overlapped optimizer's per-module chunks) or with
+  // another V rounds exactly like one over the whole.
   const bool sr = sizeof(P) == 2 && master == nullptr && hyper[8] != 0.f;
   const uint64_t srkey = hash_u64(0x5352ull ^ ((uint64_t)hyper[9] << 20));
-  const int64_t n4 = n / 4;
+  const int64_t nv = n / V;
   const int64_t stride = (int64_t)gridDim.x * kNT;
-  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n4; i += stride) {
-    const int64_t o = i * 4;
-    f32x4 mv = *reinterpret_cast<const f32x4*>(m + o);
-    f32x4 vv = *reinterpret_cast<const f32x4*>(v + o);
-    float pf[4], gf[4];
+  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < nv; i += stride) {
+    const int64_t o = i * V;
+    f32x4 mv[Q], vv[Q];
+    float pf[V], gf[V];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      mv[q] = *reinterpret_cast<const f32x4*>(m + o + 4 * q);
+      vv[q] = *reinterpret_cast<const f32x4*>(v + o + 4 * q);
+    }
     if (master) {
-      f32x4 t = *reinterpret_cast<const f32x4*>(master + o);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pf[k] = t[k];
+      for (int q = 0; q < Q; ++q) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(master + o + 4 * q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pf[4 * q + k] = t[k];
+      }
     } else if constexpr (sizeof(P) == 2) {
-      bf16x4 t = *reinterpret_cast<const bf16x4*>(p + o);
+      if constexpr (V == 8) {
+        const bf16x8 t = *reinterpret_cast<const bf16x8*>(p + o);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pf[k] = to_f(t[k]);
+        for (int k = 0; k < 8; ++k) pf[k] = to_f(t[k]);
+      } else {
+        const bf16x4 t = *reinterpret_cast<const bf16x4*>(p + o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pf[k] = to_f(t[k]);
+      }
     } else {
-      f32x4 t = *reinterpret_cast<const f32x4*>(p + o);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) pf[k] = t[k];
+      for (int q = 0; q < Q; ++q) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(p + o + 4 * q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) pf[4 * q + k] = t[k];
+      }
     }
     if constexpr (sizeof(G) == 2) {
-      bf16x4 t = *reinterpret_cast<const bf16x4*>(g + o);
+      if constexpr (V == 8) {
+        const bf16x8 t = *reinterpret_cast<const bf16x8*>(g + o);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) gf[k] = to_f(t[k]) * gs;
+        for (int k = 0; k < 8; ++k) gf[k] = to_f(t[k]) * gs;
+      } else {
+        const bf16x4 t = *reinterpret_cast<const bf16x4*>(g + o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gf[k] = to_f(t[k]) * gs;
+      }
     } else {
-      f32x4 t = *reinterpret_cast<const f32x4*>(g + o);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) gf[k] = t[k] * gs;
+      for (int q = 0; q < Q; ++q) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(g + o + 4 * q);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gf[4 * q + k] = t[k] * gs;
+      }
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      mv[k] = b1 * mv[k] + (1.f - b1) * gf[k];
-      vv[k] = b2 * vv[k] + (1.f - b2) * gf[k] * gf[k];
-      const float denom = sqrtf(vv[k]) * rbc2 + eps;
-      pf[k] = pf[k] * decay - step * mv[k] / denom;
+    for (int q = 0; q < Q; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = 4 * q + k;
+        float mk = mv[q][k], vk = vv[q][k];
+        pf[e] = adam_elem(pf[e], gf[e], mk, vk, b1, b2, rbc2, eps, decay, step);
+        mv[q][k] = mk;
+        vv[q][k] = vk;
+      }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      *reinterpret_cast<f32x4*>(m + o + 4 * q) = mv[q];
+      *reinterpret_cast<f32x4*>(v + o + 4 * q) = vv[q];
     }
-    *reinterpret_cast<f32x4*>(m + o) = mv;
-    *reinterpret_cast<f32x4*>(v + o) = vv;
     if (master) {
-      f32x4 t;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) t[k] = pf[k];
-      *reinterpret_cast<f32x4*>(master + o) = t;
+      for (int q = 0; q < Q; ++q) {
+        f32x4 t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = pf[4 * q + k];
+        *reinterpret_cast<f32x4*>(master + o + 4 * q) = t;
+      }
     }
     if constexpr (sizeof(P) == 2) {
-      bf16x4 t;
-      if (sr) {
-        const uint64_t h = hash_u64(srkey ^ ((ioff + (uint64_t)o) >> 2));
+      bf16 t[V];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = sr_bf16(pf[k], (uint32_t)(h >> (16 * k)) & 0xffffu);
-      } else {
+      for (int q = 0; q < Q; ++q) {
+        if (sr) {
+          const uint64_t h = hash_u64(srkey ^ ((ioff + (uint64_t)(o + 4 * q)) >> 2));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = from_f<bf16>(pf[k]);
+          for (int k = 0; k < 4; ++k) t[4 * q + k] = sr_bf16(pf[4 * q + k], (uint32_t)(h >> (16 * k)) & 0xffffu);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) t[4 * q + k] = from_f<bf16>(pf[4 * q + k]);
+        }
       }
-      *reinterpret_cast<bf16x4*>(p + o) = t;
-    } else {
-      f32x4 t;
+      if constexpr (V == 8) {
+        bf16x8 tv;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) t[k] = pf[k];
-      *reinterpret_cast<f32x4*>(p + o) = t;
+        for (int k = 0; k < 8; ++k) tv[k] = t[k];
+        *reinterpret_cast<bf16x8*>(p + o) = tv;
+      } else {
+        bf16x4 tv;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) tv[k] = t[k];
+        *reinterpret_cast<bf16x4*>(p + o) = tv;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        f32x4 t;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = pf[4 * q + k];
+        *reinterpret_cast<f32x4*>(p + o + 4 * q) = t;
+      }
     }
   }
-  // scalar tail (n % 4)
-  for (int64_t j = n4 * 4 + (int64_t)blockIdx.x * kNT + threadIdx.x; j < n; j += stride) {
+  // scalar tail (n % V)
+  for (int64_t j = nv * V + (int64_t)blockIdx.x * kNT + threadIdx.x; j < n; j += stride) {
     float pf = master ? master[j] : to_f(p[j]);
     const float gf = to_f(g[j]) * gs;
-    m[j] = b1 * m[j] + (1.f - b1) * gf;
-    v[j] = b2 * v[j] + (1.f - b2) * gf * gf;
-    pf = pf * decay - step * m[j] / (sqrtf(v[j]) * rbc2 + eps);
+    float mj = m[j], vj = v[j];
+    pf = adam_elem(pf, gf, mj, vj, b1, b2, rbc2, eps, decay, step);
+    m[j] = mj;
+    v[j] = vj;
     if (master) master[j] = pf;
     if constexpr (sizeof(P) == 2) {
       p[j] = sr ? sr_bf16(pf, (uint32_t)(hash_u64(srkey ^ ((ioff + (uint64_t)j) >> 2)) >> (16 * ((ioff + j) & 3))) & 0xffffu)
@@ -212,9 +280,10 @@ __global__ __launch_bounds__(kNT) void adamw_t_kernel(bf16* __restrict__ p, cons
       for (int q = 0; q < 4; ++q) {
         const int e = 4 * hh + q;
         const float gf = to_f(gv[e]) * gs;
-        mv[hh][q] = b1 * mv[hh][q] + (1.f - b1) * gf;
-        vv[hh][q] = b2 * vv[hh][q] + (1.f - b2) * gf * gf;
-        const float pf = to_f(pv[e]) * decay - step * mv[hh][q] / (sqrtf(vv[hh][q]) * rbc2 + eps);
+        float mq = mv[hh][q], vq = vv[hh][q];
+        const float pf = adam_elem(to_f(pv[e]), gf, mq, vq, b1, b2, rbc2, eps, decay, step);
+        mv[hh][q] = mq;
+        vv[hh][q] = vq;
         out[e] = sr ? sr_bf16(pf, (uint32_t)(hsh >> (16 * q)) & 0xffffu) : from_f<bf16>(pf);
       }
     }
@@ -275,19 +344,32 @@ void clip_coef_finalize(const float* ws, int nparts, float max_norm, float presc
   hipLaunchKernelGGL(clip_finalize_kernel, dim3(1), dim3(kNT), 0, s, ws, nparts, max_norm, prescale, out);
 }
 
+template <typename P, typename G>
+void launch_adamw(dim3 grid, hipStream_t s, P* p, const G* g, float* m, float* v, float* master, int64_t n,
+                  const float* hyper, const float* gsp, uint64_t ioff) {
+  // GRT_ADAMW_V4=1: always the 4-wide variant (A/B switch)
+  static const bool v4 = [] { const char* e = std::getenv("GRT_ADAMW_V4"); return e && e[0] == '1'; }();
+  auto a16 = [](const void* q) { return q == nullptr || reinterpret_cast<uintptr_t>(q) % 16 == 0; };
+  if (!v4 && a16(p) && a16(g) && a16(m) && a16(v) && a16(master))
+    hipLaunchKernelGGL((adamw_kernel<P, G, 8>), grid, dim3(kNT), 0, s, p, g, m, v, master, n, hyper, gsp, ioff);
+  else
+    hipLaunchKernelGGL((adamw_kernel<P, G, 4>), grid, dim3(kNT), 0, s, p, g, m, v, master, n, hyper, gsp, ioff);
+}
+
 void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
                 int64_t n, const float* hyper, const float* gsp, hipStream_t s, int max_blocks, int64_t ioff) {
-  unsigned nb = grid_for(n / 4 + 1);
+  unsigned nb = grid_for(n / 8 + 1);
   if (max_blocks > 0 && nb > (unsigned)max_blocks) nb = (unsigned)max_blocks;
   const dim3 grid(nb);
+  const uint64_t io = (uint64_t)ioff;
   if (pdt == DType::BF16 && gdt == DType::BF16)
-    hipLaunchKernelGGL((adamw_kernel<bf16, bf16>), grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, master, n, hyper, gsp, (uint64_t)ioff);
+    launch_adamw(grid, s, (bf16*)p, (const bf16*)g, m, v, master, n, hyper, gsp, io);
   else if (pdt == DType::BF16)
-    hipLaunchKernelGGL((adamw_kernel<bf16, float>), grid, dim3(kNT), 0, s, (bf16*)p, (const float*)g, m, v, master, n, hyper, gsp, (uint64_t)ioff);
+    launch_adamw(grid, s, (bf16*)p, (const float*)g, m, v, master, n, hyper, gsp, io);
   else if (gdt == DType::BF16)
-    hipLaunchKernelGGL((adamw_kernel<float, bf16>), grid, dim3(kNT), 0, s, (float*)p, (const bf16*)g, m, v, master, n, hyper, gsp, (uint64_t)ioff);
+    launch_adamw(grid, s, (float*)p, (const bf16*)g, m, v, master, n, hyper, gsp, io);
   else
-    hipLaunchKernelGGL((adamw_kernel<float, float>), grid, dim3(kNT), 0, s, (float*)p, (const float*)g, m, v, master, n, hyper, gsp, (uint64_t)ioff);
+    launch_adamw(grid, s, (float*)p, (const float*)g, m, v, master, n, hyper, gsp, io);
 }
 
 void adamw_t_step(void* p, const void* g, float* m, float* v, void* pt, int64_t rows, int64_t cols,

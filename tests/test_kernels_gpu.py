@@ -307,6 +307,34 @@ def test_adamw_bf16_stochastic_rounding(sr):
 
 
 @pytest.mark.parametrize("sr", [0.0, 1.0])
+def test_adamw_slices_and_alignment_bit_identical(sr):
+    """The 8-wide AdamW path (16-byte aligned operands), the 4-wide fallback (a slice starting 4
+    elements in: 8-byte aligned bf16) and chunked launches with index offsets all produce the same
+    bits as one launch over the whole buffer (the stochastic-rounding stream is keyed by the flat
+    index), including a scalar tail (n % 8 != 0)."""
+    C = _C()
+    n = (1 << 16) + 13
+    g0 = torch.Generator(device=DEV).manual_seed(5)
+    p0 = torch.randn(n, device=DEV, generator=g0).to(torch.bfloat16)
+    gr = torch.randn(n, device=DEV, generator=g0).to(torch.bfloat16)
+    m0 = torch.randn(n, device=DEV, generator=g0) * 0.01
+    v0 = torch.rand(n, device=DEV, generator=g0) * 0.01
+    hyper = torch.tensor([1e-3, 0.9, 0.999, 1e-8, 0.01, 0.1, 0.001, 1.0, sr, 3.0], device=DEV)
+
+    def run(cuts):
+        p, m, v = p0.clone(), m0.clone(), v0.clone()
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            C.adamw(p[lo:hi], gr[lo:hi], m[lo:hi], v[lo:hi], None, hyper, None, 0, lo)
+        return p, m, v
+
+    whole = run([0, n])
+    for cuts in ([0, 4, n], [0, 64, 1028, n], [0, 8, 12, n]):
+        got = run(cuts)
+        for a, b, what in zip(got, whole, ("p", "m", "v")):
+            assert torch.equal(a, b), f"cuts {cuts}: {what} differs"
+
+
+@pytest.mark.parametrize("sr", [0.0, 1.0])
 def test_adamw_t_matches_flat_update_and_transposes(sr):
     """adamw_t (update of a [rows, cols] weight that also writes W^T) == the flat AdamW kernel on
     the same data (same rounding stream for a matching index offset), and pt == p^T exactly."""
