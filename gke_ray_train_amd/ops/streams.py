@@ -40,7 +40,8 @@ def cu_mask_words(n_cus: int, total: int, pattern: str = "spread") -> List[int]:
 
 def cu_masked_stream(n_cus: int, device=None, pattern: str = "spread") -> "torch.cuda.ExternalStream":
     """A (cached, process-lifetime) HIP stream on ``device`` limited to ``n_cus`` CUs."""
-    dev = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
+    d = torch.device("cuda") if device is None else torch.device(device)
+    dev = torch.device("cuda", torch.cuda.current_device() if d.index is None else d.index)
     key = (dev.index, int(n_cus), pattern)
     s = _cache.get(key)
     if s is None:
