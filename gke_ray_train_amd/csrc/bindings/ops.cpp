@@ -552,7 +552,8 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
 std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o,
                              Tensor& lse, const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
                              const optional<Tensor>& dv_out, double scale, bool causal,
-                             const optional<Tensor>& seqlens_k, double dropout_p, int64_t seed) {
+                             const optional<Tensor>& seqlens_k, double dropout_p, int64_t seed,
+                             const optional<Tensor>& rope_cos, const optional<Tensor>& rope_sin) {
   c10::OptionalDeviceGuard g(q.device());
   check_bshd(dout, "dout");
   TORCH_CHECK(dout.sizes() == q.sizes(), "dout shape");
@@ -573,6 +574,18 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   bp.dk = dk.data_ptr(); bp.dk_bs = dk.stride(0); bp.dk_ss = dk.stride(1); bp.dk_hs = dk.stride(2);
   bp.dv = dv.data_ptr(); bp.dv_bs = dv.stride(0); bp.dv_ss = dv.stride(1); bp.dv_hs = dv.stride(2);
   bp.delta = ws.data_ptr<float>();
+  TORCH_CHECK(rope_cos.has_value() == rope_sin.has_value(), "attn_bwd: rope_cos and rope_sin together");
+  if (rope_cos.has_value()) {  // dQ / dK written un-rotated (q / k were rotated at position = index)
+    check_contig(*rope_cos, "rope_cos");
+    check_contig(*rope_sin, "rope_sin");
+    TORCH_CHECK(q.scalar_type() == at::kBFloat16 && p.D == 128, "attn_bwd rope epilogue: bf16, head_dim 128");
+    TORCH_CHECK(rope_cos->scalar_type() == at::kFloat && rope_sin->sizes() == rope_cos->sizes() &&
+                    rope_sin->scalar_type() == at::kFloat && rope_cos->dim() == 2 && rope_cos->size(1) == p.D / 2 &&
+                    rope_cos->size(0) >= std::max(p.Sq, p.Sk),
+                "attn_bwd: rope tables fp32 [>= max(Sq, Sk), D / 2]");
+    bp.rope_cos = rope_cos->data_ptr<float>();
+    bp.rope_sin = rope_sin->data_ptr<float>();
+  }
   TORCH_CHECK(dout.scalar_type() == q.scalar_type() && dq.scalar_type() == q.scalar_type() &&
                   dk.scalar_type() == q.scalar_type() && dv.scalar_type() == q.scalar_type(), "grad dtype mismatch");
   if (q.scalar_type() == at::kFloat) grt::attn_bwd_f32(bp, cur_stream(q));
@@ -890,7 +903,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"), py::arg("causal"),
-        py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);
+        py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("rope_cos") = py::none(),
+        py::arg("rope_sin") = py::none());
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);

@@ -139,6 +139,9 @@ struct AttnBwdParams {
   void* dk; int64_t dk_bs, dk_ss, dk_hs;
   void* dv; int64_t dv_bs, dv_ss, dv_hs;
   float* delta;    // fp32 workspace of attn_bwd_workspace_floats(): delta and lse2 rows
+  // optional (bf16 kernels, D = 128): q / k were RoPE-rotated at position = sequence index; the
+  // epilogues write dQ / dK already un-rotated (cos / sin fp32 [>= max(Sq, Sk), D / 2])
+  const float* rope_cos; const float* rope_sin;
 };
 void attn_bwd(const AttnBwdParams& p, hipStream_t s);
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int D);

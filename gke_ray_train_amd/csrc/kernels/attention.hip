@@ -352,6 +352,31 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p
 // (S, dP, dV^T, dK^T, 8 each); the S accumulator starts at -inf on masked (query, key) pairs of
 // the diagonal / padding tiles. One workgroup (one wave per SIMD) per CU: K / V fragments and the
 // dK / dV accumulators take ~450 registers. Heaviest (earliest, causal) key blocks launch first.
+// Backward epilogue with the RoPE of the forward undone in registers: the accumulator's element
+// (db, 4 gg + j) is head dim d = 32 db + 8 gg + 4 h + j, so the rotation pair (d, d + 64) is
+// (db, db + 2) of the same lane — x1 c + x2 s / x2 c - x1 s with the position's cos / sin rows
+// (rope_kernel<.., false>), rounded to bf16 once.
+__device__ __forceinline__ void store_unrotated(const f32x16 (&acc)[4], float scale, const float* __restrict__ cr,
+                                                const float* __restrict__ sr, bf16* dst, int h) {
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int d = db * 32 + 8 * gg + 4 * h;
+      const f32x4 c = *reinterpret_cast<const f32x4*>(cr + d);
+      const f32x4 sn = *reinterpret_cast<const f32x4*>(sr + d);
+      bf16x4 lo, hi;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float x1 = acc[db][4 * gg + j] * scale, x2 = acc[db + 2][4 * gg + j] * scale;
+        lo[j] = static_cast<bf16>(x1 * c[j] + x2 * sn[j]);
+        hi[j] = static_cast<bf16>(x2 * c[j] - x1 * sn[j]);
+      }
+      *reinterpret_cast<bf16x4*>(dst + d) = lo;
+      *reinterpret_cast<bf16x4*>(dst + d + D / 2) = hi;
+    }
+}
+
 constexpr int K2N = 128, K2M = 32, K2NT = 256, K2NSLOT = 4;
 constexpr int K2IMG = K2M * D * 2;           // one 32-row image: 8 KiB
 constexpr int K2SLOT = 2 * K2IMG + 4 * 1024;  // Q image, dO image, per-wave statistics copy
@@ -541,6 +566,8 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   if (mykey < p.Sk) {
     bf16* dK = (bf16*)P.dk + (int64_t)b * P.dk_bs + (int64_t)hkv * P.dk_hs + (int64_t)mykey * P.dk_ss;
     bf16* dV = (bf16*)P.dv + (int64_t)b * P.dv_bs + (int64_t)hkv * P.dv_hs + (int64_t)mykey * P.dv_ss;
+    if (P.rope_cos)
+      store_unrotated(dk, p.scale, P.rope_cos + (int64_t)mykey * (D / 2), P.rope_sin + (int64_t)mykey * (D / 2), dK, h);
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
@@ -551,7 +578,7 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
           a[j] = static_cast<bf16>(dk[db][4 * gg + j] * p.scale);
           v[j] = static_cast<bf16>(dv[db][4 * gg + j]);
         }
-        *reinterpret_cast<bf16x4*>(dK + db * 32 + 8 * gg + 4 * h) = a;
+        if (!P.rope_cos) *reinterpret_cast<bf16x4*>(dK + db * 32 + 8 * gg + 4 * h) = a;
         *reinterpret_cast<bf16x4*>(dV + db * 32 + 8 * gg + 4 * h) = v;
       }
   }
@@ -706,15 +733,19 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
 
   if (qok) {
     bf16* dQ = (bf16*)P.dq + (int64_t)b * P.dq_bs + (int64_t)hq * P.dq_hs + (int64_t)myq * P.dq_ss;
+    if (P.rope_cos) {
+      store_unrotated(dq, p.scale, P.rope_cos + (int64_t)myq * (D / 2), P.rope_sin + (int64_t)myq * (D / 2), dQ, h);
+    } else {
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+      for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        bf16x4 v;
+        for (int gg = 0; gg < 4; ++gg) {
+          bf16x4 v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(dq[db][4 * gg + j] * p.scale);
-        *reinterpret_cast<bf16x4*>(dQ + db * 32 + 8 * gg + 4 * h) = v;
-      }
+          for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(dq[db][4 * gg + j] * p.scale);
+          *reinterpret_cast<bf16x4*>(dQ + db * 32 + 8 * gg + 4 * h) = v;
+        }
+    }
   }
 }
 

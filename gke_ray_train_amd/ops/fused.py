@@ -249,6 +249,11 @@ def _warn_once(msg):
         warnings.warn(msg)
 
 
+# attention backward epilogues write dQ / dK un-rotated into dqkv (no rope_bwd pass);
+# GRT_ROPE_BWD_FUSED=0 -> separate dq / dk tensors + the RoPE backward kernel
+_ROPE_BWD_FUSED = os.environ.get("GRT_ROPE_BWD_FUSED", "1") != "0"
+
+
 class _RopeAttention(torch.autograd.Function):
     """qkv [B*S, (Hq + 2 Hkv) * D] -> o [B*S, Hq * D]: RoPE + causal flash attention fused.
 
@@ -279,10 +284,16 @@ class _RopeAttention(torch.autograd.Function):
         q4 = q.view(B, S, hq, D)
         k4 = k.view(B, S, hkv, D)
         v4 = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
-        dv4 = dqkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
-        dq, dk, _ = C.attn_bwd(do.contiguous().view(B, S, hq, D), q4, k4, v4, o, lse, None, None, dv4,
-                               scale, causal, None)
-        C.rope_bwd(dq, dk, dqkv, cos, sin, None, hq, hkv, D, S)
+        d4 = dqkv.view(B, S, hq + 2 * hkv, D)
+        dv4 = d4[:, :, hq + hkv:, :]
+        if _ROPE_BWD_FUSED and cos.dim() == 2 and cos.shape[0] >= S:
+            # the kernels' epilogues undo the RoPE and write dQ / dK straight into dqkv's columns
+            C.attn_bwd(do.contiguous().view(B, S, hq, D), q4, k4, v4, o, lse, d4[:, :, :hq], d4[:, :, hq:hq + hkv],
+                       dv4, scale, causal, None, rope_cos=cos, rope_sin=sin)
+        else:
+            dq, dk, _ = C.attn_bwd(do.contiguous().view(B, S, hq, D), q4, k4, v4, o, lse, None, None, dv4,
+                                   scale, causal, None)
+            C.rope_bwd(dq, dk, dqkv, cos, sin, None, hq, hkv, D, S)
         return dqkv, None, None, None, None, None, None, None, None, None
 
 

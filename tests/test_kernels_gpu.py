@@ -437,11 +437,17 @@ def test_flash_attention_fp32(case):
     _attn_case(dtype=torch.float32, **case)
 
 
-def test_rope_attention_fused():
+@pytest.mark.parametrize("fused_bwd", [True, False])
+@pytest.mark.parametrize("B,S,hq,hkv", [(2, 192, 4, 2), (1, 1024, 4, 4)])
+def test_rope_attention_fused(fused_bwd, B, S, hq, hkv, monkeypatch):
+    """RoPE + flash attention vs fp32 math; fused_bwd: the backward kernels' epilogues undo the
+    RoPE and write dQ / dK straight into dqkv (no rope_bwd pass)."""
     from gke_ray_train_amd import ops
     from gke_ray_train_amd.ops import _ref
+    from gke_ray_train_amd.ops import fused as F_
+    monkeypatch.setattr(F_, "_ROPE_BWD_FUSED", fused_bwd)
     torch.manual_seed(9)
-    B, S, hq, hkv, D = 2, 192, 4, 2, 128
+    D = 128
     qkv = torch.randn(B * S, (hq + 2 * hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
     cos, sin = _ref.rope_tables(S, D, 10000.0, device=DEV)
     o = ops.rope_attention(qkv, cos, sin, B, S, hq, hkv, D)
