@@ -59,7 +59,9 @@ _WGRAD_TN = os.environ.get("GRT_WGRAD_TN", "1") != "0"
 # the Llama projection shapes in isolation, profiles/r1_dgrad_layout_ab.jsonl). Frozen weights
 # (LoRA / QLoRA base) get it for free: +2.3 % LoRA end to end (profiles/r1_transposed_dgrad_ab.txt).
 # Trainable weights need a fresh W^T every step; the per-step transpose cancels the gain on the
-# full fine-tune, so that path is opt-in (GRT_TRANSPOSED_DGRAD_TRAINABLE=1).
+# full fine-tune, so that path is opt-in (GRT_TRANSPOSED_DGRAD_TRAINABLE=1) — except for weights the
+# engine marks ``_grt_fwd_transpose`` (ZeRO, whose sharded update cannot write W^T: there the
+# forward-time transpose is +1.7 % over the NN dX GEMM, profiles/r2_zero_fwd_transpose_proxy.txt).
 _TRANSPOSED_DGRAD = os.environ.get("GRT_TRANSPOSED_DGRAD", "1") != "0"
 _TRANSPOSED_DGRAD_TRAINABLE = os.environ.get("GRT_TRANSPOSED_DGRAD_TRAINABLE", "0") == "1"
 
@@ -100,7 +102,8 @@ def transpose_for_backward(w: torch.Tensor):
     stream (HIP transpose kernel, HBM-bound, overlapping the forward GEMMs) and return (W^T, event)
     for the backward's TN input-gradient GEMM; None where it does not apply (FSDP-managed or
     unaligned weights, non-bf16)."""
-    if not (_TRANSPOSED_DGRAD and _TRANSPOSED_DGRAD_TRAINABLE and w.is_cuda and w.dtype == torch.bfloat16
+    if not (_TRANSPOSED_DGRAD and (_TRANSPOSED_DGRAD_TRAINABLE or getattr(w, "_grt_fwd_transpose", False))
+            and w.is_cuda and w.dtype == torch.bfloat16
             and w.dim() == 2
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and getattr(w, "_grt_slot", None) is not None
             and getattr(w, "_grt_unit", None) is None and w.is_contiguous()):

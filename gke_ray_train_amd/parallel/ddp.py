@@ -23,6 +23,8 @@ MI355X design (not a translation of torch's C++ Reducer):
   traffic shrink by world), and the updated shards are ALL-GATHERED back into the flat parameter
   buffer asynchronously, bucket by bucket in forward order, each bucket waited for by a forward
   pre-hook of the first module that uses it — the gather overlaps the next step's forward.
+* ZeRO: projection weights get W^T written on a side stream during the forward (after their
+  bucket's all-gather) for the TN input-gradient GEMM (``GRT_ZERO_FWD_TRANSPOSE=0`` = NN form);
 * one GPU: the gradient-norm reduction of each bucket (sum of squares, HBM-bound) runs on a side
   stream as soon as the bucket's last gradient is written, under the remaining backward GEMMs;
   ``clip_grad_norm_`` then only combines the per-bucket partial sums (``GRT_EARLY_GRAD_NORM=0``
@@ -194,6 +196,13 @@ class DistributedDataParallel(nn.Module):
         self._register_hooks()
         if self.zero:
             self._setup_shards()
+            if os.environ.get("GRT_ZERO_FWD_TRANSPOSE", "1") != "0":
+                # the sharded AdamW cannot write W^T (a rank owns a flat slice, not whole rows), so
+                # each projection weight is transposed on a side stream in the forward, right after
+                # its all-gather, for the backward's TN input-gradient GEMM (ops/linear.py)
+                for m in module.modules():
+                    if isinstance(m, _DirectLinear) and id(m.weight) in self._direct:
+                        m.weight._grt_fwd_transpose = True
         self._norm_ws = None
         self._norm_stream = None
         self._norm_bad = False  # a step whose early norm cannot be trusted (fall back)

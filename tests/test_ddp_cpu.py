@@ -91,6 +91,10 @@ def _zero_worker(rank, world, port, q, zero, tensor_coll=False):
         m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=3)
         ddp = DistributedDataParallel(m, bucket_cap_mb=0.1, shard_optimizer=zero)
         assert ddp.zero == zero
+        # ZeRO marks the projection weights for the forward-time W^T (TN dX GEMM on GPU)
+        from gke_ray_train_amd.ops.linear import Linear
+        marked = [getattr(mm.weight, "_grt_fwd_transpose", False) for mm in m.modules() if isinstance(mm, Linear)]
+        assert marked and all(x == zero for x in marked)
         opt = FusedAdamW(ddp.optimizer_param_groups(0.1), lr=3e-3)
         if zero:  # the optimizer holds only this rank's shard
             n_opt = sum(p.numel() for gp in opt.param_groups for p in gp["params"])

@@ -88,8 +88,8 @@ def test_two_ranks_on_one_gpu_match_single_process(engine, accum):
         assert np.array_equal(res[0][n], res[1][n]) or engine == "fsdp", f"ranks disagree on {n}"
 
 
-def _opt_worker(rank, world, port, q, zero):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _opt_worker(rank, world, port, q, zero, fwd_transpose="0", grads_only=False):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GRT_ZERO_FWD_TRANSPOSE=fwd_transpose)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -100,6 +100,11 @@ def _opt_worker(rank, world, port, q, zero):
         eng = DistributedDataParallel(m, bucket_cap_mb=0.25, shard_optimizer=zero)
         opt = FusedAdamW(eng.optimizer_param_groups(0.0), lr=1e-3)
         ids = _batch(world, 2).view(2, world, -1, 128)[:, rank].cuda()
+        if grads_only:  # one backward: this rank's reduced gradient shards
+            eng(ids[0], labels=ids[0])["loss"].backward()
+            eng.finish_gradient_sync()
+            q.put((rank, {str(i): g.float().cpu().numpy() for i, g in enumerate(eng.grad_buffers())}))
+            return
         for step in range(2):
             loss = eng(ids[step], labels=ids[step])["loss"]
             loss.backward()
@@ -117,7 +122,10 @@ def test_zero_matches_plain_ddp_two_ranks_on_one_gpu(monkeypatch):
     """Sharded-optimizer DDP (reduce-scatter, 1/world AdamW, async all-gather waited by forward
     pre-hooks) takes the same two optimizer steps as plain DDP (same reduced gradients; only the
     grad-norm summation order differs -> agreement to bf16 rounding). Round-to-nearest updates:
-    stochastic rounding draws its bits by buffer index, which differs between the two layouts."""
+    stochastic rounding draws its bits by buffer index, which differs between the two layouts.
+    Both arms use the NN input-gradient GEMM (GRT_ZERO_FWD_TRANSPOSE=0): Adam's first steps move
+    near-zero-gradient weights by ~lr * sign(g), so another GEMM's rounding is not comparable here
+    (the transposed path is checked at the gradient level below)."""
     monkeypatch.setenv("GRT_ADAMW_SR", "0")  # inherited by the spawned ranks
     world = 2
     ctx = mp.get_context("spawn")
@@ -143,3 +151,32 @@ def test_zero_matches_plain_ddp_two_ranks_on_one_gpu(monkeypatch):
     for n, ref in out[False].items():
         got = out[True][n]
         assert np.all(np.abs(got - ref) <= 1e-2 * np.abs(ref) + 1e-5), f"{n}: {np.abs(got - ref).max()}"
+
+
+def test_zero_forward_transpose_gradients_match_nn_path():
+    """ZeRO's forward-time W^T (TN input-gradient GEMMs) gives the same reduced gradient shards as
+    the NN path, to bf16 GEMM rounding."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    out = {}
+    for ft in ("0", "1"):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_opt_worker, args=(r, world, port, q, True, ft, True)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = {}
+        try:
+            for _ in range(world):
+                r, g = q.get(timeout=300)
+                res[r] = g
+        finally:
+            for p in procs:
+                p.join(timeout=60)
+        assert all(p.exitcode == 0 for p in procs)
+        out[ft] = res
+    for r in range(world):
+        for k, ref in out["0"][r].items():
+            got = out["1"][r][k]
+            rel = np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-12)
+            assert rel < 2e-2, (r, k, rel)
