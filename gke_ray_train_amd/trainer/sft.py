@@ -472,12 +472,13 @@ class SFTTrainer:
         batches = self._batches(self.eval_seqs, self.args.per_device_eval_batch_size, 0, shuffle=False)
         if self._fuse_enabled():  # same token-weighted mean from fewer, larger forwards
             batches = [cb for cb, _ in self._step_chunks(batches, list(range(len(batches))), True)]
-        for b in batches:
-            b = self._to_dev(b)
-            loss = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])["loss"]
-            n = (b["labels"][:, 1:] != -100).sum()
-            tot[0] += loss.double() * n
-            tot[1] += n
+        with torch.no_grad():  # as HF's prediction_step: no saved activations, no fused CE gradient
+            for b in batches:
+                b = self._to_dev(b)
+                loss = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])["loss"]
+                n = (b["labels"][:, 1:] != -100).sum()
+                tot[0] += loss.double() * n
+                tot[1] += n
         if self.world > 1:
             dist.all_reduce(tot)
         rt = time.time() - t0
