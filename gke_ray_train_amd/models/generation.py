@@ -72,13 +72,14 @@ def _fused_ok(qkv, cache: KVCache, li: int) -> bool:
 
 
 def _mlp(mlp, x):
-    """Decode MLP: for 1-4 tokens the down projection is a GEMV whose input SwiGLU is computed on
-    the fly from the fused gate/up output (gemv.hip, one launch instead of SwiGLU + GEMV)."""
+    """Decode MLP: for 1-2 tokens (``GEMV_MAX_ROWS``) the down projection is a GEMV whose input
+    SwiGLU is computed on the fly from the fused gate/up output (gemv.hip, one launch instead of
+    SwiGLU + GEMV)."""
     from ..ops import linear as _lin
     down = mlp.down_proj
-    if (_lin._GEMV and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[0] <= 4 and type(down) is _lin.Linear
-            and down.bias is None and down.weight.dtype == torch.bfloat16 and down.weight.is_contiguous()
-            and down.in_features % 8 == 0 and not torch.is_grad_enabled()):
+    if (_lin._GEMV and x.is_cuda and x.dtype == torch.bfloat16 and x.shape[0] <= _lin.GEMV_MAX_ROWS
+            and type(down) is _lin.Linear and down.bias is None and down.weight.dtype == torch.bfloat16
+            and down.weight.is_contiguous() and down.in_features % 8 == 0 and not torch.is_grad_enabled()):
         gu = mlp.gate_up_proj(x)
         if gu.is_contiguous() and gu.data_ptr() % 16 == 0 and gu.shape[-1] == 2 * down.in_features:
             return _native.kernels().gemv(gu, down.weight, swiglu=True)

@@ -214,6 +214,10 @@ class _DirectGradLinear(torch.autograd.Function):
 
 
 _GEMV = os.environ.get("GRT_GEMV", "1") != "0"
+# rows up to which the decode GEMV beats the library GEMM (Llama-3.1-8B decode, HIP graph: batch 1
+# 285 vs 210 tok/s, batch 4 688 vs 793, batch 8 746 vs 1506 — profiles/r2_decode_batch_gemv.txt:
+# the activations, re-read by every wave, and the per-row FMAs outgrow the weight stream)
+GEMV_MAX_ROWS = int(os.environ.get("GRT_GEMV_MAX_ROWS", "2"))
 
 
 def linear(x, weight, bias=None):
@@ -222,8 +226,8 @@ def linear(x, weight, bias=None):
     K = weight.shape[-1]
     if (_GEMV and x.is_cuda and not torch.is_grad_enabled() and x.dtype == torch.bfloat16
             and weight.dtype == torch.bfloat16 and weight.dim() == 2 and weight.is_contiguous()
-            and x.numel() // K <= 4 and K % 8 == 0 and x.shape[-1] == K):
-        # decode: 1-4 tokens per step are a weight stream -> HBM-bound GEMV kernel (gemv.hip)
+            and x.numel() // K <= GEMV_MAX_ROWS and K % 8 == 0 and x.shape[-1] == K):
+        # decode: 1-2 tokens per step are a weight stream -> HBM-bound GEMV kernel (gemv.hip)
         from .. import _native
         x2 = x.reshape(-1, K)
         if x2.stride(-1) == 1 and x2.stride(0) % 8 == 0 and x2.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0:

@@ -723,9 +723,14 @@ def test_gemv_decode(M, N, K):
     y = _C().gemv(x, w)
     ref = x.float() @ w.float().t()
     _close(y, ref, 2e-2, 2e-2, "gemv")
+    from gke_ray_train_amd.ops.linear import GEMV_MAX_ROWS
     with torch.no_grad():
         y2 = linear(x.view(M, 1, K), w)
-    assert y2.shape == (M, 1, N) and torch.equal(y2.view(M, N), y)
+    assert y2.shape == (M, 1, N)
+    if M <= GEMV_MAX_ROWS:  # routed to the GEMV
+        assert torch.equal(y2.view(M, N), y)
+    else:  # the library GEMM (faster from 3-4 rows on)
+        _close(y2.view(M, N), ref, 2e-2, 2e-2, "linear (library) at M rows")
 
 
 @pytest.mark.parametrize("M", [1, 3])

@@ -14,7 +14,8 @@ from gke_ray_train_amd.models import build_llama  # noqa: E402
 
 model = sys.argv[1] if len(sys.argv) > 1 else "llama3.1-8b"
 m = build_llama(model, device="cuda", dtype=torch.bfloat16, seed=0)
-ids = torch.randint(0, m.config.vocab_size, (1, 512), device="cuda")
+B = int(os.environ.get("DECODE_B", "1"))  # sequences decoded together (batch of requests)
+ids = torch.randint(0, m.config.vocab_size, (B, 512), device="cuda")
 from gke_ray_train_amd.ops import linear as _lin  # noqa: E402
 
 runs = [(False, True), (True, False), (True, True)]  # (graph, gemv)
@@ -27,5 +28,5 @@ for mode, gemv in runs:
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     print(json.dumps({"model": model, "mode": ("hip_graph" if mode else "eager") + ("+gemv" if gemv else "+library_gemm"),
-                      "new_tokens": out.shape[1] - 512,
-                      "seconds": round(dt, 3), "tokens_per_s": round((out.shape[1] - 512) / dt, 1)}), flush=True)
+                      "batch": B, "new_tokens": out.shape[1] - 512,
+                      "seconds": round(dt, 3), "tokens_per_s": round(B * (out.shape[1] - 512) / dt, 1)}), flush=True)
