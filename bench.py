@@ -15,8 +15,12 @@ Default = config #2 "Llama-2 7B DDP bf16, 8 Ray workers on 8xMI355X (fine_tune_l
 Other BASELINE configs: ``--parallel fsdp`` (#3), ``--peft lora|qlora`` (#4),
 ``--model llama3-70b --parallel fsdp --offload`` (#5).
 
-Launch: ``python bench.py`` (1 GPU) or ``python -m torch.distributed.run --nproc-per-node N
-bench.py --gpus N``. Rank 0 prints ONE JSON line.
+Launch: ``python bench.py --gpus N``: for N > 1 (and no ``WORLD_SIZE`` in the environment) the
+parent starts N rank processes through the framework's own ``TorchTrainer(num_workers=N,
+use_gpu=True)`` — one worker actor per GPU, RCCL rendezvous, exactly the "8 Ray workers" of
+BASELINE config #2 (reference ray-jobs/pytorch_llm_ray.py:346-350,368-376) — and never touches the
+GPU itself. ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`` also works;
+a ``WORLD_SIZE`` that disagrees with ``--gpus`` is an error. Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -71,6 +75,7 @@ def parse():
     ap.add_argument("--ipc", action="store_true", help="latency-bound collectives (grad-norm all-reduce) over the "
                     "xGMI IPC one-shot kernel instead of RCCL (GRT_IPC_COLLECTIVES=1)")
     ap.add_argument("--backend", default="", help="process-group backend (default: nccl = RCCL on GPU, gloo on CPU)")
+    ap.add_argument("--launcher", default="", help=argparse.SUPPRESS)  # set by launch_workers
     return ap.parse_args()
 
 
@@ -125,8 +130,56 @@ def _baseline_metric() -> str:
         return "tokens/sec (whole node) Llama-2-7B fine-tune at 1/2/4/8 MI355X; samples/sec on Wikitext-2"
 
 
+def _bench_worker(cfg: dict):
+    """TorchTrainer ``train_loop_per_worker``: the process group is already up (TrainWorker)."""
+    run(argparse.Namespace(**cfg))
+
+
+def launch_workers(a) -> int:
+    """``--gpus N`` with no launcher: N TorchTrainer worker actors run :func:`run`; rank 0's JSON
+    line reaches this process's stdout through the inherited descriptor. This process only counts
+    devices (no HIP context), so the workers own the GPUs."""
+    import shutil
+    import tempfile
+    from gke_ray_train_amd.runtime.errors import TrainingFailedError
+    from gke_ray_train_amd.train import RunConfig, ScalingConfig, TorchTrainer
+    from gke_ray_train_amd.train.torch import TorchConfig
+    use_gpu = a.device != "cpu"
+    if use_gpu and torch.cuda.device_count() < a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but only {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+        return 2
+    backend = a.backend or ("nccl" if use_gpu else "gloo")
+    store = tempfile.mkdtemp(prefix="grt_bench_")
+    os.environ.setdefault("GRT_NUM_GPUS", str(a.gpus if use_gpu else 0))
+    try:
+        cfg = dict(vars(a), launcher=f"TorchTrainer(num_workers={a.gpus})")
+        TorchTrainer(_bench_worker, train_loop_config=cfg,
+                     scaling_config=ScalingConfig(num_workers=a.gpus, use_gpu=use_gpu),
+                     run_config=RunConfig(name="bench", storage_path=store, verbose=0),
+                     torch_config=TorchConfig(backend=backend)).fit()
+        return 0
+    except TrainingFailedError as e:
+        print(f"bench.py: a rank failed: {e}", file=sys.stderr)
+        return 1
+    finally:
+        shutil.rmtree(store, ignore_errors=True)
+
+
 def main():
     a = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != a.gpus:
+            print(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {a.gpus}; refusing to "
+                  f"benchmark a different number of ranks than requested", file=sys.stderr)
+            sys.exit(2)
+    elif a.gpus > 1:
+        sys.exit(launch_workers(a))
+    a.launcher = a.launcher or ("torch.distributed.run" if env_world is not None else "in-process")
+    run(a)
+
+
+def run(a):
     if a.ipc:
         os.environ["GRT_IPC_COLLECTIVES"] = "1"
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,9 +193,12 @@ def main():
         idx = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(idx)
         dev = torch.device("cuda", idx)
-    if world > 1:
+    if world > 1 and not dist.is_initialized():
         backend = a.backend or ("gloo" if cpu else "nccl")
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+    pg_world = dist.get_world_size() if dist.is_initialized() else 1
+    if pg_world != world:
+        raise SystemExit(f"bench.py: process group has {pg_world} ranks but WORLD_SIZE={world}")
 
     from gke_ray_train_amd.data import TokenBatchLoader, synthetic_tokens
     from gke_ray_train_amd.models import get_config
@@ -317,6 +373,9 @@ def main():
                        "optimizer_overlap": type(opt).__name__ == "OverlappedOptimizer",
                        "library_gemms": "offline-tuned" if tuned else "default"},
             "samples_per_sec": round(tps / a.seq, 2),
+            "pg_world_size": pg_world,
+            "pg_backend": dist.get_backend() if dist.is_initialized() else "none",
+            "launcher": a.launcher,
             "mfu_bf16_dense": round(mfu, 4),
             "loss": round(float(loss.item()) * accum, 4),
         }
