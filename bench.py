@@ -75,6 +75,11 @@ def parse():
     ap.add_argument("--ipc", action="store_true", help="latency-bound collectives (grad-norm all-reduce) over the "
                     "xGMI IPC one-shot kernel instead of RCCL (GRT_IPC_COLLECTIVES=1)")
     ap.add_argument("--backend", default="", help="process-group backend (default: nccl = RCCL on GPU, gloo on CPU)")
+    ap.add_argument("--force-collectives", action="store_true",
+                    help="run the multi-rank collective path even at world 1 (one-rank RCCL process group: "
+                         "ZeRO reduce-scatter / all-gather, FSDP gathers) — one-GPU rehearsal of the 8-GPU data plane")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print the per-rank HBM / host memory plan (parallel/planner.py) for this config and exit")
     ap.add_argument("--launcher", default="", help=argparse.SUPPRESS)  # set by launch_workers
     return ap.parse_args()
 
@@ -112,7 +117,7 @@ def build(a, cfg, dev, dtype, world):
         if a.peft == "qlora":
             quantize_model_(model, BitsAndBytesConfig(bnb_4bit_compute_dtype=dtype))
         fwd = get_peft_model(model, LoraConfig(r=a.lora_r, lora_alpha=16, lora_dropout=0.1))
-    zero = a.zero == "on" or (a.zero == "auto" and world > 1)
+    zero = a.zero == "on" or (a.zero == "auto" and (world > 1 or a.force_collectives))
     eng = DistributedDataParallel(fwd, bucket_cap_mb=a.bucket_mb or None, shard_optimizer=zero)
     opt = FusedAdamW(eng.optimizer_param_groups(weight_decay=0.0), lr=a.lr)
     if a.overlap_opt == "on" or (a.overlap_opt == "auto" and not zero and dev.type == "cuda"):
@@ -193,9 +198,19 @@ def run(a):
         idx = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(idx)
         dev = torch.device("cuda", idx)
-    if world > 1 and not dist.is_initialized():
+    if a.force_collectives:
+        os.environ["GRT_FORCE_COLLECTIVES"] = "1"
+    if (world > 1 or a.force_collectives) and not dist.is_initialized():
         backend = a.backend or ("gloo" if cpu else "nccl")
-        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
+        if world == 1:  # one-rank group for the forced-collective rehearsal
+            import socket
+            with socket.socket() as s_:
+                s_.bind(("127.0.0.1", 0))
+                port = s_.getsockname()[1]
+            dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                    device_id=dev if backend == "nccl" else None)
+        else:
+            dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
     pg_world = dist.get_world_size() if dist.is_initialized() else 1
     if pg_world != world:
         raise SystemExit(f"bench.py: process group has {pg_world} ranks but WORLD_SIZE={world}")
@@ -220,6 +235,21 @@ def run(a):
         from gke_ray_train_amd.ops.gemm_tuning import enable_tuned_gemms
         tuned = enable_tuned_gemms()
     cfg = get_config(a.model)
+    from gke_ray_train_amd.parallel.planner import GiB, plan_memory
+    plan = plan_memory(cfg, world, a.parallel, offload=a.offload, peft=a.peft, micro_batch=a.micro_batch or a.batch,
+                       seq=a.seq, zero=(a.zero == "on" or (a.zero == "auto" and (world > 1 or a.force_collectives))),
+                       checkpointing=a.checkpointing, lora_r=a.lora_r,
+                       hbm_capacity=None if not cpu else float("inf"))
+    if a.plan_only:
+        if rank == 0:
+            print(json.dumps({"memory_plan": plan.to_dict()}), flush=True)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return
+    if not plan.fits:  # refuse up front with the numbers instead of an allocator error mid-step
+        print(f"bench.py: memory preflight failed for {cfg.name} {a.parallel} world={world}: "
+              + "; ".join(plan.problems()), file=sys.stderr, flush=True)
+        sys.exit(3)
     model, eng, call, opt = build(a, cfg, dev, dtype, world)
     model.train()
 
@@ -371,12 +401,15 @@ def run(a):
                        "micro_batch": mb, "grad_accum": accum, "optimizer": "fused AdamW fp32 states",
                        "max_grad_norm": a.max_grad_norm, "activation_checkpointing": a.checkpointing,
                        "optimizer_overlap": type(opt).__name__ == "OverlappedOptimizer",
+                       "forced_collectives": bool(a.force_collectives),
                        "library_gemms": "offline-tuned" if tuned else "default"},
             "samples_per_sec": round(tps / a.seq, 2),
             "pg_world_size": pg_world,
             "pg_backend": dist.get_backend() if dist.is_initialized() else "none",
             "launcher": a.launcher,
             "mfu_bf16_dense": round(mfu, 4),
+            "hbm_plan_gib": round(plan.hbm_total / GiB, 1),
+            "hbm_peak_gib": round(torch.cuda.max_memory_allocated(dev) / GiB, 1) if not cpu else None,
             "loss": round(float(loss.item()) * accum, 4),
         }
         print(json.dumps(out), flush=True)

@@ -92,6 +92,8 @@ def forward_cached(model, ids: torch.Tensor, cache: KVCache) -> torch.Tensor:
     """Run `ids` [B, S] at positions cache.len ... ; returns last-position logits [B, V]."""
     B, S = ids.shape
     pos0 = cache.len
+    if pos0 + S > cache.max_len:  # rope_append writes no cache row past max_len: refuse, don't truncate
+        raise ValueError(f"KV cache overflow: {pos0} cached + {S} new tokens > max_len {cache.max_len}")
     cos, sin = model.rope(cache.max_len, ids.device)
     h = model.model.embed_tokens(ids).view(B * S, -1)
     residual = None

@@ -25,6 +25,10 @@ MI355X design (not a translation of torch's C++ Reducer):
   pre-hook of the first module that uses it — the gather overlaps the next step's forward.
 * ZeRO: projection weights get W^T written on a side stream during the forward (after their
   bucket's all-gather) for the TN input-gradient GEMM (``GRT_ZERO_FWD_TRANSPOSE=0`` = NN form);
+* ``GRT_FORCE_COLLECTIVES=1`` (or ``force_collectives=True``) with an initialised process group
+  runs the multi-rank code path even at world size 1 — bucket all-reduce / reduce-scatter on the
+  flat-buffer views, async ``Work.wait()`` from the hooks, ZeRO all-gathers waited by forward
+  pre-hooks — so a one-GPU box executes the exact RCCL calls an 8-GPU node issues;
 * one GPU: the gradient-norm reduction of each bucket (sum of squares, HBM-bound) runs on a side
   stream as soon as the bucket's last gradient is written, under the remaining backward GEMMs;
   ``clip_grad_norm_`` then only combines the per-bucket partial sums (``GRT_EARLY_GRAD_NORM=0``
@@ -88,7 +92,7 @@ class _Bucket:
     start: int
     end: int
     params: List[nn.Parameter] = field(default_factory=list)
-    ready: int = 0
+    ready: set = field(default_factory=set)   # ids of the parameters announced this step
     work: Optional[object] = None
     shard_off: int = 0        # ZeRO: offset of this bucket's chunk in the rank's shard buffers
     ag_work: Optional[object] = None
@@ -123,16 +127,20 @@ class DistributedDataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  broadcast_params: bool = True, grad_dtype: Optional[torch.dtype] = None,
-                 split_decay: bool = True, shard_optimizer: bool = False):
+                 split_decay: bool = True, shard_optimizer: bool = False, force_collectives: Optional[bool] = None):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world_size > 1 else 0
-        self.zero = bool(shard_optimizer) and self.world_size > 1
+        if force_collectives is None:
+            force_collectives = os.environ.get("GRT_FORCE_COLLECTIVES", "0") == "1"
+        # comm: the collective code path runs (world > 1, or forced at world 1 for rehearsal)
+        self.comm = self.world_size > 1 or (bool(force_collectives) and dist.is_available() and dist.is_initialized())
+        self.zero = bool(shard_optimizer) and self.comm
         # gloo branch: list-based collectives. GRT_GLOO_TENSOR_COLLECTIVES=1 runs the RCCL code path
         # (reduce_scatter_tensor / all_gather_into_tensor) over gloo so CPU tests exercise it.
-        self.gloo = (self.world_size > 1 and dist.get_backend(process_group) == "gloo"
+        self.gloo = (self.comm and dist.get_backend(process_group) == "gloo"
                      and os.environ.get("GRT_GLOO_TENSOR_COLLECTIVES", "0") != "1")
         self._sync = True
         self._hooks = []
@@ -159,14 +167,14 @@ class DistributedDataParallel(nn.Module):
                 named.append((n, p))
         total_bytes = sum(p.numel() * p.element_size() for _, p in named)
         dev0 = named[0][1].device if named else torch.device("cpu")
-        self._early_norm = (self.world_size == 1 and dev0.type == "cuda"
+        self._early_norm = (not self.comm and dev0.type == "cuda"
                             and os.environ.get("GRT_EARLY_GRAD_NORM", "1") != "0")
         if bucket_cap_mb:
             self.bucket_bytes = int(bucket_cap_mb * 2 ** 20)
         elif self._early_norm and not os.environ.get("GRT_BUCKET_MB"):
             self.bucket_bytes = 256 * 2 ** 20  # norm granularity only: no collectives on one GPU
         else:
-            self.bucket_bytes = plan_bucket_bytes(total_bytes, self.world_size)
+            self.bucket_bytes = plan_bucket_bytes(total_bytes, max(self.world_size, 2 if self.comm else 1))
         # group by (dtype, decay), reverse registration order inside each group
         groups: Dict[tuple, List[tuple]] = {}
         for n, p in named:
@@ -306,29 +314,30 @@ class DistributedDataParallel(nn.Module):
                         view.add_(p.grad)
                 p.grad = view
             sl.fresh = False
-            self._mark_ready(g, b)
+            self._mark_ready(g, b, p)
         return hook
 
     def _notify(self, p):
         p.grad = self._slots[p].view
         g, b = self._bucket_of[p]
-        self._mark_ready(g, b)
+        self._mark_ready(g, b, p)
 
-    def _mark_ready(self, g, b):
+    def _mark_ready(self, g, b, p):
         if not self._sync:
             return
-        if self.world_size == 1:
+        if not self.comm:
             if self._early_norm:
-                b.ready += 1
-                if b.ready > len(b.params):
+                if id(p) in b.ready:  # announced twice: the early norm may have read a partial bucket
                     self._norm_bad = True
-                elif b.ready == len(b.params):
+                    return
+                b.ready.add(id(p))
+                if len(b.ready) == len(b.params):
                     self._launch_norm(g, b)
             return
-        b.ready += 1
-        if b.ready > len(b.params):  # a parameter announced twice would launch a bucket early
+        if id(p) in b.ready:  # a parameter announced twice would launch a bucket early
             raise RuntimeError("DDP bucket readiness over-counted (gradient announced twice)")
-        if b.ready == len(b.params):
+        b.ready.add(id(p))
+        if len(b.ready) == len(b.params):
             self._launch(g, b)
 
     def _launch_norm(self, g: _FlatGroup, b: _Bucket):
@@ -370,13 +379,13 @@ class DistributedDataParallel(nn.Module):
             for p in stale:
                 self._slots[p].fresh = False
                 p.grad = self._slots[p].view
-        if self.world_size == 1:
+        if not self.comm:
             if self._early_norm and self._sync:
                 for g in self.groups:
                     for b in g.buckets:
                         if not b.normed:  # no gradient announced (unused params) or partial bucket
                             self._launch_norm(g, b)
-                        b.ready = 0
+                        b.ready.clear()
             return
         for g in self.groups:
             for b in g.buckets:
@@ -386,7 +395,7 @@ class DistributedDataParallel(nn.Module):
             for b in g.buckets:
                 b.work.wait()
                 b.work = None
-                b.ready = 0
+                b.ready.clear()
                 if self.zero and self.gloo:
                     c = (b.end - b.start) // self.world_size
                     lo = b.start + self.rank * c
@@ -459,8 +468,8 @@ class DistributedDataParallel(nn.Module):
         for g in self.groups:
             for b in g.buckets:
                 b.normed = False
-                if self.world_size == 1:
-                    b.ready = 0
+                if not self.comm:
+                    b.ready.clear()
         self._norm_bad = False
 
     def optimizer_param_groups(self, weight_decay: float = 0.0):

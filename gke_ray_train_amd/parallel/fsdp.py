@@ -19,12 +19,19 @@ Design for 8 x MI355X on xGMI:
   straight into the unit's full gradient buffer (ops/linear.py slots), and when the last one
   lands the buffer is reduce-scattered (SUM; the 1/world average is folded into the optimizer)
   into this rank's gradient shard and freed;
+* gathered-parameter and full-gradient buffers come from a per-size free list (every decoder
+  block has the same size, so after the first step no unit gather or backward allocates: no
+  caching-allocator churn with 1.7 GB 70B blocks); at most ``GRT_FSDP_RS_INFLIGHT`` (2)
+  reduce-scatters are outstanding, so the full-gradient buffers in flight are bounded too;
+* ``GRT_FORCE_COLLECTIVES=1`` runs the collective path (gather into separate buffers,
+  reduce-scatter, replicated all-reduce) even at world size 1, for one-GPU RCCL rehearsal;
 * ``cpu_offload=True``: fp32 Adam moments live in pinned host memory and are streamed through the
   GPU AdamW kernel in chunks on a side stream (H2D of chunk i+1 / D2H of chunk i-1 overlap the
   update of chunk i); parameters and gradients stay in HBM.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import os
 import math
@@ -82,44 +89,58 @@ class _Unit:
         self.slots: Dict[int, GradSlot] = {}
 
 
+def partition_units(module: nn.Module, world: int, unit_types=DEFAULT_UNITS):
+    """The FSDP partition: one unit per transformer block plus a root unit (embeddings, LM head)
+    holding every other matrix; 1-D parameters are replicated. Allocates nothing, so it also runs
+    on a meta-device model (``parallel/planner.py`` sizes a 70B partition this way)."""
+    unit_mods = [m for m in module.modules() if type(m).__name__ in unit_types]
+    owner = {}
+    for ui, m in enumerate(unit_mods):
+        for n, p in m.named_parameters():
+            owner.setdefault(id(p), ui)
+    seen = set()
+    per_unit: List[List[tuple]] = [[] for _ in range(len(unit_mods) + 1)]
+    replicated: List[tuple] = []
+    for n, p in module.named_parameters():
+        if id(p) in seen or not p.requires_grad:
+            continue
+        seen.add(id(p))
+        if p.dim() < 2:
+            replicated.append((n, p))
+        else:
+            per_unit[owner.get(id(p), len(unit_mods))].append((n, p))
+    mods = unit_mods + [module]
+    units = [_Unit(i, mods[i], items, world) for i, items in enumerate(per_unit) if items]
+    return units, replicated
+
+
 class FullyShardedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, unit_types=DEFAULT_UNITS, reshard_after_forward=True,
                  cpu_offload: bool = False, sync_module_states: bool = True, param_init_fn=None, device=None,
-                 offload_chunk_elems: int = 1 << 26):
+                 offload_chunk_elems: int = 1 << 26, force_collectives: Optional[bool] = None):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world > 1 else 0
+        if force_collectives is None:
+            force_collectives = os.environ.get("GRT_FORCE_COLLECTIVES", "0") == "1"
+        self.comm = self.world > 1 or (bool(force_collectives) and dist.is_initialized())
+        self._pool: Dict[int, List[torch.Tensor]] = {}
+        self._rs_inflight = collections.deque()
+        self._rs_cap = max(1, int(os.environ.get("GRT_FSDP_RS_INFLIGHT", "2")))
         self.reshard_after_forward = reshard_after_forward
         self.cpu_offload = cpu_offload
         self.offload_chunk = offload_chunk_elems
         self._sync = True
         # GRT_GLOO_TENSOR_COLLECTIVES=1: run the RCCL code path over gloo (CPU tests), see ddp.py
-        self.gloo = (dist.is_initialized() and dist.get_backend(process_group) == "gloo"
+        self.gloo = (self.comm and dist.get_backend(process_group) == "gloo"
                      and os.environ.get("GRT_GLOO_TENSOR_COLLECTIVES", "0") != "1")
         first = next(module.parameters())
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if first.device.type == "meta" else first.device)
         # ---------------------------------------------------------------- partition parameters
-        unit_mods = [m for m in module.modules() if type(m).__name__ in unit_types]
-        owner = {}
-        for ui, m in enumerate(unit_mods):
-            for n, p in m.named_parameters():
-                owner.setdefault(id(p), ui)
-        seen = set()
-        per_unit: List[List[tuple]] = [[] for _ in range(len(unit_mods) + 1)]
-        self.replicated: List[tuple] = []
-        for n, p in module.named_parameters():
-            if id(p) in seen or not p.requires_grad:
-                continue
-            seen.add(id(p))
-            if p.dim() < 2:
-                self.replicated.append((n, p))
-            else:
-                per_unit[owner.get(id(p), len(unit_mods))].append((n, p))
-        mods = unit_mods + [module]
-        self.units = [_Unit(i, mods[i], items, self.world) for i, items in enumerate(per_unit) if items]
+        self.units, self.replicated = partition_units(module, self.world, unit_types)
         self.dtype = next((p.dtype for u in self.units for p in u.params), torch.bfloat16)
         if self.dtype == torch.float32 and first.device.type != "meta":
             self.dtype = first.dtype
@@ -198,7 +219,7 @@ class FullyShardedDataParallel(nn.Module):
         if sync and self.world > 1:
             dist.broadcast(full, 0, group=self.pg)
         u.shard.copy_(full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel])
-        if self.world == 1:
+        if not self.comm:
             self._bind(u, u.shard)  # single rank: the shard IS the full buffer, never freed
         else:
             self._unbind(u)
@@ -209,18 +230,34 @@ class FullyShardedDataParallel(nn.Module):
         for p, o, n, s in zip(u.params, u.offsets, u.numels, u.shapes):
             p.data = full[o:o + n].view(s)
 
+    def _acquire(self, n: int, zero: bool = False) -> torch.Tensor:
+        free = self._pool.get(n)
+        buf = free.pop() if free else torch.empty(n, dtype=self.dtype, device=self.device)
+        if zero:
+            buf.zero_()
+        return buf
+
+    def _release(self, buf: Optional[torch.Tensor]):
+        # Stream safety: the next user of a gather buffer is an all-gather, which RCCL orders after
+        # the compute stream's queued kernels at issue; a gradient buffer comes back only after its
+        # reduce-scatter was waited on (compute stream joined RCCL's), and is re-zeroed on it.
+        if buf is not None and buf.numel() > 0:
+            self._pool.setdefault(buf.numel(), []).append(buf)
+
     def _unbind(self, u: _Unit):
-        if self.world == 1:
+        if not self.comm:
             return
+        if u.full is not None and u.full is not u.shard:
+            self._release(u.full)
         u.full = None
         for p in u.params:
             p.data = torch.empty(0, dtype=self.dtype, device=self.device)
 
     # ================================================================ all-gather
     def _issue_gather(self, u: _Unit):
-        if u.full is not None or u.gather_work is not None or self.world == 1:
+        if u.full is not None or u.gather_work is not None or not self.comm:
             return
-        buf = torch.empty(u.total, dtype=self.dtype, device=self.device)
+        buf = self._acquire(u.total)
         if self.gloo:
             parts = list(buf.chunk(self.world))
             u.gather_work = dist.all_gather(parts, u.shard, group=self.pg, async_op=True)
@@ -229,7 +266,7 @@ class FullyShardedDataParallel(nn.Module):
         u._pending_buf = buf
 
     def _wait_gather(self, u: _Unit):
-        if self.world == 1:
+        if not self.comm:
             return
         if u.full is None and u.gather_work is None:
             self._issue_gather(u)
@@ -286,8 +323,7 @@ class FullyShardedDataParallel(nn.Module):
     def _alloc_grads(self, u: _Unit):
         if u.grad_full is not None:
             return
-        g = torch.empty(u.total, dtype=self.dtype, device=self.device)
-        g.zero_()  # alignment gaps must not inject garbage into the reduction
+        g = self._acquire(u.total, zero=True)  # alignment gaps must not inject garbage into the reduction
         u.grad_full = g
         u.ready = 0
         for p, o, n, s in zip(u.params, u.offsets, u.numels, u.shapes):
@@ -337,11 +373,12 @@ class FullyShardedDataParallel(nn.Module):
 
     def _reduce_scatter(self, u: _Unit):
         g = u.grad_full
-        if self.world == 1:
+        if not self.comm:
             if self._accumulating(u):
                 u.shard_grad.add_(g)
             else:
                 u.shard_grad.copy_(g)
+            self._release(g)
         else:
             if self.gloo:
                 dist.all_reduce(g, group=self.pg)
@@ -350,6 +387,7 @@ class FullyShardedDataParallel(nn.Module):
                     u.shard_grad.add_(part)
                 else:
                     u.shard_grad.copy_(part)
+                self._release(g)
             else:
                 if u.rs_work is not None:  # previous micro-step's reduce-scatter of this unit
                     self._finish_rs(u)
@@ -357,6 +395,11 @@ class FullyShardedDataParallel(nn.Module):
                 u.rs_work = dist.reduce_scatter_tensor(out, g, op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
                 u.rs_out = out if out is not u.shard_grad else None
                 u._rs_src = g
+                self._rs_inflight.append(u)
+                while len(self._rs_inflight) > self._rs_cap:  # bound the full-gradient buffers in flight
+                    old = self._rs_inflight.popleft()
+                    if old.rs_work is not None:
+                        self._finish_rs(old)
         u.grad_full = None
         u.in_backward = False
         u.ready = 0
@@ -364,8 +407,7 @@ class FullyShardedDataParallel(nn.Module):
         if u.module is not self.module:
             self._unbind(u)
 
-    @staticmethod
-    def _finish_rs(u: _Unit):
+    def _finish_rs(self, u: _Unit):
         """Wait a unit's reduce-scatter (stream-ordered for RCCL) and fold an accumulation
         temporary into the shard; its source buffer may be released only after this."""
         u.rs_work.wait()
@@ -373,6 +415,7 @@ class FullyShardedDataParallel(nn.Module):
         if u.rs_out is not None:
             u.shard_grad.add_(u.rs_out)
             u.rs_out = None
+        self._release(u._rs_src)
         u._rs_src = None
 
     def _accumulating(self, u):
@@ -416,9 +459,10 @@ class FullyShardedDataParallel(nn.Module):
         for u in self.units:
             if u.rs_work is not None:
                 self._finish_rs(u)
-        if self.world > 1 and self.replicated and self._sync:
+        self._rs_inflight.clear()
+        if self.comm and self.replicated and self._sync:
             dist.all_reduce(self.rep_grad, group=self.pg)
-        if self._root_unit is not None and self.world > 1:
+        if self._root_unit is not None and self.comm:
             self._unbind(self._root_unit)
 
     def zero_grad(self, set_to_none: bool = True):
@@ -462,7 +506,7 @@ class FullyShardedDataParallel(nn.Module):
         ss_shard = st.buf[0] ** 2
         st2 = _clip([self.rep_grad], 0.0, prescale=1.0)
         ss_rep = st2.buf[0] ** 2
-        if self.world > 1:
+        if self.comm:
             small_all_reduce(ss_shard, group=self.pg)
         total = (ss_shard + ss_rep).sqrt() / self.world
         coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(total)
@@ -478,7 +522,7 @@ class FullyShardedDataParallel(nn.Module):
             self._wait_gather(u)
             for n, p in zip(u.names, u.params):
                 out[n] = p.detach().clone()
-            if u.module is not self.module or self.world > 1:
+            if u.module is not self.module or self.comm:
                 self._unbind(u)
         for n, p in self.replicated:
             out[n] = p.detach().clone()
@@ -491,7 +535,7 @@ class FullyShardedDataParallel(nn.Module):
         """Unsharded gradients (sum over ranks), module parameter names — tests / debugging."""
         out = {}
         for u in self.units:
-            if self.world > 1:
+            if self.comm:
                 parts = [torch.empty_like(u.shard_grad) for _ in range(self.world)]
                 dist.all_gather(parts, u.shard_grad.contiguous(), group=self.pg)
                 full = torch.cat(parts)

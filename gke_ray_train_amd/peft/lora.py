@@ -107,7 +107,10 @@ def _packed(ts):
 
 
 def _slot_of(p):
-    return getattr(p, "_grt_slot", None) if _LORA_DIRECT_GRAD and p.requires_grad else None
+    sl = getattr(p, "_grt_slot", None) if _LORA_DIRECT_GRAD and p.requires_grad else None
+    if sl is not None and sl.view.dtype != p.dtype:  # e.g. fp32 gradient buffers under bf16 adapters
+        return None
+    return sl
 
 
 class _LoraFn(torch.autograd.Function):
@@ -137,7 +140,9 @@ class _LoraFn(torch.autograd.Function):
             order, acat = pk
         # h = dropout(x) A^T in one pass over x (lora.hip; split over K when there are fewer than
         # ~3 32-token workgroups per CU); x_d is kept for the dA GEMM
-        res = C.lora_down(x2, acat, p, seed, offset, p > 0) if _LORA_DOWN and x2.shape[0] >= 256 else []
+        # the HIP adapter kernels are bf16-only (fp32 / fp16 adapters take the GEMM + dropout path)
+        bf16 = x2.dtype == torch.bfloat16 and acat.dtype == torch.bfloat16 and x2.is_cuda
+        res = C.lora_down(x2, acat, p, seed, offset, p > 0) if _LORA_DOWN and bf16 and x2.shape[0] >= 256 else []
         if res:
             h = res[0]
             xd = res[1] if p > 0 else x2
@@ -206,7 +211,8 @@ class _LoraFn(torch.autograd.Function):
                     dAs[i] = rows
         if dx is not None:
             # dx += drop'(g A): one read-modify-write of dx (lora.hip), else GEMM + dropout backward
-            if not (_LORA_DX and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
+            bf16 = g.dtype == acat.dtype == dx.dtype == torch.bfloat16 and g.is_cuda
+            if not (_LORA_DX and bf16 and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
                 if ctx.p > 0:
                     C.dropout_bwd_seeded(g @ acat, dx, ctx.p, ctx.seed, ctx.offset, True)
                 else:

@@ -12,6 +12,11 @@ Design for one MI355X node instead of a GKE/KubeRay cluster:
   index (``GRT_ASSIGNED_GPU``) but keep every device visible so RCCL can use xGMI peer access;
 * arguments/results travel as cloudpickle payloads over pipes; large numpy / torch CPU payloads
   go through the shared-memory object store (``runtime/object_store.py``) instead;
+* GPUs are LEASED from a node-wide ledger (``runtime/gpu_ledger.py``: one ``flock``-ed file per
+  GPU under the node's grt tmpdir), so concurrent drivers — e.g. two jobs submitted to one
+  ``grt start --head`` cluster, each attaching with ``ray.init(address='auto')`` — never hold the
+  same GPU; a lease dies with its process. Tasks and actors learn their GPUs through
+  ``GRT_ASSIGNED_GPU`` / ``get_gpu_ids()`` (Ray's ``ray.get_gpu_ids()``);
 * failures surface exactly where the reference expects them: a raising task -> ``RayTaskError``
   from ``get``; a dead worker/actor process -> ``WorkerCrashedError`` / ``ActorDiedError``;
   ``get(timeout=)`` -> ``GetTimeoutError``.
@@ -94,7 +99,12 @@ def _worker_main(q_in, q_out, env, working_dir, actor_spec):
         msg = q_in.get()
         if msg is None:
             break
-        task_id, payload = msg
+        task_id, payload, gpus = msg if len(msg) == 3 else (*msg, None)
+        if gpus is not None:  # this task's GPU lease (pooled workers run tasks of different GPUs)
+            if gpus:
+                os.environ["GRT_ASSIGNED_GPU"] = ",".join(map(str, gpus))
+            else:
+                os.environ.pop("GRT_ASSIGNED_GPU", None)
         name = "?"
         try:
             fn, args, kwargs, name = cloudpickle.loads(payload)
@@ -173,7 +183,8 @@ class Runtime:
         self._idle: List[_Proc] = []
         self._all: List[_Proc] = []
         self._free_cpus = self.num_cpus
-        self._free_gpus = list(range(int(self.num_gpus)))
+        from .gpu_ledger import GpuLedger
+        self._ledger = GpuLedger.for_node(int(self.num_gpus))
         self._task_res: Dict[str, tuple] = {}
         self._actors: Dict[str, "_ActorState"] = {}
         self._stop = threading.Event()
@@ -272,26 +283,30 @@ class Runtime:
                 if not self._deps_ready(t):
                     still.append(t)
                     continue
-                if t.num_cpus > self._free_cpus or t.num_gpus > len(self._free_gpus):
+                if t.num_cpus > self._free_cpus:
+                    still.append(t)
+                    continue
+                gpus = self._ledger.try_acquire(int(t.num_gpus))
+                if gpus is None:  # held by this or another driver on the node: wait (Ray semantics)
                     still.append(t)
                     continue
                 try:
                     args, kwargs = self._materialize_args(t)
                 except BaseException as e:  # dependency failed: propagate
+                    self._ledger.release(gpus)
                     self._set(t.task_id, False, payload=cloudpickle.dumps(
                         e if isinstance(e, RayTaskError) else RayTaskError(t.name, traceback.format_exc())))
                     continue
-                gpus = [self._free_gpus.pop(0) for _ in range(int(t.num_gpus))]
                 self._free_cpus -= t.num_cpus
                 w = self._idle.pop() if self._idle else self._spawn(gpus)
                 w.busy = t.task_id
                 self._task_res[t.task_id] = (t, w, gpus)
                 payload = cloudpickle.dumps((t.fn, object_store.pack_args(args), object_store.pack_args(kwargs), t.name))
-                w.q_in.put((t.task_id, payload))
+                w.q_in.put((t.task_id, payload, gpus))
             self._waiting = still
 
     def _spawn(self, gpus):
-        env = dict(self.runtime_env.get("env_vars", {}))
+        env = dict(self.runtime_env.get("env_vars", {}))  # the GPU lease travels with each task
         p = _Proc(env, self.runtime_env.get("working_dir"), name="grt-worker")
         self._all.append(p)
         return p
@@ -321,20 +336,23 @@ class Runtime:
                     w.busy = None
                     self._idle.append(w)
                 self._free_cpus += t.num_cpus
-                self._free_gpus.extend(gpus)
-                self._free_gpus.sort()
+                self._ledger.release(gpus)
                 del self._task_res[tid]
 
     # -- actors
     def create_actor(self, cls, args, kwargs, num_cpus=0.0, num_gpus=0.0, name=None, env=None):
-        with self._lock:
-            ngpu = int(num_gpus)
-            deadline = time.monotonic() + 600
-            while len(self._free_gpus) < ngpu:
-                if time.monotonic() > deadline:
-                    raise RuntimeError(f"cannot place actor needing {ngpu} GPUs")
-                time.sleep(0.01)
-            gpus = [self._free_gpus.pop(0) for _ in range(ngpu)]
+        ngpu = int(num_gpus)
+        if ngpu > self.num_gpus:
+            raise ValueError(f"actor {name or cls.__name__} requests {ngpu} GPUs, node has {int(self.num_gpus)}")
+        deadline = time.monotonic() + float(os.environ.get("GRT_PLACEMENT_TIMEOUT_S", "600"))
+        while True:
+            with self._lock:
+                gpus = self._ledger.try_acquire(ngpu)
+            if gpus is not None:
+                break
+            if time.monotonic() > deadline:
+                raise RuntimeError(f"cannot place actor needing {ngpu} GPUs (leased: {self._ledger.describe()})")
+            time.sleep(0.05)
         aenv = dict(self.runtime_env.get("env_vars", {}))
         aenv.update(env or {})
         if gpus:
@@ -347,13 +365,12 @@ class Runtime:
 
     def release_actor(self, st: "_ActorState"):
         with self._lock:
-            self._free_gpus.extend(st.gpus)
-            self._free_gpus.sort()
+            self._ledger.release(st.gpus)
             st.gpus = []
         self._actors.pop(st.actor_id, None)
 
     def available_resources(self):
-        return {"CPU": self._free_cpus, "GPU": float(len(self._free_gpus))}
+        return {"CPU": self._free_cpus, "GPU": float(self._ledger.num_free())}
 
     def cluster_resources(self):
         return {"CPU": self.num_cpus, "GPU": self.num_gpus}
@@ -365,6 +382,7 @@ class Runtime:
         for p in self._all:
             p.stop()
         self._all.clear()
+        self._ledger.close()
 
 
 class _ActorState:
@@ -516,3 +534,9 @@ def nodes():
 
 def kill(actor_handle, no_restart=True):
     actor_handle._state.kill()
+
+
+def get_gpu_ids() -> List[int]:
+    """GPU indices leased to the calling task / actor (``ray.get_gpu_ids()``)."""
+    v = os.environ.get("GRT_ASSIGNED_GPU", "")
+    return [int(x) for x in v.split(",") if x.strip()]

@@ -104,14 +104,32 @@ class _DeviceLoader:
             return
         with torch.cuda.stream(stream):
             nxt = self._move(first)
+        compute = torch.cuda.current_stream(self.device)
         for b in it:
-            torch.cuda.current_stream(self.device).wait_stream(stream)
+            compute.wait_stream(stream)
             cur = nxt
+            _record_stream(cur, compute)
             with torch.cuda.stream(stream):
                 nxt = self._move(b)
             yield cur
-        torch.cuda.current_stream(self.device).wait_stream(stream)
+        compute.wait_stream(stream)
+        _record_stream(nxt, compute)
         yield nxt
+
+
+def _record_stream(b, stream):
+    """Batches are allocated on the copy stream but read on the compute stream: tell the caching
+    allocator, so a dropped batch's memory is not handed to the next H2D copy while compute
+    kernels queued on ``stream`` still read it."""
+    if isinstance(b, torch.Tensor):
+        if b.is_cuda:
+            b.record_stream(stream)
+    elif isinstance(b, (list, tuple)):
+        for x in b:
+            _record_stream(x, stream)
+    elif isinstance(b, dict):
+        for x in b.values():
+            _record_stream(x, stream)
 
 
 def prepare_data_loader(data_loader: DataLoader, add_dist_sampler: bool = True, move_to_device: bool = True,

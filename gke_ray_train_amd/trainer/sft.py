@@ -151,8 +151,35 @@ def _rng_restore(rng: Dict[str, Any]):
     n = rng.get("numpy")
     if isinstance(n, dict):
         np.random.set_state((n["name"], n["keys"].numpy().astype(np.uint32), n["pos"], n["has_gauss"], n["cached"]))
-    if "cuda" in rng and torch.cuda.is_available() and len(rng["cuda"]) == torch.cuda.device_count():
-        torch.cuda.set_rng_state_all(rng["cuda"])
+    elif isinstance(n, (tuple, list)) and len(n) == 5:  # HF / legacy layout: np.random.get_state() itself
+        np.random.set_state(tuple(n))
+    cu = rng.get("cuda")
+    if cu is not None and torch.cuda.is_available():
+        if isinstance(cu, torch.Tensor):  # HF single-GPU layout
+            torch.cuda.set_rng_state(cu)
+        elif len(cu) == torch.cuda.device_count():
+            torch.cuda.set_rng_state_all(cu)
+
+
+def _rng_load(path: str) -> Optional[Dict[str, Any]]:
+    """Read an rng_state_<rank>.pth without executing pickled code: weights_only first, then
+    weights_only with numpy's array-reconstruction globals allow-listed (HF checkpoints and the
+    pre-round-3 layout keep ``np.random.get_state()``'s ndarray). An unreadable file is skipped
+    with a warning — resuming with fresh RNG streams beats refusing to resume."""
+    try:
+        return torch.load(path, weights_only=True)
+    except Exception:
+        pass
+    try:
+        core = getattr(np, "_core", None) or np.core
+        allowed = [core.multiarray._reconstruct, np.ndarray, np.dtype]
+        allowed += [getattr(np.dtypes, n) for n in ("UInt32DType", "Int64DType", "Float64DType") if hasattr(np, "dtypes")]
+        with torch.serialization.safe_globals(allowed):
+            return torch.load(path, weights_only=True)
+    except Exception as e:  # noqa: BLE001
+        import warnings
+        warnings.warn(f"cannot restore RNG state from {path} ({e.__class__.__name__}: {e}); continuing with fresh streams")
+        return None
 
 
 def _rank_uniform_error(err: Optional[BaseException], world: int, what: str):
@@ -615,5 +642,7 @@ class SFTTrainer:
         self.state.update(st)
         rp = os.path.join(d, f"rng_state_{self.rank}.pth")
         if os.path.exists(rp):  # continue the RNG streams (dropout masks, sampler) where they stopped
-            _rng_restore(torch.load(rp, weights_only=True))
+            rng = _rng_load(rp)
+            if rng is not None:
+                _rng_restore(rng)
         return int(st["global_step"])

@@ -28,8 +28,10 @@ def _batch(world, accum):
     return torch.randint(0, 512, (2 * world * accum, 128), generator=g)
 
 
-def _worker(rank, world, port, q, engine, accum):
+def _worker(rank, world, port, q, engine, accum, tensor_coll=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if tensor_coll:  # the RCCL call pattern (reduce_scatter_tensor / all_gather_into_tensor) over gloo
+        os.environ["GRT_GLOO_TENSOR_COLLECTIVES"] = "1"
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -56,13 +58,14 @@ def _worker(rank, world, port, q, engine, accum):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("engine,accum", [("ddp", 1), ("ddp", 2), ("fsdp", 2)])
-def test_two_ranks_on_one_gpu_match_single_process(engine, accum):
+@pytest.mark.parametrize("engine,accum,tensor_coll", [("ddp", 1, False), ("ddp", 2, False), ("fsdp", 2, False),
+                                                      ("fsdp", 2, True)])
+def test_two_ranks_on_one_gpu_match_single_process(engine, accum, tensor_coll):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, engine, accum)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, engine, accum, tensor_coll)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -1,0 +1,63 @@
+"""Memory preflight (parallel/planner.py) and the full 80-layer Llama-3-70B FSDP partition at world 8,
+sized on a meta-device model (BASELINE config #5 readiness without an 8-GPU box)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from gke_ray_train_amd.models import get_config
+from gke_ray_train_amd.parallel.planner import GiB, plan_memory, preflight
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HBM = 288e9
+
+
+def test_llama3_70b_partition_world8_on_meta():
+    cfg = get_config("llama3-70b")
+    plan = plan_memory(cfg, 8, "fsdp", offload=True, micro_batch=1, seq=1024, hbm_capacity=HBM, host_capacity=2e12)
+    u = plan.units
+    assert u["decoder_units"] == 80 and u["root_units"] == 1
+    h, f, kv = 8192, 28672, 1024
+    block = (h + 2 * kv) * h + h * h + 2 * f * h + h * f  # fused qkv, o, fused gate/up, down
+    assert u["block_params"] == block == 855_638_016
+    assert u["block_shard_params"] == block // 8  # 64-aligned already
+    assert u["root_params"] == 2 * 128256 * h  # embed_tokens + lm_head
+    assert u["replicated_params"] == 80 * 2 * h + h  # norm weights
+    # one-ahead prefetch: the running block + the prefetched one + the root unit
+    assert u["peak_gathered_bytes"] == (2 * block + 2 * 128256 * h) * 2
+    # every parameter is in exactly one shard / the replicated set
+    assert 80 * block + u["root_params"] + u["replicated_params"] == cfg.num_params()
+    # offload moves the 8 B/param fp32 moments of the shard to pinned host memory
+    assert abs(plan.host_per_rank["adam_moments_fp32"] - 8.0 * (80 * block + u["root_params"]) / 8) < 1e6
+    assert plan.fits and plan.hbm_total < 100 * GiB
+
+
+def test_70b_refusals_are_explicit():
+    cfg = get_config("llama3-70b")
+    one = plan_memory(cfg, 1, "fsdp", hbm_capacity=HBM, host_capacity=2e12)
+    assert not one.fits and any(p.startswith("HBM") for p in one.problems())
+    with pytest.raises(MemoryError, match="does not fit"):
+        preflight(one)
+    # 8 ranks x 66 GiB of pinned moments needs more host RAM than 256 GiB
+    small_host = plan_memory(cfg, 8, "fsdp", offload=True, micro_batch=1, hbm_capacity=HBM, host_capacity=256 * GiB)
+    assert any(p.startswith("host RAM") for p in small_host.problems())
+
+
+def test_7b_headline_config_fits_and_zero_shrinks_optimizer():
+    cfg = get_config("llama2-7b")
+    one = plan_memory(cfg, 1, "ddp", micro_batch=8, seq=1024, hbm_capacity=HBM)
+    eight = plan_memory(cfg, 8, "ddp", micro_batch=8, seq=1024, hbm_capacity=HBM)
+    assert one.fits and eight.fits
+    assert eight.hbm_per_rank["adam_moments_fp32"] * 8 == pytest.approx(one.hbm_per_rank["adam_moments_fp32"])
+    qlora = plan_memory(get_config("llama3.1-8b"), 1, "ddp", peft="qlora", micro_batch=2, seq=1024, hbm_capacity=HBM)
+    assert qlora.hbm_per_rank["frozen_base"] < 8 * GiB
+
+
+def test_bench_plan_only_cli():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--plan-only", "--model", "llama2-7b",
+                        "--device", "cpu"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])["memory_plan"]
+    assert d["model"] == "llama2-7b" and d["fits"] is True

@@ -85,3 +85,31 @@ def test_dropout_seed_offset_follows_cpu_rng():
     torch.manual_seed(1)
     assert dropout_seed_offset(torch.empty(8)) == a
     assert a != b and a[1] == 0 and 0 <= a[0] < 2 ** 62
+
+
+def test_rng_state_legacy_and_hf_layouts_resume(tmp_path):
+    """rng_state_<rank>.pth holding np.random.get_state() as a tuple with an ndarray (HF layout and
+    this repo's pre-round-3 files) resumes through the weights-only loader with numpy's array
+    globals allow-listed; an unreadable file is skipped with a warning."""
+    import random
+    import warnings
+
+    import numpy as np
+    import torch
+
+    from gke_ray_train_amd.trainer.sft import _rng_load, _rng_restore
+    st = np.random.get_state()
+    p = tmp_path / "rng_state_0.pth"
+    torch.save({"python": random.getstate(), "numpy": st, "cpu": torch.get_rng_state()}, str(p))
+    rng = _rng_load(str(p))
+    assert rng is not None
+    np.random.rand(7)
+    _rng_restore(rng)
+    a = np.random.rand(4)
+    np.random.set_state(st)
+    assert (a == np.random.rand(4)).all()
+    p.write_bytes(b"not a checkpoint")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert _rng_load(str(p)) is None
+    assert any("cannot restore RNG state" in str(x.message) for x in w)
