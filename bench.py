@@ -413,7 +413,7 @@ def run(a):
             "loss": round(float(loss.item()) * accum, 4),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

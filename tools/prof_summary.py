@@ -4,8 +4,16 @@ import csv
 import sys
 
 
+def _rows_from_db(path):
+    """rocprofv3 7.x writes a rocpd SQLite database; its ``top_kernels`` view has µs totals."""
+    import sqlite3
+    c = sqlite3.connect(path)
+    return [{"Name": n, "TotalDurationNs": t * 1e3, "Calls": k}
+            for n, k, t in c.execute("select name, total_calls, total_duration from top_kernels")]
+
+
 def main(path, title="", steps=None, top=40):
-    rows = list(csv.DictReader(open(path)))
+    rows = _rows_from_db(path) if path.endswith(".db") else list(csv.DictReader(open(path)))
     key_t = next(k for k in rows[0] if "TotalDuration" in k)
     key_c = next(k for k in rows[0] if k.lower() == "calls")
     tot = sum(float(r[key_t]) for r in rows)
