@@ -136,7 +136,7 @@ def input_grad(dy2: torch.Tensor, w: torch.Tensor, wt_ev=None) -> torch.Tensor:
     return dy2 @ w
 # Opt-in: the one-pass backward gives each vocabulary row to one wave, which serialises on the
 # hottest tokens of a Zipf-distributed batch (measured +6.5 ms per Llama-2-7B step vs torch's
-# partial-segment scheme, tools/gpu_emb_ab.sh); the forward gather and the uniform-id case are fine.
+# partial-segment scheme, an A/B run, profiles/r1_embedding_ab.txt); the forward gather and the uniform-id case are fine.
 _NATIVE_EMBEDDING = os.environ.get("GRT_NATIVE_EMBEDDING", "0") == "1"
 
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC passes (one counter group per pass) + a kernel trace over an arbitrary python command:
-#   bash tools/gpu_pmc_cmd.sh <outdir under gpurun_out> <script.py> [args...]
+#   bash scripts/gpu_pmc_cmd.sh <outdir under gpurun_out> <script.py> [args...]
 # then: python3 tools/pmc_summary.py gpurun_out/<outdir>
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/$1

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Every hand-written gfx950 kernel of the hot paths at its production shape, a few launches each,
-for rocprofv3 PMC passes (tools/gpu_pmc_zoo.sh). Shapes: the Llama-2-7B training step (8 x 1024
+for rocprofv3 PMC passes (scripts/gpu_pmc_zoo.sh). Shapes: the Llama-2-7B training step (8 x 1024
 tokens) and the Llama-3.1-8B decode step."""
 import os
 import sys

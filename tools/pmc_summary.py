@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise tools/gpu_pmc_zoo.sh output: per kernel, mean duration (kernel trace), MFMA busy share,
+"""Summarise scripts/gpu_pmc_zoo.sh output: per kernel, mean duration (kernel trace), MFMA busy share,
 wave-state split, LDS bank-conflict cycles, HBM-side bytes and bandwidth.
 
 Derived columns (MI355X: 256 CUs x 4 SIMDs):
