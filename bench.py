@@ -266,14 +266,19 @@ def run(a):
         def next_batch(_i):
             return next(it)[0]
     elif a.data == "pipeline":
+        # Ray-Data streaming (BASELINE config #4): windowed shuffle -> map_batches, ONE execution in
+        # a coordinator process (rank 0 hosts it) dealing equal row shares to the ranks, pinned-ring
+        # H2D prefetch on a copy stream (data/pipeline.py)
+        if a.sp > 1:
+            raise SystemExit("--data pipeline deals one split per data-parallel rank; use it with --sp 1")
         from gke_ray_train_amd.data.pipeline import Dataset
         n_win = total_micro * mb * dp_world + 8 * dp_world
         toks = synthetic_tokens(n_win * a.seq, cfg.vocab_size, seed=7)
-        ds = (Dataset.from_numpy({"input_ids": toks.reshape(n_win, a.seq)}, parallelism=16)
+        ds = (Dataset.from_numpy({"input_ids": toks.reshape(n_win, a.seq)}, parallelism=max(16, 4 * dp_world))
               .random_shuffle(seed=3)
               .map_batches(lambda b: {"input_ids": b["input_ids"].astype(np.int64)}))
-        it = iter(ds.shard_for_rank(dp_rank, dp_world).iter_torch_batches(
-            batch_size=mb, device=dev, drop_last=True, producer_process=True))
+        split = ds.streaming_split_for_rank(dp_rank, dp_world)
+        it = iter(split.iter_torch_batches(batch_size=mb, device=dev, drop_last=True, prefetch_batches=4))
 
         def next_batch(_i):
             return next(it)["input_ids"]
@@ -395,7 +400,7 @@ def run(a):
             "vs_baseline": None,
             "dtype": "bf16" if not cpu else "fp32",
             "data": "synthetic Wikitext-2-shaped token stream (Zipf ids) via "
-                    + {"loader": "the streaming loader", "pipeline": "the Ray-Data-like pipeline (shm-ring producer process)",
+                    + {"loader": "the streaming loader", "pipeline": "the Ray-Data-like streaming pipeline (coordinated streaming_split, pinned-ring H2D)",
                        "static": "on-device batches"}[a.data] + "; random-init weights",
             "config": {"model": cfg.name, "global_batch": a.batch * (world // a.sp), "seq_len": a.seq, "parallelism": par,
                        "micro_batch": mb, "grad_accum": accum, "optimizer": "fused AdamW fp32 states",

@@ -84,7 +84,18 @@ def _apply_env(env: Dict[str, str], working_dir: Optional[str]):
             sys.path.insert(0, working_dir)
 
 
-def _worker_main(q_in, q_out, env, working_dir, actor_spec):
+def _orphan_watchdog(parent: int):
+    """Workers are not daemonic (so they may start their own children: DataLoader workers, data
+    coordinators — as Ray actors can); instead each exits when its driver disappears."""
+    while True:
+        time.sleep(1.0)
+        if os.getppid() != parent:
+            os._exit(1)
+
+
+def _worker_main(q_in, q_out, env, working_dir, actor_spec, parent=None):
+    if parent is not None:
+        threading.Thread(target=_orphan_watchdog, args=(parent,), daemon=True, name="grt-orphan").start()
     _apply_env(env, working_dir)
     instance = None
     if actor_spec is not None:
@@ -134,8 +145,9 @@ class _Proc:
     def __init__(self, env, working_dir, actor_spec=None, name="worker"):
         self.q_in = _CTX.Queue()
         self.q_out = _CTX.Queue()
-        self.proc = _CTX.Process(target=_worker_main, args=(self.q_in, self.q_out, env, working_dir, actor_spec),
-                                 daemon=True, name=name)
+        self.proc = _CTX.Process(target=_worker_main, args=(self.q_in, self.q_out, env, working_dir, actor_spec,
+                                                            os.getpid()),
+                                 daemon=False, name=name)
         self.proc.start()
         self.busy: Optional[str] = None
         self.pending: List[str] = []
@@ -487,6 +499,8 @@ def init(address: Optional[str] = None, *, num_cpus=None, num_gpus=None, ignore_
         if runtime_env and runtime_env.get("env_vars"):
             os.environ.update({k: str(v) for k, v in runtime_env["env_vars"].items()})
         _RUNTIME = Runtime(num_cpus=num_cpus, num_gpus=num_gpus, runtime_env=runtime_env, namespace=namespace)
+        import atexit
+        atexit.register(shutdown)  # before multiprocessing joins its (non-daemonic) children
         return _RUNTIME
 
 

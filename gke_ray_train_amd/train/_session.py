@@ -171,6 +171,6 @@ def get_dataset_shard(name: str = "train"):
     ds = s.datasets.get(name)
     if ds is None:
         return None
-    if hasattr(ds, "shard_for_rank"):
+    if hasattr(ds, "shard_for_rank"):  # a Dataset handed over directly (TorchTrainer passes splits)
         return ds.shard_for_rank(s.ctx.world_rank, s.ctx.world_size)
-    return ds
+    return ds  # this rank's StreamSplit of the driver's streaming_split

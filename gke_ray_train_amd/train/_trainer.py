@@ -172,16 +172,31 @@ class DataParallelTrainer:
                               experiment_name=storage.experiment_name, trial_dir=storage.trial_dir,
                               storage_path=storage.storage_path)
             payload = cloudpickle.dumps(self.fn)
+            # Ray Train: each dataset is streaming_split once in the driver; worker r consumes split r
+            # of ONE execution (a coordinator process deals the rows), not its own re-execution
+            per_rank = [dict() for _ in range(n)]
+            coords = []
+            for name, ds in self.datasets.items():
+                if hasattr(ds, "streaming_split"):
+                    splits = ds.streaming_split(n, equal=True)
+                    coords.append(splits)
+                    for r in range(n):
+                        per_rank[r][name] = splits[r]
+                else:
+                    for r in range(n):
+                        per_rank[r][name] = ds
             refs = []
             for r, a in enumerate(actors):
                 local_rank = gpus[r] if (use_gpu and gpus[r] >= 0) else r
                 refs.append(a.run.remote(payload, self.config, r, n, local_rank, n, "127.0.0.1", master_port, backend,
                                          timeout_s, ctx_fields, address, authkey, ckpt.path if ckpt else None,
-                                         self.datasets, storage.iteration if ckpt else 0, attempt, use_gpu))
+                                         per_rank[r], storage.iteration if ckpt else 0, attempt, use_gpu))
             self._serve(listener, refs, n, storage)
             rt.get(refs, timeout=600)
         finally:
             listener.close()
+            for splits in locals().get("coords", []):
+                splits[0].shutdown()
             for a in actors:
                 try:
                     rt.kill(a)

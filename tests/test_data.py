@@ -99,7 +99,7 @@ def test_streaming_split_producer_process_matches_in_process():
     from gke_ray_train_amd.data.pipeline import Dataset
     ds = Dataset.from_numpy(np.arange(4000, dtype=np.int64).reshape(1000, 4)).map_batches(
         lambda b: {"x": b["data"] * 2, "y": b["data"].sum(1)})
-    it = ds.streaming_split(2)[1]
+    it = ds.shard_for_rank(1, 2)
     a = list(it.iter_torch_batches(batch_size=64, device="cpu"))
     b = list(it.iter_torch_batches(batch_size=64, device="cpu", producer_process=True))
     assert len(a) == len(b) > 3
