@@ -490,7 +490,8 @@ void check_bshd(const Tensor& t, const char* name) {
 }
 
 grt::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, Tensor& lse,
-                            double scale, bool causal, const optional<Tensor>& seqlens_k) {
+                            double scale, bool causal, const optional<Tensor>& seqlens_k,
+                            const optional<Tensor>& cu_seqlens = {}, int64_t max_seqlen = 0) {
   check_bshd(q, "q");
   check_bshd(k, "k");
   check_bshd(v, "v");
@@ -501,9 +502,11 @@ grt::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, c
   TORCH_CHECK(k.size(3) == q.size(3), "head_dim mismatch");
   TORCH_CHECK(q.size(0) == k.size(0) && o.sizes() == q.sizes(), "batch/out shape mismatch");
   TORCH_CHECK(q.size(2) % k.size(2) == 0, "Hq must be a multiple of Hkv");
-  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() &&
-                  lse.numel() == q.size(0) * q.size(2) * q.size(1),
-              "lse must be fp32 [B, Hq, Sq]");
+  const bool packed = cu_seqlens.has_value();
+  const int64_t nseq = packed ? cu_seqlens->numel() - 1 : q.size(0);
+  const int64_t sq_rows = packed ? max_seqlen : q.size(1);
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == nseq * q.size(2) * sq_rows,
+              "lse must be fp32 [B, Hq, Sq] ([num_seqs, Hq, max_seqlen] when packed)");
   grt::AttnParams p{};
   p.q = q.data_ptr(); p.k = k.data_ptr(); p.v = v.data_ptr(); p.o = o.data_ptr(); p.lse = lse.data_ptr<float>();
   p.q_bs = q.stride(0); p.q_ss = q.stride(1); p.q_hs = q.stride(2);
@@ -520,6 +523,20 @@ grt::AttnParams make_params(const Tensor& q, const Tensor& k, const Tensor& v, c
     check_contig(*seqlens_k, "seqlens_k");
     TORCH_CHECK(seqlens_k->scalar_type() == at::kInt && seqlens_k->numel() == q.size(0), "seqlens_k int32 [B]");
     p.seqlens_k = seqlens_k->data_ptr<int32_t>();
+  }
+  p.cu_seqlens = nullptr;
+  if (packed) {  // padding-free: [1, T, H, D] tensors, sequence b = token rows [cu[b], cu[b+1])
+    check_contig(*cu_seqlens, "cu_seqlens");
+    TORCH_CHECK(cu_seqlens->scalar_type() == at::kInt && cu_seqlens->is_cuda() && nseq >= 1,
+                "cu_seqlens must be int32 [num_seqs + 1] on the device");
+    TORCH_CHECK(q.scalar_type() == at::kBFloat16, "packed (cu_seqlens) attention: bf16 kernels");
+    TORCH_CHECK(q.size(0) == 1 && k.size(1) == q.size(1), "packed attention: q / k / v are [1, T, H, D]");
+    TORCH_CHECK(causal && !seqlens_k.has_value(), "packed attention is causal self-attention without seqlens_k");
+    TORCH_CHECK(max_seqlen >= 1 && max_seqlen <= q.size(1), "max_seqlen must be in [1, T]");
+    p.cu_seqlens = cu_seqlens->data_ptr<int32_t>();
+    p.B = (int)nseq;
+    p.Sq = p.Sk = (int)max_seqlen;
+    p.q_bs = p.k_bs = p.v_bs = p.o_bs = 0;
   }
   p.drop_seed = 0;
   p.drop_thresh = 0;
@@ -538,11 +555,13 @@ void set_dropout(grt::AttnParams& p, double dropout_p, int64_t seed) {
 
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& out,
                              double scale, bool causal, const optional<Tensor>& seqlens_k, double dropout_p,
-                             int64_t seed) {
+                             int64_t seed, const optional<Tensor>& cu_seqlens, int64_t max_seqlen) {
   c10::OptionalDeviceGuard g(q.device());
   Tensor o = out.has_value() ? *out : at::empty(q.sizes(), q.options());
-  auto lse = at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
-  auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k);
+  auto lse = cu_seqlens.has_value()
+                 ? at::empty({cu_seqlens->numel() - 1, q.size(2), max_seqlen}, q.options().dtype(at::kFloat))
+                 : at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
+  auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k, cu_seqlens, max_seqlen);
   set_dropout(p, dropout_p, seed);
   if (q.scalar_type() == at::kFloat) grt::attn_fwd_f32(p, cur_stream(q));
   else grt::attn_fwd(p, cur_stream(q));
@@ -553,11 +572,12 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
                              Tensor& lse, const optional<Tensor>& dq_out, const optional<Tensor>& dk_out,
                              const optional<Tensor>& dv_out, double scale, bool causal,
                              const optional<Tensor>& seqlens_k, double dropout_p, int64_t seed,
-                             const optional<Tensor>& rope_cos, const optional<Tensor>& rope_sin) {
+                             const optional<Tensor>& rope_cos, const optional<Tensor>& rope_sin,
+                             const optional<Tensor>& cu_seqlens, int64_t max_seqlen) {
   c10::OptionalDeviceGuard g(q.device());
   check_bshd(dout, "dout");
   TORCH_CHECK(dout.sizes() == q.sizes(), "dout shape");
-  auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k);
+  auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k, cu_seqlens, max_seqlen);
   set_dropout(p, dropout_p, seed);
   Tensor dq = dq_out.has_value() ? *dq_out : at::empty(q.sizes(), q.options());
   Tensor dk = dk_out.has_value() ? *dk_out : at::empty(k.sizes(), k.options());
@@ -573,6 +593,7 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   bp.dq = dq.data_ptr(); bp.dq_bs = dq.stride(0); bp.dq_ss = dq.stride(1); bp.dq_hs = dq.stride(2);
   bp.dk = dk.data_ptr(); bp.dk_bs = dk.stride(0); bp.dk_ss = dk.stride(1); bp.dk_hs = dk.stride(2);
   bp.dv = dv.data_ptr(); bp.dv_bs = dv.stride(0); bp.dv_ss = dv.stride(1); bp.dv_hs = dv.stride(2);
+  if (cu_seqlens.has_value()) bp.do_bs = bp.dq_bs = bp.dk_bs = bp.dv_bs = 0;  // packed: one token axis
   bp.delta = ws.data_ptr<float>();
   TORCH_CHECK(rope_cos.has_value() == rope_sin.has_value(), "attn_bwd: rope_cos and rope_sin together");
   if (rope_cos.has_value()) {  // dQ / dK written un-rotated (q / k were rotated at position = index)
@@ -900,11 +921,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adamw_t", &adamw_t);
   m.def("scale_", &scale_);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("scale"),
-        py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0);
+        py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0,
+        py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0);
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"), py::arg("causal"),
         py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("rope_cos") = py::none(),
-        py::arg("rope_sin") = py::none());
+        py::arg("rope_sin") = py::none(), py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);

@@ -125,6 +125,10 @@ struct AttnParams {
   float scale;
   int causal;
   const int32_t* seqlens_k;   // optional per-batch valid key length (right padding), may be null
+  // optional padding-free packing (bf16 kernels): sequence b is token rows [cu[b], cu[b+1]) of the
+  // packed q / k / v / o (batch strides 0); B = number of sequences, Sq = Sk = the longest
+  // sequence; causal self-attention inside each sequence; positions restart at 0 per sequence
+  const int32_t* cu_seqlens;
   // attention-probability dropout (0 = off): element (b*Hq + hq, q, k) is kept iff
   // attn_dropout_hash(seed, bh, q, k) >= drop_thresh (= p * 2^32); kept values scaled by drop_scale
   uint32_t drop_seed;

@@ -140,26 +140,33 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, l16 = lane & 15;
-  const int nqb = (p.Sq + F3M - 1) / F3M;
+  const int nqb = (p.Sq + F3M - 1) / F3M;  // grid: the longest sequence
   const int BH = p.B * p.Hq;
   const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) blocks first
   const int bh = blockIdx.x % BH;
   const int b = bh / p.Hq, hq = bh % p.Hq;
   const int hkv = hq / (p.Hq / p.Hkv);
   GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && qblk >= 0);
-  const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
-  const int off = p.Sk - p.Sq;  // bottom-right aligned causal mask
+  int Sq = p.Sq, Sk = p.Sk;
+  int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
+  if (p.cu_seqlens) {
+    tok0 = p.cu_seqlens[b];
+    Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
+    if (qblk * F3M >= Sq) return;  // workgroup-uniform: the sequence is shorter than the longest
+  }
+  const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
+  const int off = Sk - Sq;  // bottom-right aligned causal mask
   const int q0 = qblk * F3M, qw0 = q0 + w * 32;
   const int myq = qw0 + l32;
 
-  const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + (int64_t)hq * p.q_hs;
-  const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs;
-  const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs;
+  const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + tok0 * p.q_ss + (int64_t)hq * p.q_hs;
+  const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + tok0 * p.k_ss + (int64_t)hkv * p.k_hs;
+  const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + tok0 * p.v_ss + (int64_t)hkv * p.v_hs;
 
   bf16x8 qf[D / 16];
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) {
-    if (myq < p.Sq) qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)myq * p.q_ss + ks * 16 + 8 * h);
+    if (myq < Sq) qf[ks] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)myq * p.q_ss + ks * 16 + 8 * h);
     else qf[ks] = bf16x8{};
   }
   const int klim = p.causal ? min(sk - 1, myq + off) : sk - 1;   // keys <= klim are kept
@@ -174,7 +181,7 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   const int row0 = 8 * w + g, row1 = row0 + 4;
   const int ch0 = l16 ^ img_swz(row0), ch1 = l16 ^ img_swz(row1);
   auto dma_tile = [&](int t, uint32_t slot_off) {
-    const int64_t k0r = min(t * F3N + row0, p.Sk - 1), k1r = min(t * F3N + row1, p.Sk - 1);  // past Sk: masked
+    const int64_t k0r = min(t * F3N + row0, Sk - 1), k1r = min(t * F3N + row1, Sk - 1);  // past Sk: masked
     const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(8 * w * 256));
     lds_dma16(K + k0r * p.k_ss + ch0 * 8, dst);
     lds_dma16(Vg + k0r * p.v_ss + ch0 * 8, dst + F3IMG);
@@ -292,8 +299,8 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
 
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (myq < p.Sq) {
-    bf16* O = (bf16*)p.o + (int64_t)b * p.o_bs + (int64_t)hq * p.o_hs + (int64_t)myq * p.o_ss;
+  if (myq < Sq) {
+    bf16* O = (bf16*)p.o + (int64_t)b * p.o_bs + (tok0 + myq) * p.o_ss + (int64_t)hq * p.o_hs;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
@@ -326,10 +333,16 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p
   const int q = (int)(row % Sqp);
   const int64_t bh = row / Sqp;
   float acc = 0.f;
-  if (q < p.f.Sq) {
-    const int hq = (int)(bh % p.f.Hq), b = (int)(bh / p.f.Hq);
-    const bf16* O = (const bf16*)p.f.o + (int64_t)b * p.f.o_bs + (int64_t)hq * p.f.o_hs + (int64_t)q * p.f.o_ss;
-    const bf16* dO = (const bf16*)p.dout + (int64_t)b * p.do_bs + (int64_t)hq * p.do_hs + (int64_t)q * p.do_ss;
+  const int hq = (int)(bh % p.f.Hq), b = (int)(bh / p.f.Hq);
+  int Sq = p.f.Sq;
+  int64_t tok0 = 0;
+  if (p.f.cu_seqlens) {
+    tok0 = p.f.cu_seqlens[b];
+    Sq = p.f.cu_seqlens[b + 1] - (int)tok0;
+  }
+  if (q < Sq) {
+    const bf16* O = (const bf16*)p.f.o + (int64_t)b * p.f.o_bs + (int64_t)hq * p.f.o_hs + (tok0 + q) * p.f.o_ss;
+    const bf16* dO = (const bf16*)p.dout + (int64_t)b * p.do_bs + (int64_t)hq * p.do_hs + (tok0 + q) * p.do_ss;
     float a[8], g[8];
     load16(O + l16 * 8, a);
     load16(dO + l16 * 8, g);
@@ -341,7 +354,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p
   if (l16 == 0) {
     float* lse2 = p.delta + nrows;
     p.delta[row] = acc;
-    lse2[row] = q < p.f.Sq ? p.f.lse[bh * p.f.Sq + q] * kLog2e : INFINITY;
+    lse2[row] = q < Sq ? p.f.lse[bh * p.f.Sq + q] * kLog2e : INFINITY;
   }
 }
 
@@ -393,16 +406,23 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   const int bhk = blockIdx.x % BHk;
   const int b = bhk / p.Hkv, hkv = bhk % p.Hkv;
   const int grp = p.Hq / p.Hkv;
-  GRT_DEVICE_CHECK(grp * p.Hkv == p.Hq && kblk * K2N < p.Sk);
-  const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
-  const int off = p.Sk - p.Sq;
+  int Sq = p.Sq, Sk = p.Sk;
+  int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
+  if (p.cu_seqlens) {
+    tok0 = p.cu_seqlens[b];
+    Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
+    if (kblk * K2N >= Sk) return;  // workgroup-uniform: the sequence is shorter than the longest
+  }
+  GRT_DEVICE_CHECK(grp * p.Hkv == p.Hq && kblk * K2N < Sk);
+  const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
+  const int off = Sk - Sq;
   const int k0 = kblk * K2N, kw0 = k0 + w * 32, mykey = kw0 + l32;
   const float c = p.scale * kLog2e;
-  const int Sqp = sq_pad(p.Sq);
+  const int Sqp = sq_pad(p.Sq);  // workspace row stride: the longest sequence
   const float* lse2 = P.delta + (int64_t)p.B * p.Hq * Sqp;
 
-  const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs;
-  const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs;
+  const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + tok0 * p.k_ss + (int64_t)hkv * p.k_hs;
+  const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + tok0 * p.v_ss + (int64_t)hkv * p.v_hs;
   bf16x8 kf[D / 16], vf[D / 16];
 #pragma unroll
   for (int ks = 0; ks < D / 16; ++ks) {
@@ -420,7 +440,7 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
 
   int qstart = p.causal ? max(0, k0 - off) : 0;
   qstart = (qstart / K2M) * K2M;
-  const int nqt = qstart < p.Sq ? (p.Sq - qstart + K2M - 1) / K2M : 0;
+  const int nqt = qstart < Sq ? (Sq - qstart + K2M - 1) / K2M : 0;
   const int total = (k0 < sk) ? nqt * grp : 0;
   // per-lane mask: probability of (q, mykey) kept iff mykey < sk and (non-causal or q >= qlim)
   const int qlim = mykey < sk ? (p.causal ? mykey - off : INT_MIN) : INT_MAX;
@@ -436,9 +456,9 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   const int sl = l16 & 7;
   const int64_t st_lane = (l16 < 8 ? (int64_t)p.B * p.Hq * Sqp : 0) + 4 * sl;  // lse2 | delta
   auto dma_tile = [&](int hq, int qt, uint32_t slot_off) {
-    const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + (int64_t)hq * p.q_hs;
-    const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + (int64_t)hq * P.do_hs;
-    const int64_t q0r = min(qt + row0, p.Sq - 1), q1r = min(qt + row1, p.Sq - 1);  // past Sq: lse2 = +inf
+    const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + tok0 * p.q_ss + (int64_t)hq * p.q_hs;
+    const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + tok0 * P.do_ss + (int64_t)hq * P.do_hs;
+    const int64_t q0r = min(qt + row0, Sq - 1), q1r = min(qt + row1, Sq - 1);  // past Sq: lse2 = +inf
     const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(8 * w * 256));
     lds_dma16(Q + q0r * p.q_ss + ch0 * 8, dst);
     lds_dma16(dO + q0r * P.do_ss + ch0 * 8, dst + K2IMG);
@@ -474,7 +494,7 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   int cur_h = 0, cur_q = qstart;
   auto advance = [&](int& hh, int& qq) {
     qq += K2M;
-    if (qq >= p.Sq) { qq = qstart; ++hh; }
+    if (qq >= Sq) { qq = qstart; ++hh; }
   };
   int nxt_h = cur_h, nxt_q = cur_q;
   advance(nxt_h, nxt_q);
@@ -563,9 +583,9 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
-  if (mykey < p.Sk) {
-    bf16* dK = (bf16*)P.dk + (int64_t)b * P.dk_bs + (int64_t)hkv * P.dk_hs + (int64_t)mykey * P.dk_ss;
-    bf16* dV = (bf16*)P.dv + (int64_t)b * P.dv_bs + (int64_t)hkv * P.dv_hs + (int64_t)mykey * P.dv_ss;
+  if (mykey < Sk) {
+    bf16* dK = (bf16*)P.dk + (int64_t)b * P.dk_bs + (int64_t)hkv * P.dk_hs + (tok0 + mykey) * P.dk_ss;
+    bf16* dV = (bf16*)P.dv + (int64_t)b * P.dv_bs + (int64_t)hkv * P.dv_hs + (tok0 + mykey) * P.dv_ss;
     if (P.rope_cos)
       store_unrotated(dk, p.scale, P.rope_cos + (int64_t)mykey * (D / 2), P.rope_sin + (int64_t)mykey * (D / 2), dK, h);
 #pragma unroll
@@ -599,23 +619,30 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
   const int g = lane >> 4, l16 = lane & 15;
-  const int nqb = (p.Sq + Q2M - 1) / Q2M;
+  const int nqb = (p.Sq + Q2M - 1) / Q2M;  // grid: the longest sequence
   const int BH = p.B * p.Hq;
   const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) blocks first
   const int bh = blockIdx.x % BH;
   const int b = bh / p.Hq, hq = bh % p.Hq;
   const int hkv = hq / (p.Hq / p.Hkv);
-  const int sk = p.seqlens_k ? min(p.Sk, p.seqlens_k[b]) : p.Sk;
-  const int off = p.Sk - p.Sq;
+  int Sq = p.Sq, Sk = p.Sk;
+  int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
+  if (p.cu_seqlens) {
+    tok0 = p.cu_seqlens[b];
+    Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
+    if (qblk * Q2M >= Sq) return;  // workgroup-uniform: the sequence is shorter than the longest
+  }
+  const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
+  const int off = Sk - Sq;
   const int q0 = qblk * Q2M, qw0 = q0 + w * 32;
   const int myq = qw0 + l32;
-  const bool qok = myq < p.Sq;
-  const int Sqp = sq_pad(p.Sq);
+  const bool qok = myq < Sq;
+  const int Sqp = sq_pad(p.Sq);  // workspace row stride: the longest sequence
 
-  const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + (int64_t)hq * p.q_hs;
-  const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + (int64_t)hq * P.do_hs;
-  const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs;
-  const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs;
+  const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + tok0 * p.q_ss + (int64_t)hq * p.q_hs;
+  const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + tok0 * P.do_ss + (int64_t)hq * P.do_hs;
+  const bf16* K = (const bf16*)p.k + (int64_t)b * p.k_bs + tok0 * p.k_ss + (int64_t)hkv * p.k_hs;
+  const bf16* Vg = (const bf16*)p.v + (int64_t)b * p.v_bs + tok0 * p.v_ss + (int64_t)hkv * p.v_hs;
 
   bf16x8 qf[D / 16], of[D / 16];
 #pragma unroll
@@ -647,7 +674,7 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
   const int row0 = 8 * w + g, row1 = row0 + 4;
   const int ch0 = l16 ^ img_swz(row0), ch1 = l16 ^ img_swz(row1);
   auto dma_tile = [&](int t, uint32_t slot_off) {
-    const int64_t k0r = min(t * Q2N + row0, p.Sk - 1), k1r = min(t * Q2N + row1, p.Sk - 1);  // past Sk: masked
+    const int64_t k0r = min(t * Q2N + row0, Sk - 1), k1r = min(t * Q2N + row1, Sk - 1);  // past Sk: masked
     const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(8 * w * 256));
     lds_dma16(K + k0r * p.k_ss + ch0 * 8, dst);
     lds_dma16(Vg + k0r * p.v_ss + ch0 * 8, dst + Q2IMG);
@@ -732,7 +759,7 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   if (qok) {
-    bf16* dQ = (bf16*)P.dq + (int64_t)b * P.dq_bs + (int64_t)hq * P.dq_hs + (int64_t)myq * P.dq_ss;
+    bf16* dQ = (bf16*)P.dq + (int64_t)b * P.dq_bs + (int64_t)hq * P.dq_hs + (tok0 + myq) * P.dq_ss;
     if (P.rope_cos) {
       store_unrotated(dq, p.scale, P.rope_cos + (int64_t)myq * (D / 2), P.rope_sin + (int64_t)myq * (D / 2), dQ, h);
     } else {

@@ -139,14 +139,16 @@ class LlamaAttention(nn.Module):
                                                       ("v_proj", self.hkv * hd)], device=device, dtype=dtype)
         self.o_proj = Linear(self.hq * hd, cfg.hidden_size, bias=False, device=device, dtype=dtype)
 
-    def forward(self, x, B, S, cos, sin):
+    def forward(self, x, B, S, cos, sin, varlen=None):
         qkv = self.qkv_proj(x)
         sp = getattr(self, "sp_group", None)
         if sp is not None:  # sequence parallel: S is this rank's token count (parallel/sequence.py)
+            if varlen is not None:
+                raise NotImplementedError("padding-free packing with sequence parallelism")
             from ..parallel.sequence import ulysses_attention
             o = ulysses_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, sp, causal=True)
         else:
-            o = ops.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, causal=True)
+            o = ops.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, causal=True, varlen=varlen)
         return self.o_proj(o)
 
 
@@ -185,14 +187,14 @@ class LlamaDecoderLayer(nn.Module):
         self.post_attention_layernorm = RMSNorm(cfg.hidden_size, cfg.rms_norm_eps, device, dtype)
         self.mlp = LlamaMLP(cfg, device, dtype)
 
-    def forward(self, h, residual, B, S, cos, sin):
+    def forward(self, h, residual, B, S, cos, sin, varlen=None):
         eps = self.input_layernorm.eps
         if residual is None:
             residual = h
             x = ops.rms_norm(h, self.input_layernorm.weight, eps)
         else:
             x, residual = ops.add_rms_norm(h, residual, self.input_layernorm.weight, eps)
-        h = self.self_attn(x, B, S, cos, sin)
+        h = self.self_attn(x, B, S, cos, sin, varlen)
         x, residual = ops.add_rms_norm(h, residual, self.post_attention_layernorm.weight, eps)
         return self.mlp(x), residual
 
@@ -251,31 +253,39 @@ class LlamaForCausalLM(nn.Module):
         return t
 
     # -------------------------------------------------------------- forward
-    def hidden_states(self, input_ids):
+    def hidden_states(self, input_ids, varlen=None):
         B, S = input_ids.shape
-        # sequence parallel: RoPE tables span the full sequence (this rank holds S of S * sp_size)
-        cos, sin = self.rope(S * getattr(self, "sp_size", 1), input_ids.device)
+        # sequence parallel: RoPE tables span the full sequence (this rank holds S of S * sp_size);
+        # padding-free packing: positions restart per sequence, so the longest one bounds the table
+        n = varlen.max_len if varlen is not None else S * getattr(self, "sp_size", 1)
+        cos, sin = self.rope(n, input_ids.device)
         h = self.model.embed_tokens(input_ids).view(B * S, -1)
         residual = None
         for layer in self.model.layers:
             if self.gradient_checkpointing and self.training and torch.is_grad_enabled():
                 if residual is None:
-                    h, residual = ckpt.checkpoint(lambda a, L=layer: L(a, None, B, S, cos, sin), h, use_reentrant=False)
+                    h, residual = ckpt.checkpoint(lambda a, L=layer: L(a, None, B, S, cos, sin, varlen), h,
+                                                  use_reentrant=False)
                 else:
-                    h, residual = ckpt.checkpoint(layer, h, residual, B, S, cos, sin, use_reentrant=False)
+                    h, residual = ckpt.checkpoint(layer, h, residual, B, S, cos, sin, varlen, use_reentrant=False)
             else:
-                h, residual = layer(h, residual, B, S, cos, sin)
+                h, residual = layer(h, residual, B, S, cos, sin, varlen)
         x, _ = self.model.norm(h, residual)
         return x
 
     def forward(self, input_ids, labels=None, attention_mask=None, return_logits=None, shifted_labels=None,
-                loss_weights=None):
+                loss_weights=None, varlen=None):
         """``labels``: HF convention (shifted here). ``shifted_labels``: already next-token aligned
         (sequence-parallel shards, whose last token's label lives on the next rank).
         ``loss_weights`` ([B, S] fp32, optional): the loss is the weighted SUM of the per-position
-        next-token CE (position t predicts t+1) instead of the mean over valid positions."""
+        next-token CE (position t predicts t+1) instead of the mean over valid positions.
+        ``varlen`` (``ops.Varlen``): ``input_ids`` [1, T] holds padding-free packed sequences —
+        no padding tokens in any GEMM; attention stays inside each sequence, positions restart,
+        and the last token of a sequence predicts nothing (its shifted label is -100)."""
         B, S = input_ids.shape
-        x = self.hidden_states(input_ids)
+        if varlen is not None and (B != 1 or varlen.total != S):
+            raise ValueError(f"varlen packing expects input_ids [1, {varlen.total}], got {tuple(input_ids.shape)}")
+        x = self.hidden_states(input_ids, varlen)
         out = {}
         rw = None if loss_weights is None else loss_weights.reshape(-1)
         if shifted_labels is not None:
@@ -286,6 +296,8 @@ class LlamaForCausalLM(nn.Module):
             shifted[:, :-1] = labels[:, 1:]
             if attention_mask is not None:
                 shifted[:, :-1].masked_fill_(attention_mask[:, 1:] == 0, -100)
+            if varlen is not None:  # a sequence's last token does not predict the next sequence's first
+                shifted[0, varlen.cu[1:].long() - 1] = -100
             out["loss"] = self.lm_head(x, labels=shifted.view(-1), row_weights=rw)
         if (labels is None and shifted_labels is None) or return_logits:
             out["logits"] = self.lm_head(x).view(B, S, -1)

@@ -254,31 +254,68 @@ def _warn_once(msg):
 _ROPE_BWD_FUSED = os.environ.get("GRT_ROPE_BWD_FUSED", "1") != "0"
 
 
+class Varlen:
+    """Padding-free packing of variable-length sequences into one token axis (FlashAttention
+    "varlen"): sequence i is token rows [cu[i], cu[i+1]); attention is causal inside each
+    sequence and RoPE positions restart at 0 per sequence. ``cu`` (int32, device) and ``pos``
+    (int32 [T], device) feed the kernels; ``cu_host`` / ``max_len`` are host ints (no sync)."""
+
+    __slots__ = ("cu", "pos", "cu_host", "max_len")
+
+    def __init__(self, lengths, device):
+        lens = [int(n) for n in lengths]
+        if not lens or min(lens) < 1:
+            raise ValueError("Varlen: every packed sequence needs at least one token")
+        cu = [0]
+        for n in lens:
+            cu.append(cu[-1] + n)
+        self.cu_host = cu
+        self.max_len = max(lens)
+        self.cu = torch.tensor(cu, dtype=torch.int32).pin_memory().to(device, non_blocking=True) \
+            if torch.device(device).type == "cuda" else torch.tensor(cu, dtype=torch.int32)
+        pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens])
+        self.pos = pos.pin_memory().to(device, non_blocking=True) if torch.device(device).type == "cuda" else pos
+
+    @property
+    def total(self) -> int:
+        return self.cu_host[-1]
+
+    @property
+    def lengths(self):
+        return [b - a for a, b in zip(self.cu_host[:-1], self.cu_host[1:])]
+
+
 class _RopeAttention(torch.autograd.Function):
     """qkv [B*S, (Hq + 2 Hkv) * D] -> o [B*S, Hq * D]: RoPE + causal flash attention fused.
 
     Backward writes dV straight into the V columns of dqkv (strided) and the un-rotated dQ/dK into
     its Q/K columns, so the fused-QKV gradient is produced with no split/cat copies.
+    With ``varlen`` the B*S rows are the packed tokens of varlen.cu's sequences (B = 1, S = T).
     """
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, S, hq, hkv, D, causal, scale):
+    def forward(ctx, qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen=None):
         C = _native.kernels()
         qkv = qkv.contiguous()
-        q, k = C.rope_fwd(qkv, cos, sin, None, hq, hkv, D, S)
+        cu, ml = (varlen.cu, varlen.max_len) if varlen is not None else (None, 0)
+        q, k = C.rope_fwd(qkv, cos, sin, varlen.pos if varlen is not None else None, hq, hkv, D,
+                          ml if varlen is not None else S)
         q4 = q.view(B, S, hq, D)
         k4 = k.view(B, S, hkv, D)
         v4 = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
         o = torch.empty(B, S, hq, D, device=qkv.device, dtype=qkv.dtype)
-        _, lse = C.attn_fwd(q4, k4, v4, o, scale, causal, None)
+        _, lse = C.attn_fwd(q4, k4, v4, o, scale, causal, None, cu_seqlens=cu, max_seqlen=ml)
         ctx.save_for_backward(qkv, q, k, o, lse, cos, sin)
         ctx.dims = (B, S, hq, hkv, D, causal, scale)
+        ctx.varlen = varlen
         return o.view(B * S, hq * D)
 
     @staticmethod
     def backward(ctx, do):
         qkv, q, k, o, lse, cos, sin = ctx.saved_tensors
         B, S, hq, hkv, D, causal, scale = ctx.dims
+        vl = ctx.varlen
+        cu, ml = (vl.cu, vl.max_len) if vl is not None else (None, 0)
         C = _native.kernels()
         dqkv = torch.empty_like(qkv)
         q4 = q.view(B, S, hq, D)
@@ -286,25 +323,35 @@ class _RopeAttention(torch.autograd.Function):
         v4 = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
         d4 = dqkv.view(B, S, hq + 2 * hkv, D)
         dv4 = d4[:, :, hq + hkv:, :]
-        if _ROPE_BWD_FUSED and cos.dim() == 2 and cos.shape[0] >= S:
+        if _ROPE_BWD_FUSED and cos.dim() == 2 and cos.shape[0] >= (ml if vl is not None else S):
             # the kernels' epilogues undo the RoPE and write dQ / dK straight into dqkv's columns
+            # (packed: the key / query index inside its sequence IS its RoPE position)
             C.attn_bwd(do.contiguous().view(B, S, hq, D), q4, k4, v4, o, lse, d4[:, :, :hq], d4[:, :, hq:hq + hkv],
-                       dv4, scale, causal, None, rope_cos=cos, rope_sin=sin)
+                       dv4, scale, causal, None, rope_cos=cos, rope_sin=sin, cu_seqlens=cu, max_seqlen=ml)
         else:
             dq, dk, _ = C.attn_bwd(do.contiguous().view(B, S, hq, D), q4, k4, v4, o, lse, None, None, dv4,
-                                   scale, causal, None)
-            C.rope_bwd(dq, dk, dqkv, cos, sin, None, hq, hkv, D, S)
-        return dqkv, None, None, None, None, None, None, None, None, None
+                                   scale, causal, None, cu_seqlens=cu, max_seqlen=ml)
+            C.rope_bwd(dq, dk, dqkv, cos, sin, vl.pos if vl is not None else None, hq, hkv, D,
+                       ml if vl is not None else S)
+        return dqkv, None, None, None, None, None, None, None, None, None, None
 
 
-def rope_attention(qkv, cos, sin, B, S, hq, hkv, D, causal=True, scale=None):
+def rope_attention(qkv, cos, sin, B, S, hq, hkv, D, causal=True, scale=None, varlen: "Varlen" = None):
+    """``varlen``: the B*S rows are padding-free packed sequences (B = 1; see ``Varlen``)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if _gpu(qkv) and qkv.dtype == torch.bfloat16 and D == 128:
-        return _RopeAttention.apply(qkv, cos, sin, B, S, hq, hkv, D, causal, scale)
+        return _RopeAttention.apply(qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen)
     x = qkv.view(B * S, hq + 2 * hkv, D)
-    q = _ref.apply_rope(x[:, :hq], cos, sin)
-    k = _ref.apply_rope(x[:, hq:hq + hkv], cos, sin)
+    pos = varlen.pos if varlen is not None else None
+    q = _ref.apply_rope(x[:, :hq], cos, sin, pos)
+    k = _ref.apply_rope(x[:, hq:hq + hkv], cos, sin, pos)
     v = x[:, hq + hkv:]
+    if varlen is not None:  # reference path: attention sequence by sequence
+        outs = []
+        for a, b in zip(varlen.cu_host[:-1], varlen.cu_host[1:]):
+            outs.append(flash_attention(q[a:b].unsqueeze(0), k[a:b].unsqueeze(0), v[a:b].unsqueeze(0), causal,
+                                        scale).squeeze(0))
+        return torch.cat(outs).reshape(B * S, hq * D)
     o = flash_attention(q.view(B, S, hq, D), k.view(B, S, hkv, D), v.reshape(B, S, hkv, D), causal, scale)
     return o.reshape(B * S, hq * D)
 

@@ -93,6 +93,12 @@ class SFTConfig:
     # and token counts that avoid hipBLASLt's slow tilings of odd M (measured on the reference SFT
     # job: 128 -> +7 % tokens/s over 8 despite the extra padding, profiles/r1_sft_job_kernel_breakdown.md)
     fuse_pad_multiple: int = 128
+    # padding-free packing of each fused step (``ops.Varlen``): the step's sequences are concatenated
+    # on one token axis (attention inside each sequence, RoPE positions restarting), so no GEMM,
+    # norm or loss row is spent on padding; only the total is rounded up to fuse_pad_multiple with
+    # one masked filler segment. None = on wherever fused accumulation is on and the model's
+    # forward takes ``varlen``. Same loss and gradient as the padded batch.
+    padding_free: Optional[bool] = None
 
     def __post_init__(self):
         if self.evaluation_strategy is not None:  # deprecated alias used by the reference (:317)
@@ -309,7 +315,51 @@ class SFTTrainer:
         except (TypeError, ValueError):
             return False
 
-    def _step_chunks(self, batches, mis, fuse):
+    def _padding_free_enabled(self) -> bool:
+        a = self.args
+        if a.padding_free is not None:
+            return bool(a.padding_free)
+        if os.environ.get("GRT_SFT_PADDING_FREE", "1") == "0":
+            return False
+        import inspect
+        inner = getattr(self.model, "base_model", self.model)
+        try:
+            return "varlen" in inspect.signature(inner.forward).parameters
+        except (TypeError, ValueError):
+            return False
+
+    def _pack(self, g, mult: int, weighted: bool):
+        """Micro-batches ``g`` -> one padding-free packed row (see ``SFTConfig.padding_free``)."""
+        accum = self.args.gradient_accumulation_steps
+        ids, labs, wts, lens = [], [], [], []
+        ntarget = 0
+        for b in g:
+            lengths = b["attention_mask"].sum(1).tolist()
+            n = int(((b["labels"][:, 1:] != -100) & (b["attention_mask"][:, 1:] != 0)).sum())
+            w = 1.0 / (n * accum) if n else 0.0
+            for r, L in enumerate(lengths):
+                L = int(L)
+                if L == 0:
+                    continue
+                ids.append(b["input_ids"][r, :L])
+                labs.append(b["labels"][r, :L])
+                wts.append(torch.full((L,), w))
+                lens.append(L)
+                ntarget += int((b["labels"][r, 1:L] != -100).sum())
+        T = sum(lens)
+        pad = (-T) % max(1, mult)
+        mask = torch.ones(T + pad, dtype=torch.long)
+        if pad:  # one masked filler segment: keeps the token count on the tuned GEMM sizes
+            ids.append(torch.full((pad,), self.pad_id, dtype=ids[0].dtype))
+            labs.append(torch.full((pad,), -100, dtype=labs[0].dtype))
+            wts.append(torch.zeros(pad))
+            lens.append(pad)
+            mask[T:] = 0
+        out = {"input_ids": torch.cat(ids).view(1, -1), "labels": torch.cat(labs).view(1, -1),
+               "attention_mask": mask.view(1, -1), "lengths": lens, "ntarget": ntarget}
+        return out, (torch.cat(wts).view(1, -1) if weighted else None)
+
+    def _step_chunks(self, batches, mis, fuse, weighted: bool = True):
         """The micro-batches ``mis`` of one optimizer step -> [(batch, loss_weights | None)].
         Unfused: one entry per micro-batch (loss = mean / accum). Fused: micro-batches are right-
         padded to a common length and concatenated while the padded size stays within
@@ -338,6 +388,8 @@ class SFTTrainer:
         if cur:
             groups.append(cur)
         out = []
+        if self._padding_free_enabled():
+            return [self._pack(g, mult, weighted) for g in groups]
         for g in groups:
             L = padded(max(b["input_ids"].shape[1] for b in g))
             pads = {"input_ids": self.pad_id, "labels": -100, "attention_mask": 0}
@@ -351,8 +403,12 @@ class SFTTrainer:
         return out
 
     def _to_dev(self, b):
-        return {k: v.pin_memory().to(self.device, non_blocking=True) if self.device.type == "cuda" else v.to(self.device)
-                for k, v in b.items()}
+        out = {k: (v.pin_memory().to(self.device, non_blocking=True) if self.device.type == "cuda" else v.to(self.device))
+               for k, v in b.items() if isinstance(v, torch.Tensor)}
+        if "lengths" in b:
+            from ..ops import Varlen
+            out["varlen"] = Varlen(b["lengths"], self.device)
+        return out
 
     # ------------------------------------------------------------------ train
     def train(self, resume_from_checkpoint: Optional[str] = None) -> TrainOutput:
@@ -399,17 +455,20 @@ class SFTTrainer:
                     b = self._to_dev(cb if lw is None else dict(cb, loss_weights=lw))
                     with self.engine.no_sync(ci != len(chunks) - 1):
                         with roctx.range("forward"):
+                            vk = {"varlen": b["varlen"]} if "varlen" in b else {}
                             if lw is None:
-                                out = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])
+                                out = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"],
+                                                 **vk)
                                 loss = out["loss"] / accum
                             else:
                                 loss = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"],
-                                                  loss_weights=b["loss_weights"])["loss"]
+                                                  loss_weights=b["loss_weights"], **vk)["loss"]
                         with roctx.range("backward"):
                             loss.backward()
                     tr_loss_sum += loss.detach()
                     log_loss += loss.detach()
-                    nsamples += b["input_ids"].shape[0]
+                    nsamples += (len(cb["lengths"]) - int(int(cb["attention_mask"][0, -1]) == 0)
+                                 if "lengths" in cb else b["input_ids"].shape[0])
                 with roctx.range("grad_sync"):
                     self.engine.finish_gradient_sync()
                 with roctx.range("optimizer"):
@@ -498,12 +557,14 @@ class SFTTrainer:
         tot = torch.zeros(2, device=self.device, dtype=torch.float64)
         batches = self._batches(self.eval_seqs, self.args.per_device_eval_batch_size, 0, shuffle=False)
         if self._fuse_enabled():  # same token-weighted mean from fewer, larger forwards
-            batches = [cb for cb, _ in self._step_chunks(batches, list(range(len(batches))), True)]
+            batches = [cb for cb, _ in self._step_chunks(batches, list(range(len(batches))), True, weighted=False)]
         with torch.no_grad():  # as HF's prediction_step: no saved activations, no fused CE gradient
-            for b in batches:
-                b = self._to_dev(b)
-                loss = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"])["loss"]
-                n = (b["labels"][:, 1:] != -100).sum()
+            for cb in batches:
+                b = self._to_dev(cb)
+                vk = {"varlen": b["varlen"]} if "varlen" in b else {}
+                loss = self.model(b["input_ids"], labels=b["labels"], attention_mask=b["attention_mask"], **vk)["loss"]
+                n = cb["ntarget"] if "ntarget" in cb else (
+                    (b["labels"][:, 1:] != -100) & (b["attention_mask"][:, 1:] != 0)).sum()
                 tot[0] += loss.double() * n
                 tot[1] += n
         if self.world > 1:

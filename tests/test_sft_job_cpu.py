@@ -77,7 +77,7 @@ def test_full_ft_job_and_resume(tmp_path):
     assert out.global_step == 4
 
 
-def _fused_vs_unfused(tmp_path, fuse):
+def _fused_vs_unfused(tmp_path, fuse, padding_free=None):
     import torch
     from gke_ray_train_amd.models import build_llama
     from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
@@ -85,20 +85,23 @@ def _fused_vs_unfused(tmp_path, fuse):
     m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
     # varied lengths so micro-batches pad differently and carry different valid-token counts
     rows = [{"text": "select * from t where x = %d " % i * (1 + i % 4)} for i in range(16)]
-    tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path / str(fuse)), per_device_train_batch_size=2,
+    tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path / f"{fuse}_{padding_free}"), per_device_train_batch_size=2,
                                  gradient_accumulation_steps=4, max_steps=2, logging_steps=1, save_strategy="no",
-                                 learning_rate=1e-3, max_grad_norm=1e9, fuse_accumulation=fuse, fuse_max_tokens=10 ** 6),
+                                 learning_rate=1e-3, max_grad_norm=1e9, fuse_accumulation=fuse, fuse_max_tokens=10 ** 6,
+                                 padding_free=padding_free),
                     train_dataset=rows)
     out = tr.train()
     return out, {k: v.detach().clone() for k, v in m.state_dict().items()}
 
 
-def test_fused_grad_accumulation_matches_unfused(tmp_path):
-    """One padded batch per optimizer step with per-micro-batch loss weights == HF-style
-    accumulation of per-micro-batch means (same loss, same updated parameters)."""
+@pytest.mark.parametrize("padding_free", [False, True])
+def test_fused_grad_accumulation_matches_unfused(tmp_path, padding_free):
+    """One batch per optimizer step with per-micro-batch loss weights == HF-style accumulation of
+    per-micro-batch means (same loss, same updated parameters) — padded, or padding-free packed
+    (sequences on one token axis, ops.Varlen)."""
     import torch
     a, pa = _fused_vs_unfused(tmp_path, False)
-    b, pb = _fused_vs_unfused(tmp_path, True)
+    b, pb = _fused_vs_unfused(tmp_path, True, padding_free)
     assert abs(a.training_loss - b.training_loss) < 1e-4 * max(1.0, abs(a.training_loss))
     # AdamW's first steps are ~lr * sign(g): elements whose gradient is ~0 may flip under fp32
     # summation-order changes, so allow a handful of such elements (bounded by 2 steps x lr)
@@ -115,7 +118,7 @@ def test_step_chunks_respect_token_cap(tmp_path):
     m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
     rows = [{"text": "abc " * (3 + i)} for i in range(8)]
     tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path), per_device_train_batch_size=2, gradient_accumulation_steps=4,
-                                 fuse_accumulation=True, fuse_max_tokens=2 * 48), train_dataset=rows)
+                                 fuse_accumulation=True, fuse_max_tokens=2 * 48, padding_free=False), train_dataset=rows)
     batches = tr._batches(tr.train_seqs, 2, 0, shuffle=False)
     chunks = tr._step_chunks(batches, list(range(4)), True)
     assert 1 < len(chunks) <= 4
@@ -143,3 +146,25 @@ def test_lm_head_row_weights_cpu():
     torch.testing.assert_close(loss, ref)
     loss.backward()
     assert h.grad is not None and torch.isfinite(h.grad).all()
+
+
+def test_padding_free_pack_layout(tmp_path):
+    """Packed step: real tokens only (plus one masked filler segment up to the pad multiple), per-token
+    weights summing to 1 over the valid next-token targets, sequence lengths for ops.Varlen."""
+    import torch
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
+    rows = [{"text": "abc " * (3 + i)} for i in range(8)]
+    tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path), per_device_train_batch_size=2, gradient_accumulation_steps=4,
+                                 fuse_accumulation=True, fuse_pad_multiple=64, padding_free=True), train_dataset=rows)
+    batches = tr._batches(tr.train_seqs, 2, 0, shuffle=False)
+    (cb, w), = tr._step_chunks(batches, list(range(4)), True)
+    real = sum(len(s) for s in tr.train_seqs)
+    assert cb["input_ids"].shape == (1, sum(cb["lengths"])) and cb["input_ids"].shape[1] % 64 == 0
+    assert int(cb["attention_mask"].sum()) == real and sum(cb["lengths"][:8]) == real
+    bounds = torch.tensor(cb["lengths"]).cumsum(0)
+    valid = torch.zeros(cb["input_ids"].shape[1], dtype=torch.bool)
+    for a, b in zip([0] + bounds.tolist()[:-1], bounds.tolist()):
+        valid[a:b - 1] = cb["labels"][0, a + 1:b] != -100  # targets inside each sequence only
+    assert abs(float((w[0] * valid).sum()) - 1.0) < 1e-6
