@@ -96,8 +96,10 @@ class SFTConfig:
     # padding-free packing of each fused step (``ops.Varlen``): the step's sequences are concatenated
     # on one token axis (attention inside each sequence, RoPE positions restarting), so no GEMM,
     # norm or loss row is spent on padding; only the total is rounded up to fuse_pad_multiple with
-    # one masked filler segment. None = on wherever fused accumulation is on and the model's
-    # forward takes ``varlen``. Same loss and gradient as the padded batch.
+    # one masked filler segment. Same loss and gradient as the padded batch. None = on when
+    # GRT_SFT_PADDING_FREE=1 (and fused accumulation is on and the model's forward takes ``varlen``):
+    # off by default because the packed token counts leave the offline-tuned GEMM sizes — on the
+    # reference SFT job 27.1 vs 28.8 samples/s (profiles/r3_sft_padding_free_ab.md) until those are tuned.
     padding_free: Optional[bool] = None
 
     def __post_init__(self):
@@ -319,7 +321,7 @@ class SFTTrainer:
         a = self.args
         if a.padding_free is not None:
             return bool(a.padding_free)
-        if os.environ.get("GRT_SFT_PADDING_FREE", "1") == "0":
+        if os.environ.get("GRT_SFT_PADDING_FREE", "0") != "1":
             return False
         import inspect
         inner = getattr(self.model, "base_model", self.model)
