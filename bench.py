@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-rank collective path even at world 1 (one-rank RCCL process group: "
                          "ZeRO reduce-scatter / all-gather, FSDP gathers) — one-GPU rehearsal of the 8-GPU data plane")
+    ap.add_argument("--layers", type=int, default=0,
+                    help="rehearsal only: keep the first N decoder layers of --model (the JSON names the model "
+                         "'<model>[N/L layers]', so it is never mistaken for the full model's number)")
     ap.add_argument("--plan-only", action="store_true",
                     help="print the per-rank HBM / host memory plan (parallel/planner.py) for this config and exit")
     ap.add_argument("--launcher", default="", help=argparse.SUPPRESS)  # set by launch_workers
@@ -235,6 +238,10 @@ def run(a):
         from gke_ray_train_amd.ops.gemm_tuning import enable_tuned_gemms
         tuned = enable_tuned_gemms()
     cfg = get_config(a.model)
+    if a.layers and a.layers < cfg.num_hidden_layers:
+        full = cfg.num_hidden_layers
+        cfg = get_config(a.model, num_hidden_layers=a.layers)
+        cfg.name = f"{cfg.name}[{a.layers}/{full} layers]"
     from gke_ray_train_amd.parallel.planner import GiB, plan_memory
     plan = plan_memory(cfg, world, a.parallel, offload=a.offload, peft=a.peft, micro_batch=a.micro_batch or a.batch,
                        seq=a.seq, zero=(a.zero == "on" or (a.zero == "auto" and (world > 1 or a.force_collectives))),

@@ -42,15 +42,18 @@ void check_vec(const Tensor& t, int64_t d, const char* name) {
 const void* ptr_or_null(const optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
 
 // ------------------------------------------------------------------ norms
+// pad > 0: y is the [rows, d] view of a [rows, d + pad] buffer (row stride d + pad) whose last pad
+// columns a consumer fills (the LoRA h of a K-concatenated projection, peft/lora.py)
 std::vector<Tensor> rmsnorm_fwd(const Tensor& x, const optional<Tensor>& residual, const Tensor& w,
-                                double eps) {
+                                double eps, int64_t pad) {
   check_contig(x, "x");
   check_contig(w, "w");
   c10::OptionalDeviceGuard g(x.device());
   const int64_t d = x.size(-1), rows = x.numel() / d;
   check_vec(x, d, "x");
   TORCH_CHECK(w.numel() == d && w.scalar_type() == x.scalar_type(), "weight shape/dtype mismatch");
-  auto y = at::empty_like(x);
+  TORCH_CHECK(pad >= 0 && pad % 8 == 0 && (pad == 0 || x.dim() == 2), "rmsnorm_fwd: pad % 8 == 0 on [rows, d]");
+  auto y = pad == 0 ? at::empty_like(x) : at::empty({rows, d + pad}, x.options()).narrow(1, 0, d);
   auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
   Tensor h;
   if (residual.has_value()) {
@@ -60,7 +63,7 @@ std::vector<Tensor> rmsnorm_fwd(const Tensor& x, const optional<Tensor>& residua
   }
   grt::rmsnorm_fwd(dtype_of(x), x.data_ptr(), ptr_or_null(residual), w.data_ptr(), y.data_ptr(),
                    residual.has_value() ? h.data_ptr() : nullptr, rstd.data_ptr<float>(), rows, (int)d,
-                   (float)eps, cur_stream(x));
+                   (float)eps, cur_stream(x), d + pad);
   return {y, residual.has_value() ? h : x, rstd};
 }
 
@@ -130,15 +133,16 @@ std::vector<Tensor> layernorm_bwd(const Tensor& dy, const Tensor& h, const Tenso
 }
 
 // ------------------------------------------------------------------ elementwise
-Tensor swiglu_fwd(const Tensor& gu) {
+Tensor swiglu_fwd(const Tensor& gu, int64_t pad) {  // pad: as rmsnorm_fwd (a LoRA-tail row buffer)
   check_contig(gu, "gu");
   c10::OptionalDeviceGuard g(gu.device());
   const int64_t two_f = gu.size(-1), rows = gu.numel() / two_f, f = two_f / 2;
   check_vec(gu, f, "gu");
+  TORCH_CHECK(pad >= 0 && pad % 8 == 0 && (pad == 0 || gu.dim() == 2), "swiglu_fwd: pad % 8 == 0 on [rows, 2f]");
   auto sizes = gu.sizes().vec();
   sizes.back() = f;
-  auto out = at::empty(sizes, gu.options());
-  grt::swiglu_fwd(dtype_of(gu), gu.data_ptr(), out.data_ptr(), rows, (int)f, cur_stream(gu));
+  auto out = pad == 0 ? at::empty(sizes, gu.options()) : at::empty({rows, f + pad}, gu.options()).narrow(1, 0, f);
+  grt::swiglu_fwd(dtype_of(gu), gu.data_ptr(), out.data_ptr(), rows, (int)f, cur_stream(gu), f + pad);
   return out;
 }
 Tensor swiglu_bwd(const Tensor& gu, const Tensor& dout) {
@@ -317,7 +321,7 @@ static int device_cus(int dev) {
 // want_xd (same keep mask as dropout_fwd_seeded(x, p, seed, offset)). Returns {} when the shape is
 // not supported by the kernel (the caller falls back to the torch path).
 std::vector<Tensor> lora_down(const Tensor& x, const Tensor& a, double p, int64_t seed, int64_t offset,
-                              bool want_xd) {
+                              bool want_xd, const optional<Tensor>& h_out, double hscale) {
   check_cuda(x, "x");
   check_contig(a, "a");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && a.dim() == 2 && a.size(1) == x.size(1), "lora_down: shapes");
@@ -329,13 +333,22 @@ std::vector<Tensor> lora_down(const Tensor& x, const Tensor& a, double p, int64_
       reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 || reinterpret_cast<uintptr_t>(a.data_ptr()) % 16)
     return {};
   c10::OptionalDeviceGuard g(x.device());
-  auto h = at::empty({M, R}, x.options());
+  Tensor h;
+  if (h_out.has_value()) {  // e.g. the LoRA tail of the [x | h] row buffer (row stride > R)
+    h = *h_out;
+    TORCH_CHECK(h.dim() == 2 && h.size(0) == M && h.size(1) == R && h.stride(1) == 1 && h.stride(0) % 8 == 0 &&
+                    h.scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(h.data_ptr()) % 16 == 0,
+                "lora_down: h_out must be bf16 [M, R], unit column stride, 16-byte aligned rows");
+  } else {
+    h = at::empty({M, R}, x.options());
+  }
   Tensor xd;
   if (want_xd) xd = at::empty({M, K}, x.options());
   grt::LoraDownParams lp{};
   lp.x = x.data_ptr(); lp.a = a.data_ptr(); lp.h = h.data_ptr(); lp.xd = want_xd ? xd.data_ptr() : nullptr;
   lp.M = M; lp.K = K; lp.R = R; lp.ldx = (int)x.stride(0);
   lp.p = (float)p; lp.seed = (uint64_t)seed; lp.offset = (uint64_t)offset;
+  lp.ldh = h.stride(0); lp.hscale = (float)hscale;
   static const int split_env = [] { const char* e = getenv("GRT_LORA_DOWN_SPLIT"); return e ? atoi(e) : 0; }();
   lp.ksplit = split_env > 0 ? std::min(split_env, K / 128) : grt::lora_down_splits(M, K, device_cus(x.device().index()));
   Tensor hpart;
@@ -350,11 +363,19 @@ std::vector<Tensor> lora_down(const Tensor& x, const Tensor& a, double p, int64_
 
 // dx [M, K] (+)= keep / (1-p) * (g [M, R] @ at^T), at = A^T [K, R]; returns false (nothing done)
 // when the shape is not supported by the kernel.
+// g and dx may be row-strided (unit column stride); dx_in given: dx = dx_in + ... (dx_in row-strided too)
 bool lora_dx(const Tensor& g, const Tensor& at, const Tensor& dx, double p, int64_t seed, int64_t offset,
-             bool accumulate) {
-  check_contig(g, "g");
+             bool accumulate, const optional<Tensor>& dx_in, double gscale) {
   check_contig(at, "at");
-  check_contig(dx, "dx");
+  for (const Tensor* t : {&g, &dx}) {
+    check_cuda(*t, "lora_dx operand");
+    TORCH_CHECK(t->dim() == 2 && t->stride(1) == 1 && t->stride(0) % 8 == 0, "lora_dx: row-major operands");
+  }
+  if (dx_in.has_value()) {
+    TORCH_CHECK(dx_in->sizes() == dx.sizes() && dx_in->stride(1) == 1 && dx_in->stride(0) % 8 == 0 &&
+                    dx_in->scalar_type() == at::kBFloat16 && reinterpret_cast<uintptr_t>(dx_in->data_ptr()) % 16 == 0,
+                "lora_dx: dx_in like dx");
+  }
   TORCH_CHECK(g.dim() == 2 && at.dim() == 2 && dx.dim() == 2 && g.size(0) == dx.size(0) &&
                   at.size(0) == dx.size(1) && at.size(1) == g.size(1), "lora_dx: shapes");
   TORCH_CHECK(g.scalar_type() == at::kBFloat16 && at.scalar_type() == at::kBFloat16 &&
@@ -370,8 +391,32 @@ bool lora_dx(const Tensor& g, const Tensor& at, const Tensor& dx, double p, int6
   lp.g = g.data_ptr(); lp.at = at.data_ptr(); lp.dx = dx.data_ptr();
   lp.M = M; lp.K = K; lp.R = R;
   lp.p = (float)p; lp.seed = (uint64_t)seed; lp.offset = (uint64_t)offset; lp.accumulate = accumulate ? 1 : 0;
+  lp.ldg = g.stride(0); lp.ld_out = dx.stride(0); lp.gscale = (float)gscale;
+  if (dx_in.has_value()) { lp.dx_in = dx_in->data_ptr(); lp.ld_in = dx_in->stride(0); }
   grt::lora_dx(lp, cur_stream(dx));
   return true;
+}
+
+// B_i [n_i, r] -> the adapter tail of W' [out, ldw] (columns col0 + j r ..) and of W'^T [.., ldt]
+void lora_refresh(const std::vector<Tensor>& bs, const std::vector<int64_t>& offs, Tensor& w, Tensor& wt, int64_t col0) {
+  TORCH_CHECK(!bs.empty() && bs.size() <= 4 && offs.size() == bs.size(), "lora_refresh: 1-4 targets");
+  TORCH_CHECK(w.dim() == 2 && wt.dim() == 2 && w.stride(1) == 1 && wt.stride(1) == 1 &&
+                  w.scalar_type() == at::kBFloat16 && wt.scalar_type() == at::kBFloat16, "lora_refresh: bf16 W', W'^T");
+  grt::LoraRefreshParams p{};
+  p.ntarget = (int)bs.size();
+  p.r = (int)bs[0].size(1);
+  TORCH_CHECK(p.r % 64 == 0 && col0 % 8 == 0 && w.stride(0) % 8 == 0 && wt.stride(0) % 8 == 0, "lora_refresh: r % 64");
+  for (size_t j = 0; j < bs.size(); ++j) {
+    check_contig(bs[j], "B");
+    TORCH_CHECK(bs[j].scalar_type() == at::kBFloat16 && bs[j].size(1) == p.r && bs[j].size(0) % 64 == 0 &&
+                    offs[j] % 8 == 0 && offs[j] + bs[j].size(0) <= w.size(0) &&
+                    col0 + (int64_t)(j + 1) * p.r <= w.size(1) && col0 + (int64_t)(j + 1) * p.r <= wt.size(0),
+                "lora_refresh: B_i bf16 [n % 64 == 0, r] inside W'");
+    p.b[j] = bs[j].data_ptr(); p.off[j] = (int)offs[j]; p.n[j] = (int)bs[j].size(0);
+  }
+  p.w = w.data_ptr(); p.ldw = w.stride(0); p.wt = wt.data_ptr(); p.ldt = wt.stride(0); p.col0 = (int)col0;
+  c10::OptionalDeviceGuard g(w.device());
+  grt::lora_refresh(p, cur_stream(w));
 }
 
 // ------------------------------------------------------------------ cross entropy
@@ -892,12 +937,13 @@ std::vector<int64_t> stream_cu_mask(int64_t stream, int64_t words) {
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gke_ray_train_amd HIP kernels for gfx950 (MI355X)";
-  m.def("rmsnorm_fwd", &rmsnorm_fwd);
+  m.def("rmsnorm_fwd", &rmsnorm_fwd, py::arg("x"), py::arg("residual"), py::arg("w"), py::arg("eps"),
+        py::arg("pad") = 0);
   m.def("rmsnorm_bwd", &rmsnorm_bwd, py::arg("dy"), py::arg("h"), py::arg("w"), py::arg("rstd"), py::arg("dres"),
         py::arg("dw_out") = py::none(), py::arg("accumulate") = false);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);
-  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_fwd", &swiglu_fwd, py::arg("gu"), py::arg("pad") = 0);
   m.def("swiglu_bwd", &swiglu_bwd);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd", &gelu_bwd);
@@ -908,8 +954,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dropout_fwd", &dropout_fwd);
   m.def("dropout_bwd", &dropout_bwd);
   m.def("dropout_fwd_seeded", &dropout_fwd_seeded);
-  m.def("lora_down", &lora_down);
-  m.def("lora_dx", &lora_dx);
+  m.def("lora_down", &lora_down, py::arg("x"), py::arg("a"), py::arg("p"), py::arg("seed"), py::arg("offset"),
+        py::arg("want_xd"), py::arg("h_out") = py::none(), py::arg("hscale") = 1.0);
+  m.def("lora_dx", &lora_dx, py::arg("g"), py::arg("at"), py::arg("dx"), py::arg("p"), py::arg("seed"),
+        py::arg("offset"), py::arg("accumulate"), py::arg("dx_in") = py::none(), py::arg("gscale") = 1.0);
+  m.def("lora_refresh", &lora_refresh);
   m.def("dropout_bwd_seeded", &dropout_bwd_seeded);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

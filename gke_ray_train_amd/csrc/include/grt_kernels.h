@@ -14,7 +14,8 @@ enum class DType : int { F32 = 0, BF16 = 1 };
 // y = norm(x [+ residual]) * w [+ b]; writes rstd (and mean for LayerNorm) per row in fp32.
 // If residual != nullptr, h = x + residual is written to h_out (the new residual stream).
 void rmsnorm_fwd(DType dt, const void* x, const void* residual, const void* w, void* y, void* h_out,
-                 float* rstd, int64_t rows, int d, float eps, hipStream_t s);
+                 float* rstd, int64_t rows, int d, float eps, hipStream_t s,
+                 int64_t ldy = 0);
 // dx = d/dh (norm) + dres ; dw accumulated through fp32 partials (workspace of
 // rmsnorm_bwd_workspace(rows, d) floats).
 // dw_t != null: the weight gradient is written in the parameter dtype straight into dw_t (a
@@ -31,7 +32,7 @@ void layernorm_bwd(DType dt, const void* dy, const void* h, const void* w, const
                    float* ws, int64_t rows, int d, hipStream_t s);
 
 // ---------------- elementwise (elementwise.hip) ----------------
-void swiglu_fwd(DType dt, const void* gu, void* out, int64_t rows, int f, hipStream_t s);
+void swiglu_fwd(DType dt, const void* gu, void* out, int64_t rows, int f, hipStream_t s, int64_t ldo = 0);
 void swiglu_bwd(DType dt, const void* gu, const void* dout, void* dgu, int64_t rows, int f,
                 hipStream_t s);
 // GELU (erf form) with optional fused dropout mask (uint8, 1 = keep, scale applied).
@@ -101,6 +102,8 @@ struct LoraDownParams {
   int64_t M; int K; int R; int ldx;
   float p; uint64_t seed; uint64_t offset;
   int ksplit = 1; float* hpart = nullptr;  // split-K: fp32 partials [ksplit][M][R], summed into h
+  int64_t ldh = 0;      // h row stride (0 = R); > R: h is the tail of a [x | h] row buffer
+  float hscale = 1.f;   // h = hscale * drop(x) A^T (the LoRA scaling folded in)
 };
 int lora_down_splits(int64_t M, int K, int cus);
 bool lora_down_supported(int64_t M, int K, int R, int ldx, uint64_t offset);
@@ -110,7 +113,19 @@ struct LoraDxParams {
   const void* g; const void* at; void* dx;
   int64_t M; int K; int R;
   float p; uint64_t seed; uint64_t offset; int accumulate;
+  int64_t ldg = 0;            // g row stride (0 = R)
+  const void* dx_in = nullptr; int64_t ld_in = 0;  // accumulate from dx_in (row stride ld_in), not dx
+  int64_t ld_out = 0;         // dx row stride (0 = K)
+  float gscale = 1.f;         // dx (+)= gscale * keep / (1-p) * (g A)
 };
+// Copy LoRA B_i [n_i, r] into the adapter tail of the K-concatenated weight W' [out, ldw] (columns
+// [col0 + j r, col0 + (j+1) r) of rows [off_i, off_i + n_i)) and of its transpose W'^T (rows
+// col0 + j r .. , row stride ldt), for up to 4 targets in one launch.
+struct LoraRefreshParams {
+  const void* b[4]; int off[4]; int n[4]; int ntarget; int r;
+  void* w; int64_t ldw; void* wt; int64_t ldt; int col0;
+};
+void lora_refresh(const LoraRefreshParams& p, hipStream_t s);
 bool lora_dx_supported(int64_t M, int K, int R, uint64_t offset);
 void lora_dx(const LoraDxParams& p, hipStream_t s);
 

@@ -28,7 +28,7 @@ inline unsigned grid_for(int64_t work) {
 // gu: [rows, 2F] = [gate | up]; out = silu(gate) * up
 template <typename T>
 __global__ __launch_bounds__(kNT) void swiglu_fwd_kernel(const T* __restrict__ gu, T* __restrict__ out,
-                                                         int64_t rows, int f) {
+                                                         int64_t rows, int f, int64_t ldo) {
   constexpr int V = Vec16<T>::N;
   const int vpr = f / V;
   const int64_t total = rows * vpr;
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(kNT) void swiglu_fwd_kernel(const T* __restrict__ g
     load16(gu + r * 2 * f + f + c, u);
 #pragma unroll
     for (int k = 0; k < V; ++k) o[k] = g[k] * sigmoidf_(g[k]) * u[k];
-    store16(out + r * f + c, o);
+    store16(out + r * ldo + c, o);  // ldo > f: the row of a wider [x | LoRA h] buffer
   }
 }
 
@@ -333,8 +333,9 @@ __global__ __launch_bounds__(kNT) void dropout_bwd_kernel(const T* __restrict__ 
     else { KERNEL(float, __VA_ARGS__); }                               \
   } while (0)
 
-void swiglu_fwd(DType dt, const void* gu, void* out, int64_t rows, int f, hipStream_t s) {
-#define K(T, ...) hipLaunchKernelGGL(swiglu_fwd_kernel<T>, dim3(grid_for(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)gu, (T*)out, rows, f)
+void swiglu_fwd(DType dt, const void* gu, void* out, int64_t rows, int f, hipStream_t s, int64_t ldo) {
+  if (ldo <= 0) ldo = f;
+#define K(T, ...) hipLaunchKernelGGL(swiglu_fwd_kernel<T>, dim3(grid_for(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)gu, (T*)out, rows, f, ldo)
   GRT_DISPATCH(dt, K, 0);
 #undef K
 }

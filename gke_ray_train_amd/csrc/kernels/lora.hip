@@ -179,7 +179,8 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
         *reinterpret_cast<f32x4*>(prow + rb * 32 + 8 * q + 4 * h) = v;
       }
   } else if (w == 0 && tok < P.M) {
-    bf16* hrow = static_cast<bf16*>(P.h) + tok * (int64_t)R;
+    bf16* hrow = static_cast<bf16*>(P.h) + tok * (P.ldh > 0 ? P.ldh : (int64_t)R);
+    const float hs = P.hscale;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -188,16 +189,17 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int ix = (rb * 16 + 4 * q + j) * 64 + lane;
-          v[j] = static_cast<bf16>(acc[rb][4 * q + j] + red[ix] + red[RB * 1024 + ix] + red[2 * RB * 1024 + ix]);
+          v[j] = static_cast<bf16>((acc[rb][4 * q + j] + red[ix] + red[RB * 1024 + ix] + red[2 * RB * 1024 + ix]) * hs);
         }
         *reinterpret_cast<bf16x4*>(hrow + rb * 32 + 8 * q + 4 * h) = v;
       }
   }
 }
 
-// h[M][R] = bf16(sum over the ksplit fp32 partials)
+// h[M][R] (row stride ldh) = bf16(hscale * sum over the ksplit fp32 partials)
 __global__ __launch_bounds__(256) void lora_hsum_kernel(const float* __restrict__ part, bf16* __restrict__ h,
-                                                        int64_t n4, int ksplit, int64_t stride) {
+                                                        int64_t n4, int ksplit, int64_t stride, int R, int64_t ldh,
+                                                        float hscale) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     f32x4 a = *reinterpret_cast<const f32x4*>(part + 4 * i);
     for (int k = 1; k < ksplit; ++k) {
@@ -206,8 +208,9 @@ __global__ __launch_bounds__(256) void lora_hsum_kernel(const float* __restrict_
     }
     bf16x4 o;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) o[j] = static_cast<bf16>(a[j]);
-    *reinterpret_cast<bf16x4*>(h + 4 * i) = o;
+    for (int j = 0; j < 4; ++j) o[j] = static_cast<bf16>(a[j] * hscale);
+    const int64_t e = 4 * i, row = e / R;
+    *reinterpret_cast<bf16x4*>(h + row * ldh + (e - row * R)) = o;
   }
 }
 
@@ -236,13 +239,17 @@ __global__ __launch_bounds__(256) void lora_dx_kernel(const LoraDxParams P) {
   const int64_t tb = blockIdx.x / nkb;
   const int kb = blockIdx.x % nkb;
   bf16* dx = static_cast<bf16*>(P.dx);
+  const int64_t ldo = P.ld_out > 0 ? P.ld_out : (int64_t)P.K;
+  const bf16* din = P.dx_in != nullptr ? static_cast<const bf16*>(P.dx_in) : dx;
+  const int64_t ldi = P.dx_in != nullptr ? P.ld_in : ldo;
+  const int64_t ldg = P.ldg > 0 ? P.ldg : (int64_t)R;
   bf16x8 old[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int c = tid + 256 * i, row = c >> 4, col = (c & 15) * 8;
     const int64_t tok = tb * 64 + row;
     old[i] = bf16x8{};
-    if (P.accumulate && tok < P.M) old[i] = *reinterpret_cast<const bf16x8*>(dx + tok * (int64_t)P.K + kb * 128 + col);
+    if (P.accumulate && tok < P.M) old[i] = *reinterpret_cast<const bf16x8*>(din + tok * ldi + kb * 128 + col);
   }
   // images: R / 8 chunks of 16 B per row
   constexpr int CPR = R / 8;
@@ -253,7 +260,7 @@ __global__ __launch_bounds__(256) void lora_dx_kernel(const LoraDxParams P) {
     const int row = c / CPR, col = (c % CPR) * 8;
     const int64_t tok = tb * 64 + row;
     *reinterpret_cast<bf16x8*>(gimg + row * RP + col) =
-        *reinterpret_cast<const bf16x8*>(g + (tok < P.M ? tok : P.M - 1) * (int64_t)R + col);
+        *reinterpret_cast<const bf16x8*>(g + (tok < P.M ? tok : P.M - 1) * ldg + col);
   }
 #pragma unroll
   for (int c = tid; c < 128 * CPR; c += 256) {
@@ -284,7 +291,7 @@ __global__ __launch_bounds__(256) void lora_dx_kernel(const LoraDxParams P) {
   __syncthreads();
   const bool drop = P.p > 0.f;
   const uint32_t thr = drop_thr(P.p);
-  const float sc = drop ? 1.f / (1.f - P.p) : 1.f;
+  const float sc = (drop ? 1.f / (1.f - P.p) : 1.f) * P.gscale;
   const uint64_t key = hash_u64(P.seed);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -302,11 +309,52 @@ __global__ __launch_bounds__(256) void lora_dx_kernel(const LoraDxParams P) {
       const float v = (drop && !kp[e]) ? 0.f : d[e] * sc;
       o[e] = static_cast<bf16>(static_cast<float>(old[i][e]) + v);
     }
-    *reinterpret_cast<bf16x8*>(dx + t * (int64_t)P.K + kb * 128 + col) = o;
+    *reinterpret_cast<bf16x8*>(dx + t * ldo + kb * 128 + col) = o;
+  }
+}
+
+// ---- lora_refresh: B_i -> the adapter tail of W' (rows off_i.., columns col0 + j r ..) and of W'^T
+// (rows col0 + j r .., columns off_i ..). One workgroup = a 64-row slab of one B_i, staged in LDS so
+// both the row-major and the transposed writes are full 128 B rows.
+__global__ __launch_bounds__(256) void lora_refresh_kernel(const LoraRefreshParams P) {
+  __shared__ bf16 tile[64][64 + 8];
+  int j = 0, slab = blockIdx.x;
+  while (j + 1 < P.ntarget && slab >= (P.n[j] + 63) / 64) { slab -= (P.n[j] + 63) / 64; ++j; }
+  const bf16* B = static_cast<const bf16*>(P.b[j]);
+  const int r0 = slab * 64, n = P.n[j];
+  bf16* W = static_cast<bf16*>(P.w);
+  bf16* WT = static_cast<bf16*>(P.wt);
+  for (int c0 = 0; c0 < P.r; c0 += 64) {
+    for (int e = threadIdx.x; e < 64 * 8; e += 256) {  // 64 rows x 8 chunks of 8 bf16
+      const int rr = e >> 3, cc = (e & 7) * 8;
+      if (r0 + rr < n) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(B + (int64_t)(r0 + rr) * P.r + c0 + cc);
+        *reinterpret_cast<bf16x8*>(W + (int64_t)(P.off[j] + r0 + rr) * P.ldw + P.col0 + j * P.r + c0 + cc) = v;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tile[rr][cc + q] = v[q];
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * 8; e += 256) {  // W'^T rows = the 64 columns of the slab
+      const int cc = e >> 3, rr = (e & 7) * 8;
+      if (r0 + rr < n) {
+        bf16x8 v;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = tile[rr + q][cc];
+        *reinterpret_cast<bf16x8*>(WT + (int64_t)(P.col0 + j * P.r + c0 + cc) * P.ldt + P.off[j] + r0 + rr) = v;
+      }
+    }
+    __syncthreads();
   }
 }
 
 }  // namespace
+
+void lora_refresh(const LoraRefreshParams& p, hipStream_t s) {
+  int blocks = 0;
+  for (int j = 0; j < p.ntarget; ++j) blocks += (p.n[j] + 63) / 64;
+  hipLaunchKernelGGL(lora_refresh_kernel, dim3((unsigned)blocks), dim3(256), 0, s, p);
+}
 
 bool lora_down_supported(int64_t M, int K, int R, int ldx, uint64_t offset) {
   return M > 0 && K % 128 == 0 && R % 32 == 0 && R >= 32 && R <= 256 && ldx % 8 == 0 && offset % 4 == 0;
@@ -344,7 +392,7 @@ void lora_down(const LoraDownParams& p, hipStream_t s) {
     int64_t g = (n4 + 255) / 256;
     if (g > 2048) g = 2048;
     hipLaunchKernelGGL(lora_hsum_kernel, dim3((unsigned)g), dim3(256), 0, s, p.hpart, static_cast<bf16*>(p.h), n4,
-                       p.ksplit, p.M * (int64_t)p.R);
+                       p.ksplit, p.M * (int64_t)p.R, p.R, p.ldh > 0 ? p.ldh : (int64_t)p.R, p.hscale);
   }
 }
 

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
                                                        const T* __restrict__ b, T* __restrict__ y,
                                                        T* __restrict__ h_out, float* __restrict__ mean_out,
                                                        float* __restrict__ rstd_out, int64_t rows,
-                                                       int d, float eps) {
+                                                       int d, float eps, int64_t ldy) {
   constexpr int V = Vec16<T>::N;
   typedef typename Vec16<T>::type VT;
   const int lane = threadIdx.x & 63;
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(kNT) void norm_fwd_kernel(const T* __restrict__ x,
 #pragma unroll
         for (int i = 0; i < V; ++i) o[i] = (hv[c][i] - mu) * rstd * to_f(wvv[c][i]);
       }
-      store16(y + row * d + ch * V, o);
+      store16(y + row * ldy + ch * V, o);  // ldy > d: the row of a wider [x | LoRA h] buffer
     }
   }
   if (lane == 0) {
@@ -242,14 +242,15 @@ __global__ __launch_bounds__(kNT) void colsum_kernel(const float* __restrict__ w
 
 template <typename T, bool RMS>
 void launch_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* h_out,
-                float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t s) {
+                float* mean, float* rstd, int64_t rows, int d, float eps, hipStream_t s, int64_t ldy = 0) {
+  if (ldy <= 0) ldy = d;
   constexpr int V = Vec16<T>::N;
   const int per_lane = (d / V + kWave - 1) / kWave;
   const dim3 grid((unsigned)((rows + kRowsPerBlock - 1) / kRowsPerBlock));
 #define GRT_NF4(MC, RES, FULL)                                                                  \
   hipLaunchKernelGGL((norm_fwd_kernel<T, MC, RMS, RES, FULL>), grid, dim3(kNT), 0, s, (const T*)x, \
                      (const T*)res, (const T*)w, (const T*)b, (T*)y, (T*)h_out, mean, rstd, rows,     \
-                     d, eps)
+                     d, eps, ldy)
 #define GRT_NF(MC)                                                     \
   do {                                                                 \
     const bool full = (d / V) == (MC) * kWave;                         \
@@ -320,11 +321,11 @@ void launch_bwd(const void* dy, const void* h, const void* w, const float* mean,
 int64_t norm_bwd_workspace_floats(int64_t rows, int d) { return (int64_t)bwd_blocks(rows) * 2 * d; }
 
 void rmsnorm_fwd(DType dt, const void* x, const void* residual, const void* w, void* y, void* h_out,
-                 float* rstd, int64_t rows, int d, float eps, hipStream_t s) {
+                 float* rstd, int64_t rows, int d, float eps, hipStream_t s, int64_t ldy) {
   if (dt == DType::BF16)
-    launch_fwd<bf16, true>(x, residual, w, nullptr, y, h_out, nullptr, rstd, rows, d, eps, s);
+    launch_fwd<bf16, true>(x, residual, w, nullptr, y, h_out, nullptr, rstd, rows, d, eps, s, ldy);
   else
-    launch_fwd<float, true>(x, residual, w, nullptr, y, h_out, nullptr, rstd, rows, d, eps, s);
+    launch_fwd<float, true>(x, residual, w, nullptr, y, h_out, nullptr, rstd, rows, d, eps, s, ldy);
 }
 
 void rmsnorm_bwd(DType dt, const void* dy, const void* h, const void* w, const float* rstd,

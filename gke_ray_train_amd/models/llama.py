@@ -121,6 +121,13 @@ def get_config(name: str, **overrides) -> LlamaConfig:
     return LlamaConfig(**d)
 
 
+def _tail_pad(proj) -> int:
+    """Columns a K-concatenated LoRA projection (peft/lora.py) wants after each row of its input, so
+    the producer (norm / attention / SwiGLU kernel) writes that input into a [rows, in + pad] row
+    buffer and the adapter's h lands beside it; 0 for a plain projection."""
+    return getattr(proj, "kcat_pad", 0)
+
+
 class FusedLinear(Linear):
     """nn.Linear whose output columns are the concatenation of named HF projections."""
 
@@ -148,7 +155,8 @@ class LlamaAttention(nn.Module):
             from ..parallel.sequence import ulysses_attention
             o = ulysses_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, sp, causal=True)
         else:
-            o = ops.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, causal=True, varlen=varlen)
+            o = ops.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, causal=True, varlen=varlen,
+                                   pad=_tail_pad(self.o_proj))
         return self.o_proj(o)
 
 
@@ -160,7 +168,7 @@ class LlamaMLP(nn.Module):
         self.down_proj = Linear(f, cfg.hidden_size, bias=False, device=device, dtype=dtype)
 
     def forward(self, x):
-        return self.down_proj(ops.swiglu(self.gate_up_proj(x)))
+        return self.down_proj(ops.swiglu(self.gate_up_proj(x), pad=_tail_pad(self.down_proj)))
 
 
 class RMSNorm(nn.Module):
@@ -189,13 +197,15 @@ class LlamaDecoderLayer(nn.Module):
 
     def forward(self, h, residual, B, S, cos, sin, varlen=None):
         eps = self.input_layernorm.eps
+        pad = _tail_pad(self.self_attn.qkv_proj)
         if residual is None:
             residual = h
-            x = ops.rms_norm(h, self.input_layernorm.weight, eps)
+            x = ops.rms_norm(h, self.input_layernorm.weight, eps, pad=pad)
         else:
-            x, residual = ops.add_rms_norm(h, residual, self.input_layernorm.weight, eps)
+            x, residual = ops.add_rms_norm(h, residual, self.input_layernorm.weight, eps, pad=pad)
         h = self.self_attn(x, B, S, cos, sin, varlen)
-        x, residual = ops.add_rms_norm(h, residual, self.post_attention_layernorm.weight, eps)
+        x, residual = ops.add_rms_norm(h, residual, self.post_attention_layernorm.weight, eps,
+                                       pad=_tail_pad(self.mlp.gate_up_proj))
         return self.mlp(x), residual
 
 

@@ -21,12 +21,20 @@ def _gpu(t: torch.Tensor) -> bool:
 
 
 # ----------------------------------------------------------------------------- RMSNorm
+def _tail(y, pad):
+    """Mark a producer output written into a [rows, d + pad] row buffer: the consumer (a
+    K-concatenated LoRA projection, peft/lora.py) may fill the ``pad`` tail columns."""
+    if pad:
+        y._grt_tail = pad
+    return y
+
+
 class _RMSNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, eps):
+    def forward(ctx, x, w, eps, pad=0):
         C = _native.kernels()
         xc = x.contiguous()
-        y, _, rstd = C.rmsnorm_fwd(xc, None, w.contiguous(), eps)
+        y, _, rstd = C.rmsnorm_fwd(xc, None, w.contiguous(), eps, pad)
         ctx.save_for_backward(xc, w, rstd)
         return y
 
@@ -35,7 +43,7 @@ class _RMSNorm(torch.autograd.Function):
         x, w, rstd = ctx.saved_tensors
         dx, dw = _norm_bwd_into_slot(w, lambda out, acc: _native.kernels().rmsnorm_bwd(
             dy.contiguous(), x, w, rstd, None, out, acc))
-        return dx, dw, None
+        return dx, dw, None, None
 
 
 _NORM_DIRECT_GRAD = os.environ.get("GRT_NORM_DIRECT_GRAD", "1") != "0"
@@ -59,9 +67,9 @@ class _AddRMSNorm(torch.autograd.Function):
     """h = x + residual ; y = rmsnorm(h) * w  -> (y, h), residual add fused into the norm."""
 
     @staticmethod
-    def forward(ctx, x, residual, w, eps):
+    def forward(ctx, x, residual, w, eps, pad=0):
         C = _native.kernels()
-        y, h, rstd = C.rmsnorm_fwd(x.contiguous(), residual.contiguous(), w.contiguous(), eps)
+        y, h, rstd = C.rmsnorm_fwd(x.contiguous(), residual.contiguous(), w.contiguous(), eps, pad)
         ctx.save_for_backward(h, w, rstd)
         return y, h
 
@@ -71,19 +79,23 @@ class _AddRMSNorm(torch.autograd.Function):
         dy = torch.zeros_like(h) if dy is None else dy.contiguous()
         dres = None if dh is None else dh.contiguous()
         dx, dw = _norm_bwd_into_slot(w, lambda out, acc: _native.kernels().rmsnorm_bwd(dy, h, w, rstd, dres, out, acc))
-        return dx, dx, dw, None
+        return dx, dx, dw, None, None
 
 
-def rms_norm(x, w, eps=1e-5):
+def rms_norm(x, w, eps=1e-5, pad: int = 0):
+    """``pad`` > 0 (GPU, 2-D x): the output is the [rows, d] view of a [rows, d + pad] row buffer whose
+    tail a K-concatenated LoRA consumer fills (``peft/lora.py``); numerically unchanged."""
     if _gpu(x):
-        return _RMSNorm.apply(x, w, eps)
+        return _tail(_RMSNorm.apply(x, w, eps, pad if x.dim() == 2 else 0), pad if x.dim() == 2 else 0)
     return _ref.rmsnorm(x, w, eps)[0]
 
 
-def add_rms_norm(x, residual, w, eps=1e-5):
-    """Returns (rmsnorm(x + residual) * w, x + residual)."""
+def add_rms_norm(x, residual, w, eps=1e-5, pad: int = 0):
+    """Returns (rmsnorm(x + residual) * w, x + residual); ``pad`` as in ``rms_norm``."""
     if _gpu(x):
-        return _AddRMSNorm.apply(x, residual, w, eps)
+        pad = pad if x.dim() == 2 else 0
+        y, h = _AddRMSNorm.apply(x, residual, w, eps, pad)
+        return _tail(y, pad), h
     return _ref.rmsnorm(x, w, eps, residual=residual)
 
 
@@ -116,21 +128,23 @@ def layer_norm(x, w, b=None, eps=1e-5, residual=None):
 # ----------------------------------------------------------------------------- activations
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu):
+    def forward(ctx, gu, pad=0):
         gu = gu.contiguous()
         ctx.save_for_backward(gu)
-        return _native.kernels().swiglu_fwd(gu)
+        return _native.kernels().swiglu_fwd(gu, pad)
 
     @staticmethod
     def backward(ctx, dout):
         (gu,) = ctx.saved_tensors
-        return _native.kernels().swiglu_bwd(gu, dout.contiguous())
+        return _native.kernels().swiglu_bwd(gu, dout.contiguous()), None
 
 
-def swiglu(gu):
-    """silu(gu[..., :F]) * gu[..., F:] for the fused [gate | up] projection output."""
+def swiglu(gu, pad: int = 0):
+    """silu(gu[..., :F]) * gu[..., F:] for the fused [gate | up] projection output; ``pad`` as in
+    ``rms_norm`` (the down projection's LoRA tail)."""
     if _gpu(gu):
-        return _SwiGLU.apply(gu)
+        pad = pad if gu.dim() == 2 else 0
+        return _tail(_SwiGLU.apply(gu, pad), pad)
     return _ref.swiglu(gu)
 
 
@@ -294,7 +308,7 @@ class _RopeAttention(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen=None):
+    def forward(ctx, qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen=None, pad=0):
         C = _native.kernels()
         qkv = qkv.contiguous()
         cu, ml = (varlen.cu, varlen.max_len) if varlen is not None else (None, 0)
@@ -303,12 +317,15 @@ class _RopeAttention(torch.autograd.Function):
         q4 = q.view(B, S, hq, D)
         k4 = k.view(B, S, hkv, D)
         v4 = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
-        o = torch.empty(B, S, hq, D, device=qkv.device, dtype=qkv.dtype)
+        # the output rows may be the head of [o | LoRA h] row buffers (the o_proj's K-concat tail)
+        ld = hq * D + pad
+        ow = torch.empty(B * S, ld, device=qkv.device, dtype=qkv.dtype)
+        o = ow.as_strided((B, S, hq, D), (S * ld, ld, D, 1))
         _, lse = C.attn_fwd(q4, k4, v4, o, scale, causal, None, cu_seqlens=cu, max_seqlen=ml)
         ctx.save_for_backward(qkv, q, k, o, lse, cos, sin)
         ctx.dims = (B, S, hq, hkv, D, causal, scale)
         ctx.varlen = varlen
-        return o.view(B * S, hq * D)
+        return ow[:, :hq * D]
 
     @staticmethod
     def backward(ctx, do):
@@ -333,14 +350,16 @@ class _RopeAttention(torch.autograd.Function):
                                    scale, causal, None, cu_seqlens=cu, max_seqlen=ml)
             C.rope_bwd(dq, dk, dqkv, cos, sin, vl.pos if vl is not None else None, hq, hkv, D,
                        ml if vl is not None else S)
-        return dqkv, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None
 
 
-def rope_attention(qkv, cos, sin, B, S, hq, hkv, D, causal=True, scale=None, varlen: "Varlen" = None):
-    """``varlen``: the B*S rows are padding-free packed sequences (B = 1; see ``Varlen``)."""
+def rope_attention(qkv, cos, sin, B, S, hq, hkv, D, causal=True, scale=None, varlen: "Varlen" = None,
+                   pad: int = 0):
+    """``varlen``: the B*S rows are padding-free packed sequences (B = 1; see ``Varlen``).
+    ``pad`` as in ``rms_norm``: the o_proj's LoRA tail after each output row."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if _gpu(qkv) and qkv.dtype == torch.bfloat16 and D == 128:
-        return _RopeAttention.apply(qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen)
+        return _tail(_RopeAttention.apply(qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen, pad), pad)
     x = qkv.view(B * S, hq + 2 * hkv, D)
     pos = varlen.pos if varlen is not None else None
     q = _ref.apply_rope(x[:, :hq], cos, sin, pos)

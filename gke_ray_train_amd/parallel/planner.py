@@ -81,6 +81,10 @@ class MemoryPlan:
 
 
 def host_available_bytes() -> Optional[float]:
+    """MemAvailable, or ``GRT_HOST_MEM_GB`` when the job's share of the node is capped below it."""
+    cap = os.environ.get("GRT_HOST_MEM_GB")
+    if cap:
+        return float(cap) * GiB
     try:
         with open("/proc/meminfo") as f:
             for line in f:

@@ -849,3 +849,100 @@ def test_decode_attention(B, Sk, hq, hkv, pad):
         o = ops.flash_attention(q, k, v, causal=not pad, seqlens_k=sl)
     ref = _ref.attention(q.float(), k.float(), v.float(), causal=not pad, seqlens_k=sl)
     _close(o, ref, 1e-2, 1e-2, "decode attention")
+
+
+@pytest.mark.parametrize("nf4", [False, True])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("engine", ["none", "ddp"])
+def test_kcat_lora_matches_reference(nf4, p, engine):
+    """K-concatenated LoRA (peft/lora.py _LoraKcatFn): the input is the head of a [M, in + R] row
+    buffer, h' lands in its tail, y = [x | h'] W'^T and [dX | g] = dY W' are single GEMMs. Same
+    y / dX / dA / dB as the fp32 formula (masks regenerated from the seed the op drew)."""
+    from gke_ray_train_amd.ops import _ref
+    from gke_ray_train_amd.ops.linear import Linear
+    from gke_ray_train_amd.peft.lora import LoraConfig, LoraLinear
+    from gke_ray_train_amd.peft.quant import BitsAndBytesConfig, NF4Linear
+    torch.manual_seed(0)
+    lin = Linear(256, 768, bias=False, device=DEV, dtype=torch.bfloat16)
+    lin.slices = [("q_proj", 256), ("k_proj", 256), ("v_proj", 256)]
+    base = NF4Linear.from_linear(lin, BitsAndBytesConfig()) if nf4 else lin
+    if nf4:
+        base.set_dequant_cache(True)
+    for q in base.parameters():
+        q.requires_grad_(False)
+    cfg = LoraConfig(r=64, lora_alpha=32, lora_dropout=p)
+    tg = [("q_proj", 0), ("k_proj", 256), ("v_proj", 512)]
+    mod = LoraLinear(base, [(n, off, 256) for n, off in tg], cfg).train()
+    names = [n for n, _ in tg]
+    R = 64 * 3
+    assert mod.kcat_pad == R
+    with torch.no_grad():
+        for n in names:
+            mod.lora_B[n].normal_(0, 0.05)
+    M = 384
+    xw = torch.randn(M, 256 + R, device=DEV, dtype=torch.bfloat16)
+    xw[:, 256:] = float("nan")  # the op must write every tail element before the GEMM reads it
+    x = xw[:, :256].detach().requires_grad_()
+    x._grt_tail = R
+    fwd = mod
+    if engine == "ddp":
+        from gke_ray_train_amd.parallel import DistributedDataParallel
+        fwd = DistributedDataParallel(mod)
+        x._grt_tail = R
+    rng = torch.get_rng_state()
+    y = fwd(x)
+    dy = torch.randn_like(y)
+    (y.float() * dy.float()).sum().backward()
+    if engine == "ddp":
+        fwd.finish_gradient_sync()
+    torch.set_rng_state(rng)
+    seed = int(torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).item())
+    x2 = x.detach().float().requires_grad_()
+    w = (base.dequantize() if nf4 else lin.weight).detach().float()
+    A = {n: mod.lora_A[n].detach().float().requires_grad_() for n in names}
+    B = {n: mod.lora_B[n].detach().float().requires_grad_() for n in names}
+    if p > 0:
+        keep = _ref.dropout_keep_mask(seed, 0, x2.numel(), p).to(DEV).view_as(x2).float()
+        xd = x2 * keep / (1 - p)
+    else:
+        xd = x2
+    yr = (x2 @ w.t()).clone()
+    for n, off in tg:
+        yr[:, off:off + 256] = yr[:, off:off + 256] + cfg.scaling * (xd @ A[n].t()) @ B[n].t()
+    (yr * dy.float()).sum().backward()
+    _close(y, yr, 3e-2, 3e-2, "kcat y")
+    _close(x.grad, x2.grad, 3e-2, 3e-2, "kcat dx")
+    for n in names:
+        for got, ref, what in ((mod.lora_A[n].grad, A[n].grad, "dA"), (mod.lora_B[n].grad, B[n].grad, "dB")):
+            rel = (got.float() - ref).norm() / ref.norm().clamp_min(1e-6)
+            assert rel < 2e-2, f"kcat {what} {n}: rel err {rel.item():.3g}"
+
+
+def test_kcat_lora_model_matches_epilogue_form(monkeypatch):
+    """A LoRA Llama whose q/k/v/o/gate/up run K-concatenated (down stays on the epilogue form: its
+    input width is not a multiple of 128 here) trains like the epilogue form: same loss, same
+    adapter gradients within bf16 tolerance."""
+    import gke_ray_train_amd.peft.lora as L
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.peft import LoraConfig, get_peft_model
+    res = {}
+    for kcat in (True, False):
+        monkeypatch.setattr(L, "_LORA_KCAT", kcat)
+        torch.manual_seed(0)
+        m = build_llama("llama-tiny-gqa", device=DEV, dtype=torch.bfloat16, seed=2)
+        pm = get_peft_model(m, LoraConfig(r=64, lora_alpha=16, lora_dropout=0.0))
+        for lm in pm.lora_modules.values():
+            for b in lm.lora_B.values():
+                torch.nn.init.normal_(b, 0, 0.02, generator=torch.Generator(device=DEV).manual_seed(9))
+        ids = torch.randint(0, m.config.vocab_size, (2, 256), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
+        loss = pm(ids, labels=ids)["loss"]
+        loss.backward()
+        res[kcat] = (float(loss), {n: p.grad.float().clone() for n, p in pm.named_parameters() if p.grad is not None})
+        if kcat:
+            assert any(lm.kcat_pad for lm in pm.lora_modules.values())
+    (l1, g1), (l0, g0) = res[True], res[False]
+    assert abs(l1 - l0) < 2e-2 * max(1.0, abs(l0))
+    assert g1.keys() == g0.keys() and g1
+    for n in g0:
+        rel = (g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-8)
+        assert rel < 5e-2, f"{n}: rel {rel.item():.3g}"
