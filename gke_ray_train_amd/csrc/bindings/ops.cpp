@@ -398,14 +398,18 @@ bool lora_dx(const Tensor& g, const Tensor& at, const Tensor& dx, double p, int6
 }
 
 // B_i [n_i, r] -> the adapter tail of W' [out, ldw] (columns col0 + j r ..) and of W'^T [.., ldt]
-void lora_refresh(const std::vector<Tensor>& bs, const std::vector<int64_t>& offs, Tensor& w, Tensor& wt, int64_t col0) {
+void lora_refresh(const std::vector<Tensor>& bs, const std::vector<int64_t>& offs, Tensor& w,
+                  const optional<Tensor>& wt_opt, int64_t col0) {
   TORCH_CHECK(!bs.empty() && bs.size() <= 4 && offs.size() == bs.size(), "lora_refresh: 1-4 targets");
-  TORCH_CHECK(w.dim() == 2 && wt.dim() == 2 && w.stride(1) == 1 && wt.stride(1) == 1 &&
-                  w.scalar_type() == at::kBFloat16 && wt.scalar_type() == at::kBFloat16, "lora_refresh: bf16 W', W'^T");
+  TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.scalar_type() == at::kBFloat16, "lora_refresh: bf16 W'");
+  Tensor wt = wt_opt.has_value() ? *wt_opt : w.t();  // no W'^T: only the shape checks use the view
+  if (wt_opt.has_value())
+    TORCH_CHECK(wt.dim() == 2 && wt.stride(1) == 1 && wt.scalar_type() == at::kBFloat16 && wt.stride(0) % 8 == 0,
+                "lora_refresh: bf16 W'^T");
   grt::LoraRefreshParams p{};
   p.ntarget = (int)bs.size();
   p.r = (int)bs[0].size(1);
-  TORCH_CHECK(p.r % 64 == 0 && col0 % 8 == 0 && w.stride(0) % 8 == 0 && wt.stride(0) % 8 == 0, "lora_refresh: r % 64");
+  TORCH_CHECK(p.r % 64 == 0 && col0 % 8 == 0 && w.stride(0) % 8 == 0, "lora_refresh: r % 64");
   for (size_t j = 0; j < bs.size(); ++j) {
     check_contig(bs[j], "B");
     TORCH_CHECK(bs[j].scalar_type() == at::kBFloat16 && bs[j].size(1) == p.r && bs[j].size(0) % 64 == 0 &&
@@ -414,7 +418,9 @@ void lora_refresh(const std::vector<Tensor>& bs, const std::vector<int64_t>& off
                 "lora_refresh: B_i bf16 [n % 64 == 0, r] inside W'");
     p.b[j] = bs[j].data_ptr(); p.off[j] = (int)offs[j]; p.n[j] = (int)bs[j].size(0);
   }
-  p.w = w.data_ptr(); p.ldw = w.stride(0); p.wt = wt.data_ptr(); p.ldt = wt.stride(0); p.col0 = (int)col0;
+  p.w = w.data_ptr(); p.ldw = w.stride(0); p.col0 = (int)col0;
+  p.wt = wt_opt.has_value() ? wt.data_ptr() : nullptr;
+  p.ldt = wt_opt.has_value() ? wt.stride(0) : 0;
   c10::OptionalDeviceGuard g(w.device());
   grt::lora_refresh(p, cur_stream(w));
 }

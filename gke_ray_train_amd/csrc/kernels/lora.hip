@@ -330,10 +330,13 @@ __global__ __launch_bounds__(256) void lora_refresh_kernel(const LoraRefreshPara
       if (r0 + rr < n) {
         const bf16x8 v = *reinterpret_cast<const bf16x8*>(B + (int64_t)(r0 + rr) * P.r + c0 + cc);
         *reinterpret_cast<bf16x8*>(W + (int64_t)(P.off[j] + r0 + rr) * P.ldw + P.col0 + j * P.r + c0 + cc) = v;
+        if (WT != nullptr) {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) tile[rr][cc + q] = v[q];
+          for (int q = 0; q < 8; ++q) tile[rr][cc + q] = v[q];
+        }
       }
     }
+    if (WT == nullptr) continue;  // workgroup-uniform: no transposed copy wanted
     __syncthreads();
     for (int e = threadIdx.x; e < 64 * 8; e += 256) {  // W'^T rows = the 64 columns of the slab
       const int cc = e >> 3, rr = (e & 7) * 8;

@@ -19,13 +19,11 @@ K-concatenated form (MI355X default, ``GRT_LORA_KCAT=0`` = the epilogue form abo
 rides INSIDE the base GEMM. The producer of the projection input (RMSNorm, attention, SwiGLU
 kernel) writes it into a [tokens, in + R] row buffer (R = r * targets); ``lora_down`` writes
 h' = s * dropout(x) A_cat^T into the R tail columns; the weight is kept as W' = [W | B_blockdiag]
-([out, in + R], and W'^T for the TN input-gradient GEMM) with the B blocks refreshed from the
-trainable B each forward (``lora_refresh`` kernel). Then
-    y  = [x | h'] W'^T                 one GEMM: base output + every adapter's up-projection,
-    [dX_base | g] = dY W'              one GEMM: base input gradient + g = dL/dh' for all targets,
-    dB_i = dY_i^T h'_i,  dA_cat = s g^T x_d,  dX = dX_base + s dropout'(g A_cat)  (``lora_dx``),
-so the per-target up-projection read-modify-writes of y and the per-target g GEMMs disappear;
-the cost is R extra K columns in the two base GEMMs (1-5 % of their FLOPs at r = 64).
+([out, in + R]) with the B blocks refreshed from the trainable B each forward (``lora_refresh``
+kernel). Then y = [x | h'] W'^T is ONE GEMM — base output plus every adapter's up-projection — so
+the per-target read-modify-writes of y disappear, for R extra K columns (1-5 % of the base GEMM
+at r = 64). The backward keeps the epilogue form (a single [dX | g] = dY W' GEMM was tried: its
+N = in + R runs ~15 % below the tiled N = in on hipBLASLt/rocBLAS, more than the g GEMMs it saves).
 
 Documented deviation: one dropout mask per fused input (HF draws separate masks for q, k, v).
 """
@@ -236,7 +234,9 @@ class _LoraFn(torch.autograd.Function):
 
 class _LoraKcatFn(torch.autograd.Function):
     """The K-concatenated adapted projection (module doc): x is the [M, in] head of a [M, in + R]
-    row buffer whose tail this op fills with h' = s * dropout(x) A_cat^T."""
+    row buffer whose tail this op fills with h' = s * dropout(x) A_cat^T; y = [x | h'] W'^T.
+    The backward keeps the epilogue form's GEMMs (base dX on the cached W^T, per-target g = s dY_i B_i):
+    one [dX | g] GEMM against W' was measured slower — its N = in + R is off the library's tiles."""
 
     @staticmethod
     def forward(ctx, x, mod, p, seed, offset, *ab):
@@ -255,78 +255,78 @@ class _LoraKcatFn(torch.autograd.Function):
         else:
             xd = C.dropout_fwd_seeded(x.contiguous(), p, seed, offset) if p > 0 else x
             xw[:, K:].copy_((xd @ acat.t()) * s)
-        wk, wkt = mod._kcat_weights(order, Bs)
-        y = F.linear(xw, wk)
+        y = F.linear(xw, mod._kcat_weight(order, Bs))
+        # a contiguous copy of h' for the dB GEMMs (rank-r slices of a 4K-wide row stride halve their speed)
+        hc = xw[:, K:].contiguous()
         ctx.mod, ctx.order, ctx.p, ctx.seed, ctx.offset = mod, order, p, seed, offset
-        ctx.save_for_backward(xw, xd, acat, *As, *Bs)
+        ctx.save_for_backward(hc, xd, acat, *As, *Bs)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xw, xd, acat, *ab = ctx.saved_tensors
+        hc, xd, acat, *ab = ctx.saved_tensors
         mod, order = ctx.mod, ctx.order
         k = len(mod.targets)
         As, Bs = ab[:k], ab[k:]
         r, s = mod.r, mod.scaling
-        M, KR = xw.shape
-        K = KR - r * k
+        M = hc.shape[0]
         C = _native.kernels()
         dy2 = dy.reshape(M, -1)
-        if dy2.dtype != xw.dtype:
-            dy2 = dy2.to(xw.dtype)
-        wk, wkt = mod._kcat_weights(order, None)
-        need_dx = ctx.needs_input_grad[0]
-        # [dX_base | g] = dY W' (TN form on the cached W'^T); without dX only the g columns
-        dxw = F.linear(dy2, wkt) if need_dx else F.linear(dy2, wkt[K:])
-        g = dxw[:, K:] if need_dx else dxw
+        if dy2.dtype != hc.dtype:
+            dy2 = dy2.to(hc.dtype)
+        dx = _base_input_grad(mod.base, dy2) if ctx.needs_input_grad[0] else None
+        g = torch.zeros(M, r * k, device=dy2.device, dtype=dy2.dtype)  # dL/dh (unscaled h) = s dY_i B_i
         dBs: List[Optional[torch.Tensor]] = [None] * k
-        for j, i in enumerate(order):                        # dB_i = dY_i^T h'_i (h' carries s)
+        for j, i in enumerate(order):
             off, n, _ = mod._spec[i]
             dyi = dy2[:, off:off + n]
-            hj = xw[:, K + j * r:K + (j + 1) * r]
+            hj = hc[:, j * r:(j + 1) * r]                    # h' = s h: dB_i = dY_i^T h'_i
+            g[:, j * r:(j + 1) * r].addmm_(dyi, Bs[i], alpha=s)
             sl = _slot_of(Bs[i])
             if sl is not None:
                 sl.write(lambda v: v.addmm_(dyi.t(), hj, beta=0.0), lambda v: v.addmm_(dyi.t(), hj))
                 sl.notify(Bs[i])
             else:
                 dBs[i] = torch.mm(dyi.t(), hj)
-        dAs: List[Optional[torch.Tensor]] = [None] * k
-        aslots = [_slot_of(As[i]) for i in order]
-        pk = None
-        if all(sl is not None for sl in aslots) and len({sl.fresh for sl in aslots}) == 1:
-            pk = _packed([sl.view for sl in aslots])
-        if pk is not None and pk[0] == list(range(k)):       # dA_cat = s g^T x_d into the adjacent slots
-            dst = pk[1]
-            if aslots[0].fresh:
-                dst.addmm_(g.t(), xd, beta=0.0, alpha=s)
-            else:
-                dst.addmm_(g.t(), xd, alpha=s)
-            for sl, i in zip(aslots, order):
-                sl.fresh, sl.direct = False, True
-                sl.notify(As[i])
-        else:
-            dacat = torch.mm(g.t(), xd).mul_(s)
-            for j, i in enumerate(order):
-                rows = dacat[j * r:(j + 1) * r]
-                sl = aslots[j]
-                if sl is not None:
-                    sl.write(lambda v: v.copy_(rows), lambda v: v.add_(rows))
-                    sl.notify(As[i])
-                else:
-                    dAs[i] = rows
-        dx = None
-        if need_dx:
-            # dX = dX_base + s * dropout'(g A_cat): one pass (lora.hip), contiguous output
-            dx = torch.empty(M, K, device=dy2.device, dtype=dy2.dtype)
-            if not (_LORA_DX and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True,
-                                           dx_in=dxw[:, :K], gscale=s)):
-                ga = (g @ acat) * s
+        dAs = _lora_dA(g, xd, As, order, r)
+        if dx is not None:
+            bf16 = g.dtype == acat.dtype == dx.dtype == torch.bfloat16
+            if not (_LORA_DX and bf16 and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
                 if ctx.p > 0:
-                    dx.copy_(dxw[:, :K])
-                    C.dropout_bwd_seeded(ga, dx, ctx.p, ctx.seed, ctx.offset, True)
+                    C.dropout_bwd_seeded(g @ acat, dx, ctx.p, ctx.seed, ctx.offset, True)
                 else:
-                    torch.add(dxw[:, :K], ga, out=dx)
+                    dx.addmm_(g, acat)
         return (dx, None, None, None, None, *dAs, *dBs)
+
+
+def _lora_dA(g, xd, As, order, r):
+    """dA_cat = g^T x_d, written into the (adjacent) gradient slots when the engine provides them."""
+    k = len(As)
+    dAs: List[Optional[torch.Tensor]] = [None] * k
+    aslots = [_slot_of(As[i]) for i in order]
+    pk = None
+    if all(sl is not None for sl in aslots) and len({sl.fresh for sl in aslots}) == 1:
+        pk = _packed([sl.view for sl in aslots])
+    if pk is not None and pk[0] == list(range(k)):
+        dst = pk[1]
+        if aslots[0].fresh:
+            dst.addmm_(g.t(), xd, beta=0.0)
+        else:
+            dst.addmm_(g.t(), xd)
+        for sl, i in zip(aslots, order):
+            sl.fresh, sl.direct = False, True
+            sl.notify(As[i])
+    else:
+        dacat = g.t() @ xd
+        for j, i in enumerate(order):
+            rows = dacat[j * r:(j + 1) * r]
+            sl = aslots[j]
+            if sl is not None:
+                sl.write(lambda v: v.copy_(rows), lambda v: v.add_(rows))
+                sl.notify(As[i])
+            else:
+                dAs[i] = rows
+    return dAs
 
 
 class LoraLinear(nn.Module):
@@ -353,8 +353,7 @@ class LoraLinear(nn.Module):
         self.full_cover = (len(self.targets) == 1 and self.targets[0][1] == 0 and
                            self.targets[0][2] == self.out_features)
         self._spec = [(off, n, name) for name, off, n in self.targets]
-        self._wk = None     # K-concatenated weight [out, in + R] and its transpose (built lazily)
-        self._wkt = None
+        self._wk = None     # K-concatenated weight [out, in + R] (built lazily)
         self._wk_order = None
 
     @property
@@ -375,31 +374,29 @@ class LoraLinear(nn.Module):
         return R if ok and a0.dtype == torch.bfloat16 else 0
 
     @torch.no_grad()
-    def _kcat_weights(self, order, Bs):
-        """(W', W'^T) with the base part built once (frozen) and, when ``Bs`` is given, the B blocks
-        of the h' column order ``order`` refreshed (every forward: B changes each optimizer step)."""
-        K, R, r = self.in_features, self.r * len(self.targets), self.r
+    def _kcat_weight(self, order, Bs):
+        """W' = [W | B_blockdiag] with the base part built once (frozen) and the B blocks of the h'
+        column order ``order`` refreshed (every forward: B changes with each optimizer step)."""
+        K, r = self.in_features, self.r
+        R = r * len(self.targets)
         if self._wk is None:
             w = self.base.dequantize() if isinstance(self.base, NF4Linear) else self.base.weight.detach()
             wk = torch.zeros(self.out_features, K + R, device=w.device, dtype=w.dtype)
             wk[:, :K].copy_(w)
-            self._wk, self._wkt = wk, wk.t().contiguous()
-            if isinstance(self.base, NF4Linear):  # W' / W'^T replace the base's dequant cache
-                self.base._w_cache = self.base._wt_cache = None
-        if Bs is not None:
-            if self._wk_order != list(order):  # block positions moved: clear the whole tail once
-                self._wk[:, K:].zero_()
-                self._wkt[K:].zero_()
-                self._wk_order = list(order)
-            bl = [Bs[i].detach() for i in order]
-            offs = [self._spec[i][0] for i in order]
-            if all(b.is_contiguous() for b in bl):
-                _native.kernels().lora_refresh(bl, offs, self._wk, self._wkt, K)
-            else:
-                for j, (b, off) in enumerate(zip(bl, offs)):
-                    self._wk[off:off + b.shape[0], K + j * r:K + (j + 1) * r].copy_(b)
-                    self._wkt[K + j * r:K + (j + 1) * r, off:off + b.shape[0]].copy_(b.t())
-        return self._wk, self._wkt
+            self._wk = wk
+            if isinstance(self.base, NF4Linear):  # W' replaces the forward dequant cache (dX keeps W^T's)
+                self.base._w_cache = None
+        if self._wk_order != list(order):  # block positions moved: clear the whole tail once
+            self._wk[:, K:].zero_()
+            self._wk_order = list(order)
+        bl = [Bs[i].detach() for i in order]
+        offs = [self._spec[i][0] for i in order]
+        if all(b.is_contiguous() for b in bl):
+            _native.kernels().lora_refresh(bl, offs, self._wk, None, K)
+        else:
+            for j, (b, off) in enumerate(zip(bl, offs)):
+                self._wk[off:off + b.shape[0], K + j * r:K + (j + 1) * r].copy_(b)
+        return self._wk
 
     def direct_grad_params(self) -> List[nn.Parameter]:
         """Parameters whose gradient the GPU backward writes into the engine's slot itself."""

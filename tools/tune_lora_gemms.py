@@ -19,15 +19,19 @@ ap.add_argument("--peft", default="lora", choices=["lora", "qlora"])
 ap.add_argument("--rows", type=int, default=8, help="sequences per step (SFT: batch 2 x accumulation 4 fused)")
 ap.add_argument("--seqs", default="1024", help="padded sequence lengths to tune at (M = rows x seq)")
 ap.add_argument("--duration", type=int, default=20, help="max tuning ms per shape")
+ap.add_argument("--base", default="", help="start from this results file instead of the shipped table")
 a = ap.parse_args()
 
 from gke_ray_train_amd.models import build_llama, get_config  # noqa: E402
 from gke_ray_train_amd.parallel import DistributedDataParallel  # noqa: E402
 from gke_ray_train_amd.peft import BitsAndBytesConfig, LoraConfig, get_peft_model, quantize_model_  # noqa: E402
 
+# no rotating operand copies: TunableOp sizes them from the leading dimensions, which overruns
+# the allocation for column-block views (the "HIP error: invalid argument" abort of round 2)
+os.environ.setdefault("PYTORCH_TUNABLEOP_ROTATING_BUFFER_SIZE", "0")
 tun = torch.cuda.tunable
 tun.enable(True)
-tun.read_file(str(RESULTS))
+tun.read_file(a.base or str(RESULTS))
 tun.tuning_enable(True)
 tun.set_max_tuning_duration(a.duration)
 tun.set_max_tuning_iterations(30)
