@@ -204,6 +204,14 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
     f32x16 s = f32x16{};
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) s = mfma32(kr[ks], qf[ks], s);
+    // three K fragments in flight ahead of the MFMA chain (the default schedule waits on each read)
+    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
     return s;
   };
   // -inf on the masked keys of tile t, applied only on tiles that touch the diagonal / key padding
@@ -272,6 +280,13 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
 #pragma unroll
       for (int db = 0; db < 4; ++db) o[db] = mfma32(va[stp][db], pb, o[db]);
     }
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 3, 0);
   };
 
   if (nt > 0) {
@@ -483,11 +498,27 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
       for (int r = 0; r < 16; ++r) s[r] = qt + acc_row(r, h) >= qlim ? 0.f : -INFINITY;
     }
     dp = f32x16{};
+    bf16x8 fq[D / 16], fd[D / 16];
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
-      s = mfma32(lds_row_read(qi, l32, 2 * ks + h), kf[ks], s);
-      dp = mfma32(lds_row_read(qi + K2IMG, l32, 2 * ks + h), vf[ks], dp);
+      fq[ks] = lds_row_read(qi, l32, 2 * ks + h);
+      fd[ks] = lds_row_read(qi + K2IMG, l32, 2 * ks + h);
     }
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      s = mfma32(fq[ks], kf[ks], s);
+      dp = mfma32(fd[ks], vf[ks], dp);
+    }
+    // keep three fragment pairs in flight ahead of the MFMAs that consume them (the default
+    // schedule issues each read right before its MFMA behind lgkmcnt(0): one wave per SIMD has no
+    // partner wave to cover that latency)
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
   };
 
   // tile cursors (query head, query start): the tile being consumed, the next one, the DMA one
@@ -539,18 +570,32 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
     sb[0] = pack8(dp_c, 0);
     sb[1] = pack8(dp_c, 8);
     // dV^T += dO^T P, dK^T += Q^T dS (transposed reads of tile t's images)
+    bf16x8 oa[2][4], qa[2][4];
 #pragma unroll
     for (int stp = 0; stp < 2; ++stp) {
       const int kk = 16 * stp + 4 * h;
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
         const int c0 = db * 32 + (g & 1) * 16;
-        const bf16x8 oa = cat(lds_tr_read(qi + K2IMG, kk, c0, l16), lds_tr_read(qi + K2IMG, kk + 8, c0, l16));
-        dv[db] = mfma32(oa, pb[stp], dv[db]);
-        const bf16x8 qa = cat(lds_tr_read(qi, kk, c0, l16), lds_tr_read(qi, kk + 8, c0, l16));
-        dk[db] = mfma32(qa, sb[stp], dk[db]);
+        oa[stp][db] = cat(lds_tr_read(qi + K2IMG, kk, c0, l16), lds_tr_read(qi + K2IMG, kk + 8, c0, l16));
+        qa[stp][db] = cat(lds_tr_read(qi, kk, c0, l16), lds_tr_read(qi, kk + 8, c0, l16));
       }
     }
+#pragma unroll
+    for (int stp = 0; stp < 2; ++stp)
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        dv[db] = mfma32(oa[stp][db], pb[stp], dv[db]);
+        dk[db] = mfma32(qa[stp][db], sb[stp], dk[db]);
+      }
+    // the transposed reads run three fragments (6 reads) ahead of their MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
     cur_h = nxt_h;
     cur_q = nxt_q;
     advance(nxt_h, nxt_q);
@@ -697,11 +742,25 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
       for (int r = 0; r < 16; ++r) s[r] = kb + acc_row(r, h) <= klim ? 0.f : -INFINITY;
     }
     dp = f32x16{};
+    bf16x8 fk[D / 16], fv[D / 16];
 #pragma unroll
     for (int ks = 0; ks < D / 16; ++ks) {
-      s = mfma32(lds_row_read(ki, l32, 2 * ks + h), qf[ks], s);
-      dp = mfma32(lds_row_read(ki + Q2IMG, l32, 2 * ks + h), of[ks], dp);
+      fk[ks] = lds_row_read(ki, l32, 2 * ks + h);
+      fv[ks] = lds_row_read(ki + Q2IMG, l32, 2 * ks + h);
     }
+#pragma unroll
+    for (int ks = 0; ks < D / 16; ++ks) {
+      s = mfma32(fk[ks], qf[ks], s);
+      dp = mfma32(fv[ks], of[ks], dp);
+    }
+    // two fragment pairs in flight ahead of the MFMAs (see the dK / dV kernel)
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
   };
 
   f32x16 dq[4];
