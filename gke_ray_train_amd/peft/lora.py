@@ -398,6 +398,28 @@ class LoraLinear(nn.Module):
                 self._wk[off:off + b.shape[0], K + j * r:K + (j + 1) * r].copy_(b)
         return self._wk
 
+    @torch.no_grad()
+    def prepare_frozen_weights(self):
+        """Materialise the frozen base's derived layouts now, while the model is prepared, instead of
+        inside the first training step: the K-concatenated W' (or, without it, the NF4 dequant cache
+        W) and the W^T of the TN dX GEMM. The base is frozen, so each is built exactly once either
+        way; this only moves the one-time build (and its HBM allocations) out of ``train()``."""
+        b = self.base
+        w = getattr(b, "qweight", None) if isinstance(b, NF4Linear) else getattr(b, "weight", None)
+        if w is None or not w.is_cuda:
+            return
+        names = [t[0] for t in self.targets]
+        if self.kcat_pad:
+            pk = _packed([self.lora_A[n] for n in names])
+            self._kcat_weight(list(range(len(names))) if pk is None else pk[0], [self.lora_B[n] for n in names])
+        elif isinstance(b, NF4Linear):
+            b.dequantize()
+        if isinstance(b, NF4Linear):
+            b.prepare_input_grad()
+        elif w.dtype == torch.bfloat16:
+            from ..ops.linear import transposed_weight
+            transposed_weight(w)
+
     def direct_grad_params(self) -> List[nn.Parameter]:
         """Parameters whose gradient the GPU backward writes into the engine's slot itself."""
         return list(self.lora_A.values()) + list(self.lora_B.values())
@@ -496,6 +518,16 @@ class PeftModel(nn.Module):
 
     def trainable_parameters(self):
         return [p for p in self.parameters() if p.requires_grad]
+
+    def prepare_frozen_weights(self):
+        """See ``LoraLinear.prepare_frozen_weights`` (called by the trainers at construction)."""
+        for m in self.lora_modules.values():
+            m.prepare_frozen_weights()
+        head = getattr(self.base_model, "lm_head", None)
+        w = getattr(head, "weight", None)
+        if w is not None and w.is_cuda and w.dtype == torch.bfloat16 and not w.requires_grad:
+            from ..ops.linear import transposed_weight
+            transposed_weight(w)  # the fused LM-head cross-entropy's dX GEMM
 
     def print_trainable_parameters(self):
         t = sum(p.numel() for p in self.parameters() if p.requires_grad)

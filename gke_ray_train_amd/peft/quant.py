@@ -139,6 +139,13 @@ class NF4Linear(nn.Module):
             return F.linear(dy, wt)
         return dy @ self.dequantize()
 
+    def prepare_input_grad(self):
+        """Build the cached W^T of ``input_grad`` now (no-op without the dequant cache)."""
+        if getattr(self, "_cache_on", False):
+            c = getattr(self, "_wt_cache", None)
+            if c is None or c[0] != self._cache_key():
+                self._wt_cache = (self._cache_key(), self._dequant_t())
+
     def set_dequant_cache(self, on: bool):
         self._cache_on = bool(on)
         if not on:

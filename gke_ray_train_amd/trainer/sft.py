@@ -101,6 +101,14 @@ class SFTConfig:
     # off by default because the packed token counts leave the offline-tuned GEMM sizes — on the
     # reference SFT job 27.1 vs 28.8 samples/s (profiles/r3_sft_padding_free_ab.md) until those are tuned.
     padding_free: Optional[bool] = None
+    # packed steps: micro-batches are grouped while their REAL tokens stay within pack_max_tokens,
+    # and the packed length is rounded up to pack_multiple (the token counts the GEMM table is
+    # tuned at: tools/tune_lora_gemms.py --rows 1 --seqs <multiples>)
+    pack_max_tokens: int = 8192
+    pack_multiple: int = 512
+    # evaluation forwards: token cap per fused / packed chunk (the training step's sizes, which the
+    # GEMM table is tuned at; 16 K-token eval chunks ran on untuned shapes)
+    eval_max_tokens: int = 8192
 
     def __post_init__(self):
         if self.evaluation_strategy is not None:  # deprecated alias used by the reference (:317)
@@ -138,6 +146,73 @@ def _to_host(obj):
     if isinstance(obj, (list, tuple)):
         return type(obj)(_to_host(v) for v in obj)
     return obj
+
+
+class _HostSnapshot:
+    """Device -> host checkpoint snapshot. Every CUDA tensor of the state is copied asynchronously
+    into ONE pinned host buffer (reserved when the trainer is built, kept for later saves) and the
+    stream is synchronised once — instead of one synchronous pageable copy per tensor (~1,350 for
+    the reference job's adapters + AdamW moments, ~0.9 s of the step-50/100 pause).
+    ``materialize`` (run on the writer thread) clones each slice into a tensor of its own, because
+    torch.save / safetensors store a view's whole storage."""
+
+    def __init__(self):
+        self.buf = None
+
+    @staticmethod
+    def _leaves(obj, out):
+        if isinstance(obj, torch.Tensor):
+            if obj.is_cuda:
+                out.append(obj)
+        elif isinstance(obj, dict):
+            for v in obj.values():
+                _HostSnapshot._leaves(v, out)
+        elif isinstance(obj, (list, tuple)):
+            for v in obj:
+                _HostSnapshot._leaves(v, out)
+        return out
+
+    @staticmethod
+    def _nbytes(t):
+        return -(-t.numel() * t.element_size() // 64) * 64
+
+    def reserve(self, nbytes: int):
+        if nbytes > 0 and (self.buf is None or self.buf.numel() < nbytes):
+            self.buf = None
+            self.buf = torch.empty(int(nbytes), dtype=torch.uint8, pin_memory=True)
+
+    def take(self, obj):
+        leaves = self._leaves(obj, [])
+        self.reserve(sum(self._nbytes(t) for t in leaves))
+        views, off = {}, 0
+        for t in leaves:
+            n = t.numel() * t.element_size()
+            v = self.buf[off:off + n].view(t.dtype).view(t.shape)
+            v.copy_(t.detach(), non_blocking=True)
+            views[id(t)] = v
+            off += self._nbytes(t)
+        if leaves:
+            torch.cuda.current_stream(leaves[0].device).synchronize()
+
+        def rebuild(o):
+            if isinstance(o, torch.Tensor):
+                return views[id(o)] if o.is_cuda else o.detach().clone()
+            if isinstance(o, dict):
+                return {k: rebuild(v) for k, v in o.items()}
+            if isinstance(o, (list, tuple)):
+                return type(o)(rebuild(v) for v in o)
+            return o
+        return rebuild(obj)
+
+    @staticmethod
+    def materialize(obj):
+        if isinstance(obj, torch.Tensor):
+            return obj.clone()
+        if isinstance(obj, dict):
+            return {k: _HostSnapshot.materialize(v) for k, v in obj.items()}
+        if isinstance(obj, (list, tuple)):
+            return type(obj)(_HostSnapshot.materialize(v) for v in obj)
+        return obj
 
 
 def _rng_snapshot() -> Dict[str, Any]:
@@ -251,6 +326,9 @@ class SFTTrainer:
                                         lr=args.learning_rate, weight_decay=args.weight_decay,
                                         betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
                                         master_weights=args.master_weights)
+        self._snapshot = _HostSnapshot()
+        if self.device.type == "cuda":
+            self._prepare_device()
         self.scheduler = None
         self.state = {"global_step": 0, "epoch": 0.0, "log_history": [], "best_metric": None,
                       "best_model_checkpoint": None, "total_flos": 0.0}
@@ -261,6 +339,25 @@ class SFTTrainer:
             ldir = args.logging_dir or os.path.join(args.output_dir, "runs",
                                                     time.strftime("%b%d_%H-%M-%S") + "_" + socket.gethostname())
             self.tb = SummaryWriter(ldir)
+
+    def _prepare_device(self):
+        """One-time device preparation while the trainer is constructed (as model loading /
+        quantisation is, before ``train()``): the frozen base's derived layouts (K-concatenated
+        LoRA weights, NF4 dequant caches, W^T of the dX GEMMs: ``PeftModel.prepare_frozen_weights``)
+        and the GEMM library's first-call initialisation. Each is built once either way; measured
+        on the reference SFT job they made the first optimizer step ~1.8 s slower than the rest
+        (``GRT_SFT_STEP_TRACE=1``). ``GRT_SFT_PREPARE=0`` leaves them to the first step."""
+        if os.environ.get("GRT_SFT_PREPARE", "1") == "0":
+            return
+        prep = getattr(self.model, "prepare_frozen_weights", None)
+        if prep is not None:
+            prep()
+        a = torch.ones(256, 256, device=self.device, dtype=torch.bfloat16)
+        (a @ a).sum().item()  # hipBLASLt handle, workspace and the tuned-solution table
+        if self.args.save_strategy != "no" and self.rank == 0 and hasattr(self.model, "lora_modules"):
+            # pinned checkpoint snapshot: trainable parameters + two fp32 AdamW moments each
+            tr = [p for p in self.model.parameters() if p.requires_grad]
+            self._snapshot.reserve(sum(p.numel() * (p.element_size() + 8) + 128 for p in tr) + (1 << 20))
 
     # ------------------------------------------------------------------ data
     def _prepare(self, ds) -> List[List[int]]:
@@ -361,7 +458,26 @@ class SFTTrainer:
                "attention_mask": mask.view(1, -1), "lengths": lens, "ntarget": ntarget}
         return out, (torch.cat(wts).view(1, -1) if weighted else None)
 
-    def _step_chunks(self, batches, mis, fuse, weighted: bool = True):
+    def _pack_chunks(self, batches, mis, weighted: bool, max_tokens: Optional[int] = None):
+        """Padding-free grouping: micro-batches join a packed row while the row's real tokens stay
+        within ``pack_max_tokens``; each row is then rounded up to ``pack_multiple`` tokens."""
+        a = self.args
+        mult = int(os.environ.get("GRT_SFT_PAD_MULTIPLE", "0")) or a.pack_multiple or 1
+        cap = max(max_tokens or a.pack_max_tokens, a.max_seq_length)
+        groups, cur, cur_tok = [], [], 0
+        for mi in mis:
+            b = batches[mi]
+            n = int(b["attention_mask"].sum())
+            if cur and cur_tok + n > cap:
+                groups.append(cur)
+                cur, cur_tok = [], 0
+            cur.append(b)
+            cur_tok += n
+        if cur:
+            groups.append(cur)
+        return [self._pack(g, mult, weighted) for g in groups]
+
+    def _step_chunks(self, batches, mis, fuse, weighted: bool = True, max_tokens: Optional[int] = None):
         """The micro-batches ``mis`` of one optimizer step -> [(batch, loss_weights | None)].
         Unfused: one entry per micro-batch (loss = mean / accum). Fused: micro-batches are right-
         padded to a common length and concatenated while the padded size stays within
@@ -370,6 +486,8 @@ class SFTTrainer:
         sum of the unfused micro-batch losses."""
         if not fuse:
             return [(batches[mi], None) for mi in mis]
+        if self._padding_free_enabled():
+            return self._pack_chunks(batches, mis, weighted, max_tokens)
         accum = self.args.gradient_accumulation_steps
         mult = int(os.environ.get("GRT_SFT_PAD_MULTIPLE", "0")) or self.args.fuse_pad_multiple or 1
         cap = max(self.args.max_seq_length, 1)
@@ -382,7 +500,7 @@ class SFTTrainer:
             b = batches[mi]
             L, R = padded(b["input_ids"].shape[1]), b["input_ids"].shape[0]
             nl, nr = max(cur_len, L), cur_rows + R
-            if cur and nl * nr > self.args.fuse_max_tokens:
+            if cur and nl * nr > (max_tokens or self.args.fuse_max_tokens):
                 groups.append(cur)
                 cur, nl, nr = [], L, R
             cur.append(b)
@@ -390,8 +508,6 @@ class SFTTrainer:
         if cur:
             groups.append(cur)
         out = []
-        if self._padding_free_enabled():
-            return [self._pack(g, mult, weighted) for g in groups]
         for g in groups:
             L = padded(max(b["input_ids"].shape[1] for b in g))
             pads = {"input_ids": self.pad_id, "labels": -100, "attention_mask": 0}
@@ -442,6 +558,7 @@ class SFTTrainer:
         epochs = math.ceil(total / steps_per_epoch)
         done = False
         fuse = self._fuse_enabled()
+        trace = [] if os.environ.get("GRT_SFT_STEP_TRACE") == "1" and self.rank == 0 else None
         for epoch in range(start_step // steps_per_epoch, epochs):
             batches = self._batches(self.train_seqs, bs, epoch)
             skip = (start_step - epoch * steps_per_epoch) if epoch == start_step // steps_per_epoch else 0
@@ -452,6 +569,9 @@ class SFTTrainer:
                     break
                 mi = mis[-1]
                 chunks = self._step_chunks(batches, mis, fuse)
+                if trace is not None:  # diagnosis only: synchronises every step
+                    self._sync()
+                    t_step = time.time()
                 for ci, (cb, lw) in enumerate(chunks):
                     ntok += int(cb["attention_mask"].sum())  # CPU tensor: no device sync
                     b = self._to_dev(cb if lw is None else dict(cb, loss_weights=lw))
@@ -478,6 +598,11 @@ class SFTTrainer:
                     self.optimizer.step(grad_scale=st)
                 self.scheduler.step()
                 self.engine.zero_grad()
+                if trace is not None:
+                    self._sync()
+                    trace.append((step + 1, round((time.time() - t_step) * 1e3, 2),
+                                  [tuple(c["input_ids"].shape) for c, _ in chunks],
+                                  sum(int(c["attention_mask"].sum()) for c, _ in chunks)))
                 step += 1
                 log_count += 1
                 self.state["global_step"] = step
@@ -494,10 +619,15 @@ class SFTTrainer:
                     self._log(logs)
                     log_loss.zero_()
                     log_count = 0
+                t_aux = time.time()
                 if a.eval_strategy == "steps" and self.eval_seqs and a.eval_steps and step % a.eval_steps == 0:
                     self.evaluate()
+                t_save = time.time()
                 if a.save_strategy == "steps" and a.save_steps and step % a.save_steps == 0:
                     self._save_checkpoint(step)
+                if trace is not None and time.time() - t_aux > 1e-3:
+                    trace.append((step, "eval", round((t_save - t_aux) * 1e3, 2), "save",
+                                  round((time.time() - t_save) * 1e3, 2), getattr(self, "_save_times", None)))
                 if step >= total:
                     done = True
                     break
@@ -511,6 +641,11 @@ class SFTTrainer:
         if self.device.type == "cuda":
             torch.cuda.synchronize()
         rt = time.time() - t0
+        if trace is not None:
+            with open(os.path.join(a.output_dir, "step_trace.jsonl"), "w") as f:
+                for row in trace:
+                    f.write(json.dumps(row) + "\n")
+            print(f"step trace: {len(trace)} rows -> {a.output_dir}/step_trace.jsonl", flush=True)
         train_loss = self._mean_across_ranks(tr_loss_sum / max(1, step - start_step))
         gsamples = nsamples * self.world
         metrics = {"train_runtime": round(rt, 4), "train_samples_per_second": round(gsamples / rt, 3),
@@ -525,6 +660,10 @@ class SFTTrainer:
         if self.tb is not None:
             self.tb.flush()
         return TrainOutput(step, train_loss, metrics)
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     def _mean_across_ranks(self, t: torch.Tensor) -> float:
         t = t.detach().float().reshape(1).clone()
@@ -559,7 +698,8 @@ class SFTTrainer:
         tot = torch.zeros(2, device=self.device, dtype=torch.float64)
         batches = self._batches(self.eval_seqs, self.args.per_device_eval_batch_size, 0, shuffle=False)
         if self._fuse_enabled():  # same token-weighted mean from fewer, larger forwards
-            batches = [cb for cb, _ in self._step_chunks(batches, list(range(len(batches))), True, weighted=False)]
+            batches = [cb for cb, _ in self._step_chunks(batches, list(range(len(batches))), True, weighted=False,
+                                                         max_tokens=self.args.eval_max_tokens)]
         with torch.no_grad():  # as HF's prediction_step: no saved activations, no fused CE gradient
             for cb in batches:
                 b = self._to_dev(cb)
@@ -571,6 +711,7 @@ class SFTTrainer:
                 tot[1] += n
         if self.world > 1:
             dist.all_reduce(tot)
+        tot = tot.cpu()  # the runtime covers the device work, not just its enqueueing
         rt = time.time() - t0
         m = {"eval_loss": float(tot[0] / tot[1].clamp_min(1)), "eval_runtime": round(rt, 4),
              "eval_samples_per_second": round(len(self.eval_seqs) / max(rt, 1e-9), 3),
@@ -602,7 +743,9 @@ class SFTTrainer:
         files on a background thread while training continues; full-model checkpoints are written
         synchronously. The previous write is always finished before a new one starts, before
         ``train`` returns and before a checkpoint is loaded."""
+        tm = [time.time()]
         self._finish_save()
+        tm.append(time.time())
         a = self.args
         d = os.path.join(a.output_dir, f"checkpoint-{step}")
         job = None
@@ -611,14 +754,23 @@ class SFTTrainer:
             try:
                 os.makedirs(d, exist_ok=True)
                 m = self._unwrapped()
-                files = {"optimizer.pt": _to_host(self.optimizer.state_dict()),
+                is_adapter = hasattr(m, "adapter_state_dict") and hasattr(m, "lora_modules")
+                snap = self._snapshot if self.device.type == "cuda" and is_adapter else None
+                if snap is not None:  # ONE pinned snapshot of optimizer state (+ adapters)
+                    host = snap.take({"o": self.optimizer.state_dict(),
+                                      "a": m.adapter_state_dict() if is_adapter else None})
+                else:
+                    host = {"o": _to_host(self.optimizer.state_dict()),
+                            "a": _to_host(m.adapter_state_dict()) if is_adapter else None}
+                tm.append(time.time())
+                files = {"optimizer.pt": host["o"],
                          "scheduler.pt": self.scheduler.state_dict(), "training_args.bin": a.to_dict()}
                 st = dict(self.state, train_batch_size=a.per_device_train_batch_size, max_steps=a.max_steps,
                           logging_steps=a.logging_steps, save_steps=a.save_steps, eval_steps=a.eval_steps)
                 st = json.loads(json.dumps(st))  # frozen copy: the live state keeps changing
                 adapter = None
-                if hasattr(m, "adapter_state_dict") and hasattr(m, "lora_modules"):
-                    adapter = _to_host(m.adapter_state_dict())
+                if is_adapter:
+                    adapter = host["a"]
                     m.save_adapter_config(d)
                     if hasattr(self.tokenizer, "save_pretrained"):
                         self.tokenizer.save_pretrained(d)
@@ -628,13 +780,15 @@ class SFTTrainer:
                 def job():
                     if adapter is not None:
                         from safetensors.torch import save_file
-                        save_file(adapter, os.path.join(d, "adapter_model.safetensors"))
+                        save_file(_HostSnapshot.materialize(adapter) if snap is not None else adapter,
+                                  os.path.join(d, "adapter_model.safetensors"))
                     for name, obj in files.items():
-                        torch.save(obj, os.path.join(d, name))
+                        torch.save(_HostSnapshot.materialize(obj) if snap is not None else obj, os.path.join(d, name))
                     with open(os.path.join(d, "trainer_state.json"), "w") as f:
                         json.dump(st, f, indent=2)
             except Exception as e:  # reported on every rank below, not raised ahead of the others
                 err, job = e, None
+        tm.append(time.time())
         try:
             os.makedirs(d, exist_ok=True)
             torch.save(_rng_snapshot(), os.path.join(d, f"rng_state_{self.rank}.pth"))
@@ -664,6 +818,8 @@ class SFTTrainer:
                     self._save_error = e
         if not use_async:
             self._finish_save()
+        tm.append(time.time())
+        self._save_times = [round((b - a_) * 1e3, 1) for a_, b in zip(tm[:-1], tm[1:])]  # step trace
 
     def _finish_save(self):
         """Complete the pending checkpoint: join the writer, rotate old checkpoints, run callbacks.

@@ -157,7 +157,7 @@ def test_padding_free_pack_layout(tmp_path):
     m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
     rows = [{"text": "abc " * (3 + i)} for i in range(8)]
     tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path), per_device_train_batch_size=2, gradient_accumulation_steps=4,
-                                 fuse_accumulation=True, fuse_pad_multiple=64, padding_free=True), train_dataset=rows)
+                                 fuse_accumulation=True, pack_multiple=64, padding_free=True), train_dataset=rows)
     batches = tr._batches(tr.train_seqs, 2, 0, shuffle=False)
     (cb, w), = tr._step_chunks(batches, list(range(4)), True)
     real = sum(len(s) for s in tr.train_seqs)
@@ -168,3 +168,30 @@ def test_padding_free_pack_layout(tmp_path):
     for a, b in zip([0] + bounds.tolist()[:-1], bounds.tolist()):
         valid[a:b - 1] = cb["labels"][0, a + 1:b] != -100  # targets inside each sequence only
     assert abs(float((w[0] * valid).sum()) - 1.0) < 1e-6
+
+
+def test_padding_free_groups_by_real_tokens(tmp_path):
+    """Packed rows hold whole micro-batches while their real tokens fit pack_max_tokens; the
+    weights over all rows of the step still sum to 1."""
+    import torch
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
+    rows = [{"text": "abc " * (3 + i)} for i in range(8)]
+    tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path), per_device_train_batch_size=2, gradient_accumulation_steps=4,
+                                 max_seq_length=64, fuse_accumulation=True, pack_multiple=16, pack_max_tokens=70,
+                                 padding_free=True), train_dataset=rows)
+    batches = tr._batches(tr.train_seqs, 2, 0, shuffle=False)
+    chunks = tr._step_chunks(batches, list(range(4)), True)
+    assert len(chunks) > 1
+    tot = 0.0
+    for cb, w in chunks:
+        real = int(cb["attention_mask"].sum())
+        assert real <= 70 or len(cb["lengths"]) <= 3      # one micro-batch (2 rows + filler) may exceed
+        assert cb["input_ids"].shape[1] % 16 == 0
+        bounds = torch.tensor(cb["lengths"]).cumsum(0).tolist()
+        valid = torch.zeros(cb["input_ids"].shape[1], dtype=torch.bool)
+        for a, b in zip([0] + bounds[:-1], bounds):
+            valid[a:b - 1] = cb["labels"][0, a + 1:b] != -100
+        tot += float((w[0] * valid).sum())
+    assert abs(tot - 1.0) < 1e-5
