@@ -29,10 +29,13 @@ def enable_tuned_gemms(path: str | os.PathLike | None = None) -> bool:
     p = Path(path or os.environ.get("GRT_TUNED_GEMM_FILE") or RESULTS)
     if not p.exists():
         return False
+    rec = os.environ.get("GRT_TUNED_GEMM_RECORD_UNTUNED")  # path: log every GEMM shape the table misses
+    if rec:
+        os.environ["PYTORCH_TUNABLEOP_UNTUNED_FILENAME"] = rec
     tun = torch.cuda.tunable
     tun.enable(True)
     tun.tuning_enable(False)
-    tun.record_untuned_enable(False)
+    tun.record_untuned_enable(bool(rec))
     ok = bool(tun.read_file(str(p)))
     _enabled = ok
     return ok
