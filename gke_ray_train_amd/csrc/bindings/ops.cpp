@@ -982,6 +982,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"), py::arg("causal"),
         py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("rope_cos") = py::none(),
         py::arg("rope_sin") = py::none(), py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0);
+  m.def("attn_set_schedule", &grt::attn_set_schedule,
+        "bf16 attention workgroup schedule: 0 = one block per workgroup, 1 = causal pairs, XCD-grouped");
+  m.def("attn_get_schedule", &grt::attn_get_schedule);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);

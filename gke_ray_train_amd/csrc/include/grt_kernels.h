@@ -149,7 +149,12 @@ struct AttnParams {
   uint32_t drop_seed;
   uint32_t drop_thresh;
   float drop_scale;
+  // workgroup schedule of the bf16 q-block kernels (forward, dQ), set by the launchers from
+  // attn_set_schedule(): 0 = one q-block per workgroup, heaviest first; 1 = causal pairs
+  int sched;
 };
+void attn_set_schedule(int s);
+int attn_get_schedule();
 void attn_fwd(const AttnParams& p, hipStream_t s);
 struct AttnBwdParams {
   AttnParams f;

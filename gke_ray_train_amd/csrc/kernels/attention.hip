@@ -134,6 +134,38 @@ constexpr int F3M = 128, F3N = 32, F3NT = 256, F3NSLOT = 4;
 constexpr int F3IMG = F3N * D * 2;   // 8 KiB
 constexpr int F3SLOT = 2 * F3IMG;    // K, V
 
+// Workgroup -> (batch*head, q-blocks) of the q-block kernels (forward, dQ; grid: q_grid()).
+// sched 0: one q-block per workgroup, heaviest (causal) first.
+// sched 1: causal pairs — heavy block nqb-1-j then light block j in one workgroup (equal work per
+//   workgroup: no tail of heavy blocks), and the pairs of one (batch, head), then of the heads of one
+//   GQA group, dealt to consecutive workgroups of ONE XCD (bijective remap, cdna_hip_programming.md
+//   §5 "XCD swizzle must be bijective"): a head's workgroups stream its K / V tiles together, so all
+//   but the first read of a tile hit that XCD's L2 instead of going to HBM.
+struct QJobs {
+  int bh;
+  int blk[2];  // -1 = none
+};
+__device__ __forceinline__ QJobs q_jobs(int sched, int nqb, int BH) {
+  QJobs j;
+  if (sched == 1) {
+    const int npair = (nqb + 1) >> 1, nwg = BH * npair;
+    const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    j.bh = L / npair;
+    const int pr = L % npair;
+    j.blk[0] = nqb - 1 - pr;
+    j.blk[1] = pr != nqb - 1 - pr ? pr : -1;
+  } else {
+    j.bh = blockIdx.x % BH;
+    j.blk[0] = nqb - 1 - (int)(blockIdx.x / BH);
+    j.blk[1] = -1;
+  }
+  return j;
+}
+__host__ __device__ inline unsigned q_grid(int sched, int nqb, int BH) {
+  return (unsigned)(sched == 1 ? BH * ((nqb + 1) / 2) : BH * nqb);
+}
+
 template <bool DROP>
 __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   __shared__ __attribute__((aligned(16))) char smem[F3NSLOT * F3SLOT];
@@ -142,17 +174,24 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   const int g = lane >> 4, l16 = lane & 15;
   const int nqb = (p.Sq + F3M - 1) / F3M;  // grid: the longest sequence
   const int BH = p.B * p.Hq;
-  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) blocks first
-  const int bh = blockIdx.x % BH;
+  const QJobs jobs = q_jobs(p.sched, nqb, BH);
+  const int bh = jobs.bh;
   const int b = bh / p.Hq, hq = bh % p.Hq;
   const int hkv = hq / (p.Hq / p.Hkv);
-  GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && qblk >= 0);
+  GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && jobs.blk[0] >= 0 && jobs.blk[0] < nqb);
+  for (int jb = 0; jb < 2; ++jb) {
+  const int qblk = jobs.blk[jb];
+  if (qblk < 0) break;
+  if (jb) {  // every wave is done with the ring (LDS reads and its own DMAs) before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
   int Sq = p.Sq, Sk = p.Sk;
   int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
   if (p.cu_seqlens) {
     tok0 = p.cu_seqlens[b];
     Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
-    if (qblk * F3M >= Sq) return;  // workgroup-uniform: the sequence is shorter than the longest
+    if (qblk * F3M >= Sq) continue;  // workgroup-uniform: the sequence is shorter than the longest
   }
   const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
   const int off = Sk - Sq;  // bottom-right aligned causal mask
@@ -328,6 +367,7 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
     if (h == 0 && p.lse)
       p.lse[((int64_t)b * p.Hq + hq) * p.Sq + myq] = lt > 0.f ? (m + __log2f(lt)) * kLn2 : INFINITY;
   }
+  }  // q-blocks of this workgroup
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -417,16 +457,33 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
   const int g = lane >> 4, l16 = lane & 15;
   const int BHk = p.B * p.Hkv;
-  const int kblk = (int)(blockIdx.x / BHk);  // causal: heaviest (earliest) key blocks first
-  const int bhk = blockIdx.x % BHk;
+  const int nkb = (p.Sk + K2N - 1) / K2N;
+  // sched 0: one key block per workgroup, heaviest (earliest, causal) first; sched 1: key blocks
+  // paired light + heavy, the pairs of one (batch, kv head) on one XCD (see q_jobs)
+  QJobs jobs;
+  if (p.sched == 1) {
+    jobs = q_jobs(1, nkb, BHk);
+  } else {
+    jobs.bh = blockIdx.x % BHk;
+    jobs.blk[0] = (int)(blockIdx.x / BHk);
+    jobs.blk[1] = -1;
+  }
+  const int bhk = jobs.bh;
   const int b = bhk / p.Hkv, hkv = bhk % p.Hkv;
   const int grp = p.Hq / p.Hkv;
+  for (int jb = 0; jb < 2; ++jb) {
+  const int kblk = jobs.blk[jb];
+  if (kblk < 0) break;
+  if (jb) {  // every wave is done with the ring before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
   int Sq = p.Sq, Sk = p.Sk;
   int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
   if (p.cu_seqlens) {
     tok0 = p.cu_seqlens[b];
     Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
-    if (kblk * K2N >= Sk) return;  // workgroup-uniform: the sequence is shorter than the longest
+    if (kblk * K2N >= Sk) continue;  // workgroup-uniform: the sequence is shorter than the longest
   }
   GRT_DEVICE_CHECK(grp * p.Hkv == p.Hq && kblk * K2N < Sk);
   const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
@@ -647,6 +704,7 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
         *reinterpret_cast<bf16x4*>(dV + db * 32 + 8 * gg + 4 * h) = v;
       }
   }
+  }  // key blocks of this workgroup
 }
 
 // dQ: the forward's mapping (32 query rows per wave on the MFMA lane, 4 waves = 128 rows) over
@@ -666,16 +724,24 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
   const int g = lane >> 4, l16 = lane & 15;
   const int nqb = (p.Sq + Q2M - 1) / Q2M;  // grid: the longest sequence
   const int BH = p.B * p.Hq;
-  const int qblk = nqb - 1 - (int)(blockIdx.x / BH);  // heaviest (causal) blocks first
-  const int bh = blockIdx.x % BH;
+  const QJobs jobs = q_jobs(p.sched, nqb, BH);  // see the forward
+  const int bh = jobs.bh;
   const int b = bh / p.Hq, hq = bh % p.Hq;
   const int hkv = hq / (p.Hq / p.Hkv);
+  GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && jobs.blk[0] >= 0 && jobs.blk[0] < nqb);
+  for (int jb = 0; jb < 2; ++jb) {
+  const int qblk = jobs.blk[jb];
+  if (qblk < 0) break;
+  if (jb) {  // every wave is done with the ring before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
   int Sq = p.Sq, Sk = p.Sk;
   int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
   if (p.cu_seqlens) {
     tok0 = p.cu_seqlens[b];
     Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
-    if (qblk * Q2M >= Sq) return;  // workgroup-uniform: the sequence is shorter than the longest
+    if (qblk * Q2M >= Sq) continue;  // workgroup-uniform: the sequence is shorter than the longest
   }
   const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
   const int off = Sk - Sq;
@@ -833,12 +899,29 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
         }
     }
   }
+  }  // q-blocks of this workgroup
 }
 
 }  // namespace
 
-void attn_fwd(const AttnParams& p, hipStream_t s) {
-  const dim3 grid((unsigned)(((p.Sq + F3M - 1) / F3M) * p.B * p.Hq));
+namespace {
+int g_sched = -1;  // -1: not set yet (GRT_ATTN_SCHED, default 1)
+int sched_now() {
+  if (g_sched < 0) {
+    const char* e = getenv("GRT_ATTN_SCHED");
+    g_sched = e ? atoi(e) : 1;
+  }
+  return g_sched;
+}
+}  // namespace
+
+void attn_set_schedule(int s) { g_sched = s; }
+int attn_get_schedule() { return sched_now(); }
+
+void attn_fwd(const AttnParams& p0, hipStream_t s) {
+  AttnParams p = p0;
+  p.sched = sched_now();
+  const dim3 grid(q_grid(p.sched, (p.Sq + F3M - 1) / F3M, p.B * p.Hq));
   if (p.drop_thresh) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(F3NT), 0, s, p);
   else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(F3NT), 0, s, p);
 }
@@ -848,12 +931,14 @@ int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
   return 2 * (int64_t)B * Hq * sq_pad(Sq);  // delta and lse2, rows padded to 32
 }
 
-void attn_bwd(const AttnBwdParams& p, hipStream_t s) {
+void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
+  AttnBwdParams p = p0;
+  p.f.sched = sched_now();
   const int64_t rows = (int64_t)p.f.B * p.f.Hq * sq_pad(p.f.Sq);
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
   const int nkb = (p.f.Sk + K2N - 1) / K2N;
   const int nqb = (p.f.Sq + Q2M - 1) / Q2M;
-  const dim3 g1((unsigned)(nkb * p.f.B * p.f.Hkv)), g2((unsigned)(nqb * p.f.B * p.f.Hq));
+  const dim3 g1(q_grid(p.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(p.f.sched, nqb, p.f.B * p.f.Hq));
   if (p.f.drop_thresh) {
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, p);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(Q2NT), 0, s, p);

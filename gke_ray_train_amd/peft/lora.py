@@ -81,12 +81,34 @@ def _base_weight(base: nn.Module) -> torch.Tensor:
     return base.dequantize() if isinstance(base, NF4Linear) else base.weight
 
 
-def _base_input_grad(base: nn.Module, dy2: torch.Tensor) -> torch.Tensor:
+def _base_input_grad(base: nn.Module, dy2: torch.Tensor, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dX of the frozen base projection: TN GEMM on a transposed weight (cached for a bf16 base;
-    for NF4 the dequantising kernel writes W^T directly)."""
+    for NF4 the dequantising kernel writes W^T directly). With ``acc`` the GEMM adds onto it in its
+    epilogue (beta = 1) and returns it."""
     if isinstance(base, NF4Linear):
-        return base.input_grad(dy2)
+        return base.input_grad(dy2, acc)
+    if acc is not None:
+        from ..ops.linear import transposed_weight
+        wt = transposed_weight(base.weight) if dy2.is_cuda and dy2.dtype == torch.bfloat16 else None
+        return acc.addmm_(dy2, wt.t()) if wt is not None else acc.addmm_(dy2, base.weight)
     return input_grad(dy2, base.weight)
+
+
+# The adapter's dX term first, then the base dX GEMM accumulating onto it in its epilogue (beta = 1):
+# the adapter kernel only WRITES its [M, K] term, and the GEMM's read of it overlaps its MFMA work,
+# instead of a separate read-modify-write pass over dX after the GEMM. GRT_LORA_DX_EPI=0 -> RMW.
+_LORA_DX_EPI = os.environ.get("GRT_LORA_DX_EPI", "1") != "0"
+
+
+def _adapter_then_base_dx(ctx, C, base, dy2, g, acat):
+    """dX = dY W + drop'(g A) as [adapter kernel writes T] + [base GEMM T += dY W]; None when the
+    adapter kernel does not apply (the caller then runs the GEMM + read-modify-write path)."""
+    if not (_LORA_DX_EPI and _LORA_DX and g.is_cuda and g.dtype == acat.dtype == dy2.dtype == torch.bfloat16):
+        return None
+    t = torch.empty(g.shape[0], acat.shape[1], device=dy2.device, dtype=dy2.dtype)
+    if not C.lora_dx(g, acat.t().contiguous(), t, ctx.p, ctx.seed, ctx.offset, False):
+        return None
+    return _base_input_grad(base, dy2, t)
 
 
 # LoRA gradients written by the adapter GEMMs straight into the data-parallel gradient slots
@@ -180,8 +202,6 @@ class _LoraFn(torch.autograd.Function):
         if dy2.dtype != acat.dtype:
             dy2 = dy2.to(acat.dtype)
         dx = None
-        if ctx.needs_input_grad[0]:
-            dx = _base_input_grad(ctx.base, dy2)           # base dX (frozen weight)
         # g = dL/dh = s * dY_i B_i per target, into its column block (alpha = s, no scaled copy of B)
         g = torch.zeros(dy2.shape[0], r * k, device=dy2.device, dtype=dy2.dtype)
         dBs: List[Optional[torch.Tensor]] = [None] * k
@@ -220,7 +240,10 @@ class _LoraFn(torch.autograd.Function):
                     sl.notify(As[i])
                 else:
                     dAs[i] = rows
-        if dx is not None:
+        if ctx.needs_input_grad[0]:
+            dx = _adapter_then_base_dx(ctx, C, ctx.base, dy2, g, acat)
+        if ctx.needs_input_grad[0] and dx is None:
+            dx = _base_input_grad(ctx.base, dy2)           # base dX (frozen weight)
             # dx += drop'(g A): one read-modify-write of dx (lora.hip), else GEMM + dropout backward
             bf16 = g.dtype == acat.dtype == dx.dtype == torch.bfloat16 and g.is_cuda
             if not (_LORA_DX and bf16 and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
@@ -228,6 +251,7 @@ class _LoraFn(torch.autograd.Function):
                     C.dropout_bwd_seeded(g @ acat, dx, ctx.p, ctx.seed, ctx.offset, True)
                 else:
                     dx.addmm_(g, acat)
+        if dx is not None:
             dx = dx.view(ctx.xshape)
         return (dx, None, None, None, None, None, None, None, *dAs, *dBs)
 
@@ -274,7 +298,7 @@ class _LoraKcatFn(torch.autograd.Function):
         dy2 = dy.reshape(M, -1)
         if dy2.dtype != hc.dtype:
             dy2 = dy2.to(hc.dtype)
-        dx = _base_input_grad(mod.base, dy2) if ctx.needs_input_grad[0] else None
+        dx = None
         g = torch.zeros(M, r * k, device=dy2.device, dtype=dy2.dtype)  # dL/dh (unscaled h) = s dY_i B_i
         dBs: List[Optional[torch.Tensor]] = [None] * k
         for j, i in enumerate(order):
@@ -289,7 +313,10 @@ class _LoraKcatFn(torch.autograd.Function):
             else:
                 dBs[i] = torch.mm(dyi.t(), hj)
         dAs = _lora_dA(g, xd, As, order, r)
-        if dx is not None:
+        if ctx.needs_input_grad[0]:
+            dx = _adapter_then_base_dx(ctx, C, mod.base, dy2, g, acat)
+        if ctx.needs_input_grad[0] and dx is None:
+            dx = _base_input_grad(mod.base, dy2)
             bf16 = g.dtype == acat.dtype == dx.dtype == torch.bfloat16
             if not (_LORA_DX and bf16 and C.lora_dx(g, acat.t().contiguous(), dx, ctx.p, ctx.seed, ctx.offset, True)):
                 if ctx.p > 0:

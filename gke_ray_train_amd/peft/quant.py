@@ -125,9 +125,10 @@ class NF4Linear(nn.Module):
             return c[1]
         return self._dequant()
 
-    def input_grad(self, dy: torch.Tensor) -> torch.Tensor:
+    def input_grad(self, dy: torch.Tensor, acc: Optional[torch.Tensor] = None) -> torch.Tensor:
         """dX = dY W: on MI355X the HIP kernel dequantises straight into W^T so the GEMM runs in the
-        TN layout (ops.linear.input_grad); elsewhere dY @ W."""
+        TN layout (ops.linear.input_grad); elsewhere dY @ W. With ``acc``: acc += dY W (the GEMM's
+        beta = 1 epilogue), returned."""
         if getattr(self, "_cache_on", False):
             c = getattr(self, "_wt_cache", None)
             if c is None or c[0] != self._cache_key():
@@ -135,6 +136,8 @@ class NF4Linear(nn.Module):
             wt = c[1]
         else:
             wt = self._dequant_t() if dy.is_cuda else None
+        if acc is not None:
+            return acc.addmm_(dy, wt.t()) if wt is not None else acc.addmm_(dy, self.dequantize())
         if wt is not None:
             return F.linear(dy, wt)
         return dy @ self.dequantize()
