@@ -143,7 +143,7 @@ constexpr int F3SLOT = 2 * F3IMG;    // K, V
 //   but the first read of a tile hit that XCD's L2 instead of going to HBM.
 struct QJobs {
   int bh;
-  int blk[2];  // -1 = none
+  int blk0, blk1;  // blk1 = -1: none (scalars, not an array: a runtime-indexed array is promoted to LDS)
 };
 __device__ __forceinline__ QJobs q_jobs(int sched, int nqb, int BH) {
   QJobs j;
@@ -153,12 +153,12 @@ __device__ __forceinline__ QJobs q_jobs(int sched, int nqb, int BH) {
     const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
     j.bh = L / npair;
     const int pr = L % npair;
-    j.blk[0] = nqb - 1 - pr;
-    j.blk[1] = pr != nqb - 1 - pr ? pr : -1;
+    j.blk0 = nqb - 1 - pr;
+    j.blk1 = pr != nqb - 1 - pr ? pr : -1;
   } else {
     j.bh = blockIdx.x % BH;
-    j.blk[0] = nqb - 1 - (int)(blockIdx.x / BH);
-    j.blk[1] = -1;
+    j.blk0 = nqb - 1 - (int)(blockIdx.x / BH);
+    j.blk1 = -1;
   }
   return j;
 }
@@ -178,20 +178,16 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   const int bh = jobs.bh;
   const int b = bh / p.Hq, hq = bh % p.Hq;
   const int hkv = hq / (p.Hq / p.Hkv);
-  GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && jobs.blk[0] >= 0 && jobs.blk[0] < nqb);
-  for (int jb = 0; jb < 2; ++jb) {
-  const int qblk = jobs.blk[jb];
-  if (qblk < 0) break;
-  if (jb) {  // every wave is done with the ring (LDS reads and its own DMAs) before it is refilled
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
+  GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && jobs.blk0 >= 0 && jobs.blk0 < nqb);
+  // one call per block of this workgroup; inlined twice, so the second block's registers are
+  // allocated independently (a loop over the two blocks spilled the dQ kernel)
+  auto run_block = [&](const int qblk) {
   int Sq = p.Sq, Sk = p.Sk;
   int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
   if (p.cu_seqlens) {
     tok0 = p.cu_seqlens[b];
     Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
-    if (qblk * F3M >= Sq) continue;  // workgroup-uniform: the sequence is shorter than the longest
+    if (qblk * F3M >= Sq) return;  // workgroup-uniform: the sequence is shorter than the longest
   }
   const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
   const int off = Sk - Sq;  // bottom-right aligned causal mask
@@ -367,7 +363,13 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
     if (h == 0 && p.lse)
       p.lse[((int64_t)b * p.Hq + hq) * p.Sq + myq] = lt > 0.f ? (m + __log2f(lt)) * kLn2 : INFINITY;
   }
-  }  // q-blocks of this workgroup
+  };
+  run_block(jobs.blk0);
+  if (jobs.blk1 >= 0) {  // every wave is done with the ring (LDS reads, its own DMAs) before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    run_block(jobs.blk1);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -465,25 +467,21 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
     jobs = q_jobs(1, nkb, BHk);
   } else {
     jobs.bh = blockIdx.x % BHk;
-    jobs.blk[0] = (int)(blockIdx.x / BHk);
-    jobs.blk[1] = -1;
+    jobs.blk0 = (int)(blockIdx.x / BHk);
+    jobs.blk1 = -1;
   }
   const int bhk = jobs.bh;
   const int b = bhk / p.Hkv, hkv = bhk % p.Hkv;
   const int grp = p.Hq / p.Hkv;
-  for (int jb = 0; jb < 2; ++jb) {
-  const int kblk = jobs.blk[jb];
-  if (kblk < 0) break;
-  if (jb) {  // every wave is done with the ring before it is refilled
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
+  // one call per block of this workgroup; inlined twice, so the second block's registers are
+  // allocated independently (a loop over the two blocks spilled the dQ kernel)
+  auto run_block = [&](const int kblk) {
   int Sq = p.Sq, Sk = p.Sk;
   int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
   if (p.cu_seqlens) {
     tok0 = p.cu_seqlens[b];
     Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
-    if (kblk * K2N >= Sk) continue;  // workgroup-uniform: the sequence is shorter than the longest
+    if (kblk * K2N >= Sk) return;  // workgroup-uniform: the sequence is shorter than the longest
   }
   GRT_DEVICE_CHECK(grp * p.Hkv == p.Hq && kblk * K2N < Sk);
   const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
@@ -704,7 +702,13 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
         *reinterpret_cast<bf16x4*>(dV + db * 32 + 8 * gg + 4 * h) = v;
       }
   }
-  }  // key blocks of this workgroup
+  };
+  run_block(jobs.blk0);
+  if (jobs.blk1 >= 0) {  // every wave is done with the ring (LDS reads, its own DMAs) before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    run_block(jobs.blk1);
+  }
 }
 
 // dQ: the forward's mapping (32 query rows per wave on the MFMA lane, 4 waves = 128 rows) over
@@ -728,20 +732,16 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
   const int bh = jobs.bh;
   const int b = bh / p.Hq, hq = bh % p.Hq;
   const int hkv = hq / (p.Hq / p.Hkv);
-  GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && jobs.blk[0] >= 0 && jobs.blk[0] < nqb);
-  for (int jb = 0; jb < 2; ++jb) {
-  const int qblk = jobs.blk[jb];
-  if (qblk < 0) break;
-  if (jb) {  // every wave is done with the ring before it is refilled
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  }
+  GRT_DEVICE_CHECK(b < p.B && hkv < p.Hkv && jobs.blk0 >= 0 && jobs.blk0 < nqb);
+  // one call per block of this workgroup; inlined twice, so the second block's registers are
+  // allocated independently (a loop over the two blocks spilled the dQ kernel)
+  auto run_block = [&](const int qblk) {
   int Sq = p.Sq, Sk = p.Sk;
   int64_t tok0 = 0;  // padding-free packing: this sequence's first token row
   if (p.cu_seqlens) {
     tok0 = p.cu_seqlens[b];
     Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
-    if (qblk * Q2M >= Sq) continue;  // workgroup-uniform: the sequence is shorter than the longest
+    if (qblk * Q2M >= Sq) return;  // workgroup-uniform: the sequence is shorter than the longest
   }
   const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
   const int off = Sk - Sq;
@@ -899,7 +899,13 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
         }
     }
   }
-  }  // q-blocks of this workgroup
+  };
+  run_block(jobs.blk0);
+  if (jobs.blk1 >= 0) {  // every wave is done with the ring (LDS reads, its own DMAs) before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    run_block(jobs.blk1);
+  }
 }
 
 }  // namespace
