@@ -149,8 +149,8 @@ struct AttnParams {
   uint32_t drop_seed;
   uint32_t drop_thresh;
   float drop_scale;
-  // workgroup schedule of the bf16 q-block kernels (forward, dQ), set by the launchers from
-  // attn_set_schedule(): 0 = one q-block per workgroup, heaviest first; 1 = causal pairs
+  // workgroup schedule of one bf16 kernel, set by the launchers from the attn_set_schedule() mask
+  // (1 = forward, 2 = dQ, 4 = dK / dV): 0 = one block per workgroup, heaviest first; 1 = causal pairs
   int sched;
 };
 void attn_set_schedule(int s);

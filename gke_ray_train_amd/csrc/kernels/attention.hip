@@ -911,7 +911,10 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
 }  // namespace
 
 namespace {
-int g_sched = -1;  // -1: not set yet (GRT_ATTN_SCHED, default 1)
+// bit mask of the kernels that use the causal-pair schedule: 1 = forward, 2 = dQ, 4 = dK / dV
+// (-1: not set yet -> GRT_ATTN_SCHED, default 1: forward -8 % at B8 S1024 H32, the backward kernels
+// measured neutral-to-slower with it: profiles/r3_attn_schedule.md)
+int g_sched = -1;
 int sched_now() {
   if (g_sched < 0) {
     const char* e = getenv("GRT_ATTN_SCHED");
@@ -926,7 +929,7 @@ int attn_get_schedule() { return sched_now(); }
 
 void attn_fwd(const AttnParams& p0, hipStream_t s) {
   AttnParams p = p0;
-  p.sched = sched_now();
+  p.sched = sched_now() & 1;
   const dim3 grid(q_grid(p.sched, (p.Sq + F3M - 1) / F3M, p.B * p.Hq));
   if (p.drop_thresh) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(F3NT), 0, s, p);
   else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(F3NT), 0, s, p);
@@ -939,18 +942,21 @@ int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
 
 void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   AttnBwdParams p = p0;
-  p.f.sched = sched_now();
+  const int sc = sched_now();
   const int64_t rows = (int64_t)p.f.B * p.f.Hq * sq_pad(p.f.Sq);
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
   const int nkb = (p.f.Sk + K2N - 1) / K2N;
   const int nqb = (p.f.Sq + Q2M - 1) / Q2M;
-  const dim3 g1(q_grid(p.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(p.f.sched, nqb, p.f.B * p.f.Hq));
+  AttnBwdParams pk = p, pq = p;
+  pk.f.sched = (sc >> 2) & 1;
+  pq.f.sched = (sc >> 1) & 1;
+  const dim3 g1(q_grid(pk.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(pq.f.sched, nqb, p.f.B * p.f.Hq));
   if (p.f.drop_thresh) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, p);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(Q2NT), 0, s, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, pk);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(Q2NT), 0, s, pq);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(K2NT), 0, s, p);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(Q2NT), 0, s, p);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(K2NT), 0, s, pk);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(Q2NT), 0, s, pq);
   }
 }
 
