@@ -37,6 +37,7 @@
 #include <stdlib.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "grt_common.h"
 #include "grt_kernels.h"
@@ -124,6 +125,21 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 }
 __device__ __forceinline__ int img_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
+// f(integral_constant<int, I>) for I in the sequence, unrolled at compile time (ring slots and
+// register-set parity stay compile-time constants in the pipelined loops)
+template <class F, int... I>
+__device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+// s_waitcnt vmcnt(4 * tiles): the DMA of `tiles` 4-instruction tiles may stay in flight
+__device__ __forceinline__ void wait_tiles4(int tiles) {
+  if (tiles >= 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if (tiles == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (tiles == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (tiles == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // ---------------------------------------------------------------------------------------------
 // Forward: 4 waves x 32 query rows, 32-key K / V tiles through the ring, 16 MFMAs per tile and
 // wave, two workgroups per CU. (A 256-row / 8-wave workgroup, halving the K / V bytes per FLOP,
@@ -166,9 +182,10 @@ __host__ __device__ inline unsigned q_grid(int sched, int nqb, int BH) {
   return (unsigned)(sched == 1 ? BH * ((nqb + 1) / 2) : BH * nqb);
 }
 
-template <bool DROP>
+// NS: ring slots (4: 64 KiB; 5: 80 KiB = half the CU's LDS, the most two workgroups per CU allow)
+template <bool DROP, int NS>
 __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
-  __shared__ __attribute__((aligned(16))) char smem[F3NSLOT * F3SLOT];
+  __shared__ __attribute__((aligned(16))) char smem[NS * F3SLOT];
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, l16 = lane & 15;
@@ -223,11 +240,7 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
     lds_dma16(K + k1r * p.k_ss + ch1 * 8, dst + 1024);
     lds_dma16(Vg + k1r * p.v_ss + ch1 * 8, dst + F3IMG + 1024);
   };
-  auto wait_dma = [&](int pending_tiles) {  // 4 DMA instructions per tile
-    if (pending_tiles >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (pending_tiles == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
+  auto wait_dma = [&](int pending_tiles) { wait_tiles4(pending_tiles); };  // 4 DMA instructions per tile
   // S^T = K Q^T of the tile in slot SL; the 8 K-row fragments are read into registers before the
   // MFMA chain so the reads are in flight together (not one LDS round trip per MFMA)
   auto qk = [&](auto slot_c) {
@@ -270,9 +283,9 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   auto step = [&](int t, auto slot_c, f32x16& s_c, f32x16& s_n) {
     constexpr int SL = decltype(slot_c)::value;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (t + 1 < nt) wait_dma(min(nt, t + F3NSLOT - 1) - (t + 2));
+    if (t + 1 < nt) wait_dma(min(nt, t + NS - 1) - (t + 2));
     __builtin_amdgcn_s_barrier();
-    if (t + F3NSLOT - 1 < nt) dma_tile(t + F3NSLOT - 1, (uint32_t)(((SL + F3NSLOT - 1) % F3NSLOT) * F3SLOT));
+    if (t + NS - 1 < nt) dma_tile(t + NS - 1, (uint32_t)(((SL + NS - 1) % NS) * F3SLOT));
 
     apply_mask(t, s_c);
     float mx = fmaxf(s_c[0], s_c[1]);
@@ -289,7 +302,7 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
     }
     const float msub = m == -INFINITY ? 0.f : m;
 
-    s_n = qk(std::integral_constant<int, (SL + 1) % F3NSLOT>{});  // past the end: dropped
+    s_n = qk(std::integral_constant<int, (SL + 1) % NS>{});  // past the end: dropped
     float rs = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -325,25 +338,21 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   };
 
   if (nt > 0) {
-    const int pre = min(nt, F3NSLOT - 1);
+    const int pre = min(nt, NS - 1);
     for (int t = 0; t < pre; ++t) dma_tile(t, (uint32_t)(t * F3SLOT));
     wait_dma(pre - 1);
     __builtin_amdgcn_s_barrier();
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    using I3 = std::integral_constant<int, 3>;
-    f32x16 sA = qk(I0{}), sB;
+    // unrolled over whole ring revolutions with an even step count (slot and S register set static)
+    constexpr int UNR = NS % 2 == 0 ? NS : 2 * NS;
+    f32x16 sA = qk(std::integral_constant<int, 0>{}), sB;
+    auto step_i = [&](int t0, auto i_c) {
+      constexpr int I = decltype(i_c)::value;
+      if constexpr (I & 1) step(t0 + I, std::integral_constant<int, I % NS>{}, sB, sA);
+      else step(t0 + I, std::integral_constant<int, I % NS>{}, sA, sB);
+    };
     int t = 0;
-    for (; t + F3NSLOT <= nt; t += F3NSLOT) {
-      step(t, I0{}, sA, sB);
-      step(t + 1, I1{}, sB, sA);
-      step(t + 2, I2{}, sA, sB);
-      step(t + 3, I3{}, sB, sA);
-    }
-    if (t < nt) step(t, I0{}, sA, sB);
-    if (t + 1 < nt) step(t + 1, I1{}, sB, sA);
-    if (t + 2 < nt) step(t + 2, I2{}, sA, sB);
+    for (; t + UNR <= nt; t += UNR) static_for([&](auto i_c) { step_i(t, i_c); }, std::make_integer_sequence<int, UNR>{});
+    static_for([&](auto i_c) { if (t + decltype(i_c)::value < nt) step_i(t, i_c); }, std::make_integer_sequence<int, UNR - 1>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -931,8 +940,9 @@ void attn_fwd(const AttnParams& p0, hipStream_t s) {
   AttnParams p = p0;
   p.sched = sched_now() & 1;
   const dim3 grid(q_grid(p.sched, (p.Sq + F3M - 1) / F3M, p.B * p.Hq));
-  if (p.drop_thresh) hipLaunchKernelGGL(attn_fwd_kernel<true>, grid, dim3(F3NT), 0, s, p);
-  else hipLaunchKernelGGL(attn_fwd_kernel<false>, grid, dim3(F3NT), 0, s, p);
+  // (a 5-slot ring, 3 tiles in flight, spills 41 VGPRs with its 10-step unroll: not instantiated)
+  if (p.drop_thresh) hipLaunchKernelGGL((attn_fwd_kernel<true, F3NSLOT>), grid, dim3(F3NT), 0, s, p);
+  else hipLaunchKernelGGL((attn_fwd_kernel<false, F3NSLOT>), grid, dim3(F3NT), 0, s, p);
 }
 
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
