@@ -203,13 +203,14 @@ class _LoraFn(torch.autograd.Function):
             dy2 = dy2.to(acat.dtype)
         dx = None
         # g = dL/dh = s * dY_i B_i per target, into its column block (alpha = s, no scaled copy of B)
-        g = torch.zeros(dy2.shape[0], r * k, device=dy2.device, dtype=dy2.dtype)
+        # every column block of g is written by its GEMM with beta = 0 (no zero fill, C not read)
+        g = torch.empty(dy2.shape[0], r * k, device=dy2.device, dtype=dy2.dtype)
         dBs: List[Optional[torch.Tensor]] = [None] * k
         for j, i in enumerate(order):
             off, n = spec[i]
             dyi = dy2[:, off:off + n]
             hj = h[:, j * r:(j + 1) * r]
-            g[:, j * r:(j + 1) * r].addmm_(dyi, Bs[i], alpha=s)
+            g[:, j * r:(j + 1) * r].addmm_(dyi, Bs[i], beta=0.0, alpha=s)
             sl = _slot_of(Bs[i])
             if sl is not None:                               # dB_i = s dY_i^T h_i into the slot
                 sl.write(lambda v: v.addmm_(dyi.t(), hj, beta=0.0, alpha=s), lambda v: v.addmm_(dyi.t(), hj, alpha=s))
@@ -299,13 +300,13 @@ class _LoraKcatFn(torch.autograd.Function):
         if dy2.dtype != hc.dtype:
             dy2 = dy2.to(hc.dtype)
         dx = None
-        g = torch.zeros(M, r * k, device=dy2.device, dtype=dy2.dtype)  # dL/dh (unscaled h) = s dY_i B_i
+        g = torch.empty(M, r * k, device=dy2.device, dtype=dy2.dtype)  # dL/dh (unscaled h) = s dY_i B_i
         dBs: List[Optional[torch.Tensor]] = [None] * k
         for j, i in enumerate(order):
             off, n, _ = mod._spec[i]
             dyi = dy2[:, off:off + n]
             hj = hc[:, j * r:(j + 1) * r]                    # h' = s h: dB_i = dY_i^T h'_i
-            g[:, j * r:(j + 1) * r].addmm_(dyi, Bs[i], alpha=s)
+            g[:, j * r:(j + 1) * r].addmm_(dyi, Bs[i], beta=0.0, alpha=s)
             sl = _slot_of(Bs[i])
             if sl is not None:
                 sl.write(lambda v: v.addmm_(dyi.t(), hj, beta=0.0), lambda v: v.addmm_(dyi.t(), hj))
