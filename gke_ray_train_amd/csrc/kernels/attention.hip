@@ -460,7 +460,10 @@ constexpr int K2N = 128, K2M = 32, K2NT = 256, K2NSLOT = 4;
 constexpr int K2IMG = K2M * D * 2;           // one 32-row image: 8 KiB
 constexpr int K2SLOT = 2 * K2IMG + 4 * 1024;  // Q image, dO image, per-wave statistics copy
 
-template <bool DROP>
+// ILV: one explicit schedule for the whole step (sched_group_barrier): tile t+1's S / dP MFMAs each
+// followed by up to 5 of tile t's softmax-gradient VALU ops and its LDS reads, then the dV / dK MFMAs
+// with the remaining transposed reads — one wave per SIMD has no partner wave to fill MFMA gaps.
+template <bool DROP, bool ILV>
 __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdParams P) {
   const AttnParams& p = P.f;
   __shared__ __attribute__((aligned(16))) char smem[K2NSLOT * K2SLOT];
@@ -576,13 +579,15 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
     // keep three fragment pairs in flight ahead of the MFMAs that consume them (the default
     // schedule issues each read right before its MFMA behind lgkmcnt(0): one wave per SIMD has no
     // partner wave to cover that latency)
-    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+    if constexpr (!ILV) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      for (int i = 0; i < 5; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
   };
 
   // tile cursors (query head, query start): the tile being consumed, the next one, the DMA one
@@ -606,15 +611,22 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
       advance(dma_h, dma_q);
     }
 
-    sdp(nxt_q, std::integral_constant<int, (SL + 1) % K2NSLOT>{}, s_n, dp_n);  // past the end: dropped
-
     const char* qi = smem + SL * K2SLOT;
     const float* st = reinterpret_cast<const float*>(qi + 2 * K2IMG + w * 1024);
+    f32x4 lsv[4], dev[4];  // tile t's row statistics, read before tile t+1's S / dP
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      lsv[gg] = *reinterpret_cast<const f32x4*>(st + 8 * gg + 4 * h);
+      dev[gg] = *reinterpret_cast<const f32x4*>(st + 32 + 8 * gg + 4 * h);
+    }
+
+    sdp(nxt_q, std::integral_constant<int, (SL + 1) % K2NSLOT>{}, s_n, dp_n);  // past the end: dropped
+
     bf16x8 pb[2], sb[2];
 #pragma unroll
     for (int gg = 0; gg < 4; ++gg) {
-      const f32x4 ls = *reinterpret_cast<const f32x4*>(st + 8 * gg + 4 * h);
-      const f32x4 de = *reinterpret_cast<const f32x4*>(st + 32 + 8 * gg + 4 * h);
+      const f32x4 ls = lsv[gg];
+      const f32x4 de = dev[gg];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int r = 4 * gg + j;
@@ -652,14 +664,37 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
         dv[db] = mfma32(oa[stp][db], pb[stp], dv[db]);
         dk[db] = mfma32(qa[stp][db], sb[stp], dk[db]);
       }
-    // the transposed reads run three fragments (6 reads) ahead of their MFMAs
-    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+    if constexpr (ILV) {
+      // S / dP of tile t+1 (16 MFMAs) with tile t's VALU and the remaining fragment reads in their
+      // gaps, then the dV / dK MFMAs with the transposed reads
+      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      for (int i = 0; i < 10; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    } else {
+      // the transposed reads run three fragments (6 reads) ahead of their MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
     cur_h = nxt_h;
     cur_q = nxt_q;
     advance(nxt_h, nxt_q);
@@ -961,11 +996,13 @@ void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   pk.f.sched = (sc >> 2) & 1;
   pq.f.sched = (sc >> 1) & 1;
   const dim3 g1(q_grid(pk.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(pq.f.sched, nqb, p.f.B * p.f.Hq));
+  static const bool ilv = [] { const char* e = getenv("GRT_ATTN_DKDV_ILV"); return e && atoi(e) == 1; }();
   if (p.f.drop_thresh) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, pk);
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, false>), g1, dim3(K2NT), 0, s, pk);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(Q2NT), 0, s, pq);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(K2NT), 0, s, pk);
+    if (ilv) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, true>), g1, dim3(K2NT), 0, s, pk);
+    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, false>), g1, dim3(K2NT), 0, s, pk);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(Q2NT), 0, s, pq);
   }
 }
