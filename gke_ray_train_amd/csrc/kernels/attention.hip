@@ -955,7 +955,8 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
 }  // namespace
 
 namespace {
-// bit mask of the kernels that use the causal-pair schedule: 1 = forward, 2 = dQ, 4 = dK / dV
+// bit mask of the kernels that use the causal-pair schedule: 1 = forward, 2 = dQ, 4 = dK / dV;
+// 8 = the dK / dV kernel's interleaved step (ILV)
 // (-1: not set yet -> GRT_ATTN_SCHED, default 1: forward -8 % at B8 S1024 H32, the backward kernels
 // measured neutral-to-slower with it: profiles/r3_attn_schedule.md)
 int g_sched = -1;
@@ -996,7 +997,7 @@ void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   pk.f.sched = (sc >> 2) & 1;
   pq.f.sched = (sc >> 1) & 1;
   const dim3 g1(q_grid(pk.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(pq.f.sched, nqb, p.f.B * p.f.Hq));
-  static const bool ilv = [] { const char* e = getenv("GRT_ATTN_DKDV_ILV"); return e && atoi(e) == 1; }();
+  const bool ilv = (sc >> 3) & 1;  // mask bit 8: the interleaved dK / dV step schedule
   if (p.f.drop_thresh) {
     hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, false>), g1, dim3(K2NT), 0, s, pk);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(Q2NT), 0, s, pq);
