@@ -957,25 +957,42 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
 namespace {
 // bit mask of the kernels that use the causal-pair schedule: 1 = forward, 2 = dQ, 4 = dK / dV;
 // 8 = the dK / dV kernel's interleaved step (ILV)
-// (-1: not set yet -> GRT_ATTN_SCHED, default 1: forward -8 % at B8 S1024 H32, the backward kernels
-// measured neutral-to-slower with it: profiles/r3_attn_schedule.md)
+// (-1: not set yet -> GRT_ATTN_SCHED, default 7: all three kernels pair when the paired grid fills
+// the chip; B8 S1024 H32: forward -10 %, backward -6 %: profiles/r3_attn_schedule.md)
 int g_sched = -1;
 int sched_now() {
   if (g_sched < 0) {
     const char* e = getenv("GRT_ATTN_SCHED");
-    g_sched = e ? atoi(e) : 1;
+    g_sched = e ? atoi(e) : 7;
   }
   return g_sched;
 }
 }  // namespace
+
+// The causal pairs halve the grid: take them only when the paired grid still fills every
+// workgroup slot of the chip (B8 S1024 H32: 2048 dK/dV workgroups -> 1024 pairs on 256 CUs, -6 % backward;
+// B2 S2048 Hkv8: 256 dK/dV workgroups -> 128 pairs would leave half the CUs idle, +3 %).
+static int cu_count() {
+  static const int n = [] {
+    int d = 0, c = 256;
+    hipGetDevice(&d);
+    hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, d);
+    return c > 0 ? c : 256;
+  }();
+  return n;
+}
+static int pair_if_fills(int want, int nblk, int groups, int per_cu) {
+  return want && (int64_t)groups * ((nblk + 1) / 2) >= (int64_t)cu_count() * per_cu ? 1 : 0;
+}
 
 void attn_set_schedule(int s) { g_sched = s; }
 int attn_get_schedule() { return sched_now(); }
 
 void attn_fwd(const AttnParams& p0, hipStream_t s) {
   AttnParams p = p0;
-  p.sched = sched_now() & 1;
-  const dim3 grid(q_grid(p.sched, (p.Sq + F3M - 1) / F3M, p.B * p.Hq));
+  const int nqb = (p.Sq + F3M - 1) / F3M;
+  p.sched = pair_if_fills(sched_now() & 1, nqb, p.B * p.Hq, 2);
+  const dim3 grid(q_grid(p.sched, nqb, p.B * p.Hq));
   // (a 5-slot ring, 3 tiles in flight, spills 41 VGPRs with its 10-step unroll: not instantiated)
   if (p.drop_thresh) hipLaunchKernelGGL((attn_fwd_kernel<true, F3NSLOT>), grid, dim3(F3NT), 0, s, p);
   else hipLaunchKernelGGL((attn_fwd_kernel<false, F3NSLOT>), grid, dim3(F3NT), 0, s, p);
@@ -994,8 +1011,8 @@ void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   const int nkb = (p.f.Sk + K2N - 1) / K2N;
   const int nqb = (p.f.Sq + Q2M - 1) / Q2M;
   AttnBwdParams pk = p, pq = p;
-  pk.f.sched = (sc >> 2) & 1;
-  pq.f.sched = (sc >> 1) & 1;
+  pk.f.sched = pair_if_fills((sc >> 2) & 1, nkb, p.f.B * p.f.Hkv, 1);
+  pq.f.sched = pair_if_fills((sc >> 1) & 1, nqb, p.f.B * p.f.Hq, 2);
   const dim3 g1(q_grid(pk.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(pq.f.sched, nqb, p.f.B * p.f.Hq));
   const bool ilv = (sc >> 3) & 1;  // mask bit 8: the interleaved dK / dV step schedule
   if (p.f.drop_thresh) {
