@@ -983,7 +983,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("rope_cos") = py::none(),
         py::arg("rope_sin") = py::none(), py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0);
   m.def("attn_set_schedule", &grt::attn_set_schedule,
-        "bf16 attention schedule bit mask: causal pairs / XCD grouping for 1 = forward, 2 = dQ, 4 = dK/dV; 8 = interleaved dK/dV step");
+        "bf16 attention causal-pair / XCD-grouped schedule, bit mask: 1 = forward, 2 = dQ, 4 = dK/dV");
   m.def("attn_get_schedule", &grt::attn_get_schedule);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);

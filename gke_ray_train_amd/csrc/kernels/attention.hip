@@ -460,10 +460,9 @@ constexpr int K2N = 128, K2M = 32, K2NT = 256, K2NSLOT = 4;
 constexpr int K2IMG = K2M * D * 2;           // one 32-row image: 8 KiB
 constexpr int K2SLOT = 2 * K2IMG + 4 * 1024;  // Q image, dO image, per-wave statistics copy
 
-// ILV: one explicit schedule for the whole step (sched_group_barrier): tile t+1's S / dP MFMAs each
-// followed by up to 5 of tile t's softmax-gradient VALU ops and its LDS reads, then the dV / dK MFMAs
-// with the remaining transposed reads — one wave per SIMD has no partner wave to fill MFMA gaps.
-template <bool DROP, bool ILV>
+// (An explicit whole-step interleave — tile t+1's S / dP MFMAs each followed by 5 of tile t's VALU
+// ops — measured slower: B8 S1024 H32 backward 428 -> 444 us, GQA 407 -> 451; r3_attn_schedule.md.)
+template <bool DROP>
 __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdParams P) {
   const AttnParams& p = P.f;
   __shared__ __attribute__((aligned(16))) char smem[K2NSLOT * K2SLOT];
@@ -579,15 +578,13 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
     // keep three fragment pairs in flight ahead of the MFMAs that consume them (the default
     // schedule issues each read right before its MFMA behind lgkmcnt(0): one wave per SIMD has no
     // partner wave to cover that latency)
-    if constexpr (!ILV) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    for (int i = 0; i < 5; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
   };
 
   // tile cursors (query head, query start): the tile being consumed, the next one, the DMA one
@@ -664,37 +661,14 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
         dv[db] = mfma32(oa[stp][db], pb[stp], dv[db]);
         dk[db] = mfma32(qa[stp][db], sb[stp], dk[db]);
       }
-    if constexpr (ILV) {
-      // S / dP of tile t+1 (16 MFMAs) with tile t's VALU and the remaining fragment reads in their
-      // gaps, then the dV / dK MFMAs with the transposed reads
-      __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+    // the transposed reads run three fragments (6 reads) ahead of their MFMAs
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
 #pragma unroll
-      for (int i = 0; i < 10; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-      }
-    } else {
-      // the transposed reads run three fragments (6 reads) ahead of their MFMAs
-      __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-#pragma unroll
-      for (int i = 0; i < 10; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    for (int i = 0; i < 10; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
     cur_h = nxt_h;
     cur_q = nxt_q;
     advance(nxt_h, nxt_q);
@@ -955,8 +929,7 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
 }  // namespace
 
 namespace {
-// bit mask of the kernels that use the causal-pair schedule: 1 = forward, 2 = dQ, 4 = dK / dV;
-// 8 = the dK / dV kernel's interleaved step (ILV)
+// bit mask of the kernels that use the causal-pair schedule: 1 = forward, 2 = dQ, 4 = dK / dV
 // (-1: not set yet -> GRT_ATTN_SCHED, default 7: all three kernels pair when the paired grid fills
 // the chip; B8 S1024 H32: forward -10 %, backward -6 %: profiles/r3_attn_schedule.md)
 int g_sched = -1;
@@ -1014,13 +987,11 @@ void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   pk.f.sched = pair_if_fills((sc >> 2) & 1, nkb, p.f.B * p.f.Hkv, 1);
   pq.f.sched = pair_if_fills((sc >> 1) & 1, nqb, p.f.B * p.f.Hq, 2);
   const dim3 g1(q_grid(pk.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(pq.f.sched, nqb, p.f.B * p.f.Hq));
-  const bool ilv = (sc >> 3) & 1;  // mask bit 8: the interleaved dK / dV step schedule
   if (p.f.drop_thresh) {
-    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<true, false>), g1, dim3(K2NT), 0, s, pk);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, pk);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(Q2NT), 0, s, pq);
   } else {
-    if (ilv) hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, true>), g1, dim3(K2NT), 0, s, pk);
-    else hipLaunchKernelGGL((attn_bwd_dkdv_kernel<false, false>), g1, dim3(K2NT), 0, s, pk);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(K2NT), 0, s, pk);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(Q2NT), 0, s, pq);
   }
 }

@@ -10,7 +10,7 @@ export GRT_STORAGE_PATH=/tmp/grt_sftt
 SFT="env ${SFT_ENV:-GRT_X=0} python3 tools/sft_inproc.py --set NUM_TRAIN_SAMPLES=320 --set EVAL_STEPS_SFT=20 --set SAVE_STEPS_SFT=1000 --set OUTPUT_DIR_BASE=/tmp/grt_sftt/out"
 GRT_TUNED_GEMM_RECORD_UNTUNED=$PWD/$O/untuned.csv timeout -k 10 300 $SFT > $O/record.log 2>&1 || exit $?
 ls $O
-timeout -k 10 ${TUNE_S:-900} python3 tools/tune_untuned.py "$O/untuned*.csv" --out $O/tuned.csv > $O/tune.log 2>&1 || exit $?
+timeout -k 10 ${TUNE_S:-900} python3 tools/tune_untuned.py "$O/untuned*.csv" --out $O/tuned.csv --only "${TUNE_ONLY:-}" > $O/tune.log 2>&1 || exit $?
 tail -3 $O/tune.log
 for r in 1 2; do
   timeout -k 10 300 $SFT > $O/ab_old_$r.log 2>&1 || exit $?

@@ -20,6 +20,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gke_ray_train_amd.ops.gemm_tuning import RESULTS, check_tuned_table  # noqa: E402
 
 
+def write_results(tun, path):
+    with open(path + ".tmp", "w") as fh:
+        for k, v in tun.get_validators():
+            fh.write(f"Validator,{k},{v}\n")
+        for op_sig, param_sig, kernel, ms in tun.get_results():
+            fh.write(f"{op_sig},{param_sig},{kernel},{ms}\n")
+    os.replace(path + ".tmp", path)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("untuned", help="untuned-shape file(s), glob allowed")
@@ -58,13 +67,10 @@ def main(argv=None):
         tun.tune_gemm_in_file(tmp)
         torch.cuda.synchronize()
         print(f"[{i + 1}/{len(todo)}] {ln.split(',')[1]} tuned in {time.time() - t0:.1f} s", flush=True)
+        write_results(tun, a.out)  # after every shape: a time-limited run keeps what it tuned
     os.remove(tmp) if os.path.exists(tmp) else None
     tun.tuning_enable(False)
-    with open(a.out, "w") as fh:
-        for k, v in tun.get_validators():
-            fh.write(f"Validator,{k},{v}\n")
-        for op_sig, param_sig, kernel, ms in tun.get_results():
-            fh.write(f"{op_sig},{param_sig},{kernel},{ms}\n")
+    write_results(tun, a.out)
     res = check_tuned_table(a.out)
     bad = [r for r in res if not r[3]]
     for ln, fin, rel, ok in bad:
