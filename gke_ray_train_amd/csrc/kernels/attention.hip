@@ -358,17 +358,27 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
 
   const float lt = l + __shfl_xor(l, 32, 64);
   const float inv = lt > 0.f ? 1.f / lt : 0.f;
-  if (myq < Sq) {
-    bf16* O = (bf16*)p.o + (int64_t)b * p.o_bs + (tok0 + myq) * p.o_ss + (int64_t)hq * p.o_hs;
+  // O rows as 16-byte stores (cdna_hip_programming.md T21): lane l (h = 0) holds columns
+  // 8 gg .. 8 gg + 3 of its row and lane l + 32 columns 8 gg + 4 .. 8 gg + 7; one v_permlane32_swap
+  // per dword of the (gg, gg + 1) pair gives lanes 0-31 columns 8 gg .. 8 gg + 7 and lanes 32-63
+  // columns 8 gg + 8 .. 8 gg + 15 — half the store instructions. Every lane takes part in the swap.
+  bf16* O = (bf16*)p.o + (int64_t)b * p.o_bs + (tok0 + min(myq, Sq - 1)) * p.o_ss + (int64_t)hq * p.o_hs;
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+  for (int db = 0; db < 4; ++db)
 #pragma unroll
-      for (int gg = 0; gg < 4; ++gg) {
-        bf16x4 v;
+    for (int gp = 0; gp < 2; ++gp) {
+      union { bf16x4 v; uint32_t u[2]; } a, c2;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(o[db][4 * gg + j] * inv);
-        *reinterpret_cast<bf16x4*>(O + db * 32 + 8 * gg + 4 * h) = v;
+      for (int j = 0; j < 4; ++j) {
+        a.v[j] = static_cast<bf16>(o[db][8 * gp + j] * inv);
+        c2.v[j] = static_cast<bf16>(o[db][8 * gp + 4 + j] * inv);
       }
+      const auto r0 = __builtin_amdgcn_permlane32_swap(a.u[0], c2.u[0], false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(a.u[1], c2.u[1], false, false);
+      if (myq < Sq)
+        *reinterpret_cast<uint4*>(O + db * 32 + 16 * gp + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+    }
+  if (myq < Sq) {
     if (h == 0 && p.lse)
       p.lse[((int64_t)b * p.Hq + hq) * p.Sq + myq] = lt > 0.f ? (m + __log2f(lt)) * kLn2 : INFINITY;
   }
