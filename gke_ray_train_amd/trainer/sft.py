@@ -109,6 +109,9 @@ class SFTConfig:
     # evaluation forwards: token cap per fused / packed chunk (the training step's sizes, which the
     # GEMM table is tuned at; 16 K-token eval chunks ran on untuned shapes)
     eval_max_tokens: int = 8192
+    # evaluation batches packed padding-free (None: whenever the model supports it, see
+    # SFTTrainer._eval_padding_free)
+    eval_padding_free: Optional[bool] = None
 
     def __post_init__(self):
         if self.evaluation_strategy is not None:  # deprecated alias used by the reference (:317)
@@ -477,7 +480,24 @@ class SFTTrainer:
             groups.append(cur)
         return [self._pack(g, mult, weighted) for g in groups]
 
-    def _step_chunks(self, batches, mis, fuse, weighted: bool = True, max_tokens: Optional[int] = None):
+    def _eval_padding_free(self) -> bool:
+        """Evaluation packs its batches padding-free whenever the model takes ``varlen`` (forward
+        only: no per-step GEMM-shape concern; eval_runtime 2.37 -> 2.19 s on the reference SFT job,
+        profiles/r3_sft_job_trace.md). ``eval_padding_free=False`` / GRT_SFT_EVAL_PADDING_FREE=0: padded."""
+        a = self.args
+        if a.eval_padding_free is not None:
+            return bool(a.eval_padding_free)
+        if os.environ.get("GRT_SFT_EVAL_PADDING_FREE", "1") == "0" or self.device.type != "cuda":
+            return self._padding_free_enabled()
+        import inspect
+        inner = getattr(self.model, "base_model", self.model)
+        try:
+            return "varlen" in inspect.signature(inner.forward).parameters
+        except (TypeError, ValueError):
+            return False
+
+    def _step_chunks(self, batches, mis, fuse, weighted: bool = True, max_tokens: Optional[int] = None,
+                     padding_free: Optional[bool] = None):
         """The micro-batches ``mis`` of one optimizer step -> [(batch, loss_weights | None)].
         Unfused: one entry per micro-batch (loss = mean / accum). Fused: micro-batches are right-
         padded to a common length and concatenated while the padded size stays within
@@ -486,7 +506,7 @@ class SFTTrainer:
         sum of the unfused micro-batch losses."""
         if not fuse:
             return [(batches[mi], None) for mi in mis]
-        if self._padding_free_enabled():
+        if self._padding_free_enabled() if padding_free is None else padding_free:
             return self._pack_chunks(batches, mis, weighted, max_tokens)
         accum = self.args.gradient_accumulation_steps
         mult = int(os.environ.get("GRT_SFT_PAD_MULTIPLE", "0")) or self.args.fuse_pad_multiple or 1
@@ -699,7 +719,8 @@ class SFTTrainer:
         batches = self._batches(self.eval_seqs, self.args.per_device_eval_batch_size, 0, shuffle=False)
         if self._fuse_enabled():  # same token-weighted mean from fewer, larger forwards
             batches = [cb for cb, _ in self._step_chunks(batches, list(range(len(batches))), True, weighted=False,
-                                                         max_tokens=self.args.eval_max_tokens)]
+                                                         max_tokens=self.args.eval_max_tokens,
+                                                         padding_free=self._eval_padding_free())]
         with torch.no_grad():  # as HF's prediction_step: no saved activations, no fused CE gradient
             for cb in batches:
                 b = self._to_dev(cb)

@@ -195,3 +195,22 @@ def test_padding_free_groups_by_real_tokens(tmp_path):
             valid[a:b - 1] = cb["labels"][0, a + 1:b] != -100
         tot += float((w[0] * valid).sum())
     assert abs(tot - 1.0) < 1e-5
+
+
+def test_padding_free_eval_matches_padded(tmp_path):
+    """evaluate() on padding-free packed batches (the default on GPU) gives the padded token-weighted
+    eval_loss: same sequences, attention confined to each sequence by ops.Varlen."""
+    import torch
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    torch.manual_seed(0)
+    m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
+    rows = [{"text": "select * from t where x = %d " % i * (1 + i % 4)} for i in range(12)]
+    losses = []
+    for pf in (False, True):
+        tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path / f"e{pf}"), per_device_train_batch_size=2,
+                                     per_device_eval_batch_size=3, gradient_accumulation_steps=2,
+                                     fuse_accumulation=True, eval_padding_free=pf, pack_multiple=16),
+                        train_dataset=rows, eval_dataset=rows)
+        losses.append(tr.evaluate()["eval_loss"])
+    assert abs(losses[0] - losses[1]) < 1e-5 * max(1.0, abs(losses[0])), losses
