@@ -397,9 +397,51 @@ bool lora_dx(const Tensor& g, const Tensor& at, const Tensor& dx, double p, int6
   return true;
 }
 
+static bool rowmajor_bf16(const Tensor& t) {
+  return t.is_cuda() && t.dim() == 2 && t.scalar_type() == at::kBFloat16 && t.stride(1) == 1 &&
+         t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0;
+}
+
+// c [M, 64] (+)= alpha * a [M, K] @ bt^T, bt = B^T [64, K] (lora_grad.hip); all row-major with unit
+// column stride (row-strided views allowed). Returns false (nothing done) when unsupported.
+bool lora_g(const Tensor& a, const Tensor& bt, const Tensor& c, double alpha, bool accumulate) {
+  if (!rowmajor_bf16(a) || !rowmajor_bf16(bt) || !rowmajor_bf16(c)) return false;
+  const int64_t M = a.size(0);
+  const int K = (int)a.size(1);
+  if (bt.size(0) != c.size(1) || bt.size(1) != K || c.size(0) != M || !grt::lora_g_supported(M, K, (int)c.size(1)))
+    return false;
+  c10::OptionalDeviceGuard dg(c.device());
+  grt::LoraGParams p{};
+  p.a = a.data_ptr(); p.lda = a.stride(0); p.bt = bt.data_ptr(); p.ldbt = bt.stride(0);
+  p.c = c.data_ptr(); p.ldc = c.stride(0); p.M = M; p.K = K; p.alpha = (float)alpha; p.accumulate = accumulate ? 1 : 0;
+  grt::lora_g(p, cur_stream(c));
+  return true;
+}
+
+// out (+)= alpha * a^T @ h, a [M, N], h [M, R]: out [N, R], or [R, N] when transpose (lora_grad.hip);
+// fp32 token-split partials in a workspace from the caching allocator. False when unsupported.
+bool lora_tred(const Tensor& a, const Tensor& h, const Tensor& out, double alpha, bool accumulate, bool transpose) {
+  if (!rowmajor_bf16(a) || !rowmajor_bf16(h) || !rowmajor_bf16(out)) return false;
+  const int64_t M = a.size(0);
+  const int N = (int)a.size(1), R = (int)h.size(1);
+  if (h.size(0) != M || !grt::lora_tred_supported(M, N, R)) return false;
+  if (transpose ? (out.size(0) != R || out.size(1) != N) : (out.size(0) != N || out.size(1) != R)) return false;
+  if (out.stride(0) % 4 != 0) return false;
+  c10::OptionalDeviceGuard dg(out.device());
+  grt::LoraTredParams p{};
+  p.ks = grt::lora_tred_splits(M, N, R, device_cus(out.get_device()));
+  Tensor ws = at::empty({(int64_t)p.ks * N * R}, out.options().dtype(at::kFloat));
+  p.a = a.data_ptr(); p.lda = a.stride(0); p.h = h.data_ptr(); p.ldh = h.stride(0); p.ws = ws.data_ptr<float>();
+  p.M = M; p.N = N; p.R = R; p.out = out.data_ptr(); p.ldo = out.stride(0);
+  p.transpose = transpose ? 1 : 0; p.accumulate = accumulate ? 1 : 0; p.alpha = (float)alpha;
+  grt::lora_tred(p, cur_stream(out));
+  return true;
+}
+
 // B_i [n_i, r] -> the adapter tail of W' [out, ldw] (columns col0 + j r ..) and of W'^T [.., ldt]
 void lora_refresh(const std::vector<Tensor>& bs, const std::vector<int64_t>& offs, Tensor& w,
-                  const optional<Tensor>& wt_opt, int64_t col0) {
+                  const optional<Tensor>& wt_opt, int64_t col0, int64_t wt_row0) {
+  if (wt_row0 < 0) wt_row0 = col0;  // W'^T rows of the adapter block (a separate B^T buffer: 0)
   TORCH_CHECK(!bs.empty() && bs.size() <= 4 && offs.size() == bs.size(), "lora_refresh: 1-4 targets");
   TORCH_CHECK(w.dim() == 2 && w.stride(1) == 1 && w.scalar_type() == at::kBFloat16, "lora_refresh: bf16 W'");
   Tensor wt = wt_opt.has_value() ? *wt_opt : w.t();  // no W'^T: only the shape checks use the view
@@ -414,11 +456,12 @@ void lora_refresh(const std::vector<Tensor>& bs, const std::vector<int64_t>& off
     check_contig(bs[j], "B");
     TORCH_CHECK(bs[j].scalar_type() == at::kBFloat16 && bs[j].size(1) == p.r && bs[j].size(0) % 64 == 0 &&
                     offs[j] % 8 == 0 && offs[j] + bs[j].size(0) <= w.size(0) &&
-                    col0 + (int64_t)(j + 1) * p.r <= w.size(1) && col0 + (int64_t)(j + 1) * p.r <= wt.size(0),
+                    col0 + (int64_t)(j + 1) * p.r <= w.size(1) && wt_row0 + (int64_t)(j + 1) * p.r <= wt.size(0) &&
+                    (!wt_opt.has_value() || offs[j] + bs[j].size(0) <= wt.size(1)),
                 "lora_refresh: B_i bf16 [n % 64 == 0, r] inside W'");
     p.b[j] = bs[j].data_ptr(); p.off[j] = (int)offs[j]; p.n[j] = (int)bs[j].size(0);
   }
-  p.w = w.data_ptr(); p.ldw = w.stride(0); p.col0 = (int)col0;
+  p.w = w.data_ptr(); p.ldw = w.stride(0); p.col0 = (int)col0; p.trow0 = (int)wt_row0;
   p.wt = wt_opt.has_value() ? wt.data_ptr() : nullptr;
   p.ldt = wt_opt.has_value() ? wt.stride(0) : 0;
   c10::OptionalDeviceGuard g(w.device());
@@ -964,7 +1007,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("want_xd"), py::arg("h_out") = py::none(), py::arg("hscale") = 1.0);
   m.def("lora_dx", &lora_dx, py::arg("g"), py::arg("at"), py::arg("dx"), py::arg("p"), py::arg("seed"),
         py::arg("offset"), py::arg("accumulate"), py::arg("dx_in") = py::none(), py::arg("gscale") = 1.0);
-  m.def("lora_refresh", &lora_refresh);
+  m.def("lora_refresh", &lora_refresh, py::arg("bs"), py::arg("offs"), py::arg("w"), py::arg("wt"), py::arg("col0"),
+        py::arg("wt_row0") = -1);
+  m.def("lora_g", &lora_g, py::arg("a"), py::arg("bt"), py::arg("c"), py::arg("alpha"), py::arg("accumulate"));
+  m.def("lora_tred", &lora_tred, py::arg("a"), py::arg("h"), py::arg("out"), py::arg("alpha"), py::arg("accumulate"),
+        py::arg("transpose"));
   m.def("dropout_bwd_seeded", &dropout_bwd_seeded);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

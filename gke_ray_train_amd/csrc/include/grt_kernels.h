@@ -124,10 +124,30 @@ struct LoraDxParams {
 struct LoraRefreshParams {
   const void* b[4]; int off[4]; int n[4]; int ntarget; int r;
   void* w; int64_t ldw; void* wt; int64_t ldt; int col0;
+  int trow0;  // W'^T row of the first adapter block (col0 for the full transpose; 0 for a B^T buffer)
 };
 void lora_refresh(const LoraRefreshParams& p, hipStream_t s);
 bool lora_dx_supported(int64_t M, int K, int R, uint64_t offset);
 void lora_dx(const LoraDxParams& p, hipStream_t s);
+
+// ---------------- LoRA gradient GEMMs (lora_grad.hip) ----------------
+// C[M][64] (+)= alpha * A[M][K] B[K][64], from B^T [64][K] (row stride ldbt)
+struct LoraGParams {
+  const void* a; int64_t lda; const void* bt; int64_t ldbt; void* c; int64_t ldc;
+  int64_t M; int K; float alpha; int accumulate;
+};
+bool lora_g_supported(int64_t M, int K, int r);
+void lora_g(const LoraGParams& p, hipStream_t s);
+// out (+)= alpha * A^T H, A [M][N], H [M][R]: out [N][R] (row stride ldo), or [R][N] when transpose;
+// ks token splits through the fp32 workspace ws [ks][N * R] (lora_tred_splits)
+struct LoraTredParams {
+  const void* a; int64_t lda; const void* h; int64_t ldh; float* ws;
+  int64_t M; int N; int R; int ks; int64_t mchunk;
+  void* out; int64_t ldo; int transpose; int accumulate; float alpha;
+};
+bool lora_tred_supported(int64_t M, int N, int R);
+int lora_tred_splits(int64_t M, int N, int R, int cus);
+void lora_tred(const LoraTredParams& p, hipStream_t s);
 
 // ---------------- attention (attention.hip) ----------------
 struct AttnParams {

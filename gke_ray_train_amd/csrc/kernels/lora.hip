@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void lora_refresh_kernel(const LoraRefreshPara
         bf16x8 v;
 #pragma unroll
         for (int q = 0; q < 8; ++q) v[q] = tile[rr + q][cc];
-        *reinterpret_cast<bf16x8*>(WT + (int64_t)(P.col0 + j * P.r + c0 + cc) * P.ldt + P.off[j] + r0 + rr) = v;
+        *reinterpret_cast<bf16x8*>(WT + (int64_t)(P.trow0 + j * P.r + c0 + cc) * P.ldt + P.off[j] + r0 + rr) = v;
       }
     }
     __syncthreads();

@@ -1,0 +1,331 @@
+// LoRA adapter gradient GEMMs for gfx950 / CDNA4: the skinny products of the LoRA backward, each
+// ONE pass over its big [tokens, features] operand at HBM rate.
+//
+// Reference role: the backward of PEFT's LoRA layer on every adapted projection of the QLoRA SFT job
+// (r = 64 on q,k,v,o,gate,up,down; reference ray-jobs/fine_tune_llama_ray.py:243-254,
+// fine_tune_config.json:6-8,30-33): per target i, with dY_i the projection's
+// output gradient [M tokens, n_i], h'_i = s drop(x) A_i^T [M, r] and x_d = drop(x) [M, in]:
+//     g_i  = s dY_i B_i          [M, r]     (dL/dh, feeds dA and the adapter's dX)
+//     dB_i = dY_i^T h'_i         [n_i, r]
+//     dA   = g^T x_d             [R, in]    (all targets of one input, R = r * targets)
+// These are memory-bound (the r- or R-wide side is tiny): hipBLASLt tiles them as 64x16 .. 64x64
+// output tiles, so every column tile re-reads the whole [M, n] operand (2-4 reads of dY per
+// product; profiles/r3_lora_grad_gemms.md). Here each big operand is read once:
+//
+//   lora_g    C[M][64] (+)= alpha A[M][K] B[K][64], from B^T [64][K] (row stride ldbt).
+//             One workgroup = 32 rows; its 4 waves take interleaved 128-column k-tiles. A tiles are
+//             loaded as whole 256 B rows (16 lanes per row), written to the wave's OWN swizzled LDS
+//             image and read back as MFMA fragments (no barrier in the loop: the image is private,
+//             and one wave's LDS operations execute in order); B^T fragments come from L2. The 4
+//             partial 32x64 tiles are summed through LDS at the end.
+//   lora_tred C = A^T H, A [M][N], H [M][R] (R = 64 / 128 / 192): the token-reduction products dB
+//             (A = dY_i, H = h'_i) and dA (A = x_d, H = g; stored transposed). One workgroup = 128
+//             columns of A x one range of tokens (split over M to fill the chip); A and H arrive in
+//             32-token tiles by LDS-DMA into a 4-slot ring (attention.hip's pipeline: swizzled image,
+//             counted vmcnt across raw s_barriers) and feed the MFMAs through transposed
+//             (ds_read_b64_tr_b16) reads, wave w owning columns 32w..32w+31. fp32 partials per token
+//             range go to a workspace in the OUTPUT layout (staged through LDS so both layouts store
+//             whole rows); lora_tred_fin sums them, scales, converts and assigns / accumulates.
+// v_mfma_f32_32x32x16_bf16 throughout (cdna_hip_programming.md §3 layouts).
+#include <type_traits>
+
+#include "grt_common.h"
+#include "grt_kernels.h"
+
+namespace grt {
+namespace {
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+
+__device__ __forceinline__ f32x16 mfma_bf16_32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+// accumulator element r of lane half hh holds row (r & 3) + 8 (r >> 2) + 4 hh of the 32-row tile
+__device__ __forceinline__ int acc_row32(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+// [rows][128 x bf16] LDS image, 256 B rows, 16-byte chunks XOR-swizzled so that both the b128 row
+// reads (32 rows, one chunk) and the tr_b16 column reads are conflict-free (attention.hip img_off)
+__device__ __forceinline__ int swz16(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int img_byte(int row, int ch) { return row * 256 + 16 * (ch ^ swz16(row)); }
+__device__ __forceinline__ bf16x4 tr_read(const char* base, int r0, int c0, int l16) {
+  const int q = l16 >> 2, p = l16 & 3;
+  const int col = c0 + 4 * p;
+  const char* a = base + img_byte(r0 + q, col >> 3) + 8 * ((col >> 2) & 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a);
+}
+__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+__device__ __forceinline__ void dma16(const void* gptr, uint32_t lds_byte_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(gptr), "s"(lds_byte_addr) : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(p);
+}
+
+// ---------------------------------------------------------------------------------------------
+// lora_g
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 8192];  // one 32x128 image per wave; then 4 fp32 32x64 partials
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g4 = lane >> 4, l16 = lane & 15;
+  const int64_t m0 = (int64_t)blockIdx.x * 32;
+  const bf16* A = static_cast<const bf16*>(P.a);
+  const bf16* BT = static_cast<const bf16*>(P.bt);
+  char* img = smem + w * 8192;
+  const int nkt = P.K / 128;
+  // this lane's 8 rows of the 32-row tile (row 4 i + g4) and its 16-byte chunk l16 of each
+  const bf16* arow[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t m = min(m0 + 4 * i + g4, P.M - 1);
+    arow[i] = A + m * P.lda + 8 * l16;
+  }
+  const bf16* brow0 = BT + (int64_t)l32 * P.ldbt + 8 * hh;
+  const bf16* brow1 = BT + (int64_t)(32 + l32) * P.ldbt + 8 * hh;
+
+  auto load = [&](int kt, bf16x8 (&ra)[8], bf16x8 (&rb)[16]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ra[i] = *reinterpret_cast<const bf16x8*>(arow[i] + kt * 128);
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      rb[ks] = *reinterpret_cast<const bf16x8*>(brow0 + kt * 128 + 16 * ks);
+      rb[8 + ks] = *reinterpret_cast<const bf16x8*>(brow1 + kt * 128 + 16 * ks);
+    }
+  };
+  f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+  auto compute = [&](const bf16x8 (&ra)[8], const bf16x8 (&rb)[16]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<bf16x8*>(img + img_byte(4 * i + g4, l16)) = ra[i];
+    bf16x8 af[8];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) af[ks] = *reinterpret_cast<const bf16x8*>(img + img_byte(l32, 2 * ks + hh));
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      acc0 = mfma_bf16_32(af[ks], rb[ks], acc0);
+      acc1 = mfma_bf16_32(af[ks], rb[8 + ks], acc1);
+    }
+  };
+  bf16x8 raA[8], raB[8], rbA[16], rbB[16];
+  int kt = w;  // this wave's k-tiles: w, w + 4, w + 8, ...
+  if (kt < nkt) load(kt, raA, rbA);
+  while (kt < nkt) {
+    if (kt + 4 < nkt) load(kt + 4, raB, rbB);
+    compute(raA, rbA);
+    kt += 4;
+    if (kt >= nkt) break;
+    if (kt + 4 < nkt) load(kt + 4, raA, rbA);
+    compute(raB, rbB);
+    kt += 4;
+  }
+  __syncthreads();  // every wave is done with its image: the space takes the partial tiles
+  float* part = reinterpret_cast<float*>(smem);  // [4 waves][32 rows][64 cols]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    part[w * 2048 + acc_row32(r, hh) * 64 + l32] = acc0[r];
+    part[w * 2048 + acc_row32(r, hh) * 64 + 32 + l32] = acc1[r];
+  }
+  __syncthreads();
+  const int row = tid >> 3, c8 = (tid & 7) * 8;
+  const int64_t m = m0 + row;
+  if (m >= P.M) return;
+  float s[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(&part[q * 2048 + row * 64 + c8]);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(&part[q * 2048 + row * 64 + c8 + 4]);
+    s[0] += a[0]; s[1] += a[1]; s[2] += a[2]; s[3] += a[3];
+    s[4] += b[0]; s[5] += b[1]; s[6] += b[2]; s[7] += b[3];
+  }
+  bf16* C = static_cast<bf16*>(P.c) + m * P.ldc + c8;
+  bf16x8 o;
+  if (P.accumulate) {
+    const bf16x8 old = *reinterpret_cast<const bf16x8*>(C);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = static_cast<bf16>(static_cast<float>(old[e]) + P.alpha * s[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = static_cast<bf16>(P.alpha * s[e]);
+  }
+  *reinterpret_cast<bf16x8*>(C) = o;
+}
+
+// ---------------------------------------------------------------------------------------------
+// lora_tred
+// ---------------------------------------------------------------------------------------------
+constexpr int TR_NS = 4;           // ring slots
+constexpr int TR_IMG = 32 * 256;   // one 32-token x 128-column image: 8 KiB
+
+template <int RT>  // R = 32 RT
+constexpr int tr_nhi() { return (32 * RT + 127) / 128; }
+template <int RT>
+constexpr int tr_slot() { return TR_IMG * (1 + tr_nhi<RT>()); }
+template <int RT>
+constexpr int tr_lds() {  // ring, or the 128 x (R + 4) fp32 output tile of the epilogue
+  return TR_NS * tr_slot<RT>() > 128 * (32 * RT + 4) * 4 ? TR_NS * tr_slot<RT>() : 128 * (32 * RT + 4) * 4;
+}
+
+template <int D>  // D DMA instructions per tile: wait until at most `pending` tiles are in flight
+__device__ __forceinline__ void wait_pending(int pending) {
+  if (pending >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * D) : "memory");
+  else if (pending == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(D) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int RT>
+__global__ __launch_bounds__(256) void lora_tred_kernel(const LoraTredParams P) {
+  constexpr int R = 32 * RT, NHI = tr_nhi<RT>(), SLOT = tr_slot<RT>(), DPT = 2 * (1 + NHI);
+  __shared__ __attribute__((aligned(16))) char smem[tr_lds<RT>()];
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g4 = lane >> 4, l16 = lane & 15;
+  const int nblk = P.N / 128;
+  const int nb = blockIdx.x % nblk, ks = blockIdx.x / nblk;
+  const int64_t mbeg = (int64_t)ks * P.mchunk;
+  const int64_t mend = min(P.M, mbeg + P.mchunk);
+  const int nt = mend > mbeg ? (int)((mend - mbeg) / 32) : 0;
+  const bf16* A = static_cast<const bf16*>(P.a) + (int64_t)nb * 128;
+  const bf16* H = static_cast<const bf16*>(P.h);
+
+  // LDS-DMA of tile t: wave w fills image rows 8w .. 8w+7 (two 1-KiB pieces of 4 rows) of the A
+  // image and of every H image; the XOR swizzle is applied to the per-lane SOURCE chunk. H images
+  // past column R (R = 64, or the second image at R = 192) re-read a valid chunk: never consumed.
+  const uint32_t smem0 = lds_addr(smem);
+  const int row0 = 8 * w + g4, row1 = row0 + 4;
+  const int ch0 = l16 ^ swz16(row0), ch1 = l16 ^ swz16(row1);
+  auto dma_tile = [&](int t, int slot) {
+    const int64_t r0 = mbeg + 32 * t + row0, r1 = mbeg + 32 * t + row1;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + (uint32_t)(slot * SLOT + 8 * w * 256));
+    dma16(A + r0 * P.lda + 8 * ch0, dst);
+    dma16(A + r1 * P.lda + 8 * ch1, dst + 1024);
+#pragma unroll
+    for (int hi = 0; hi < NHI; ++hi) {
+      const int valid = (R - 128 * hi) >= 128 ? 16 : (R - 128 * hi) / 8;  // chunks of this image inside R
+      const int c0 = 128 * hi + 8 * (ch0 % valid), c1 = 128 * hi + 8 * (ch1 % valid);
+      dma16(H + r0 * P.ldh + c0, dst + (1 + hi) * TR_IMG);
+      dma16(H + r1 * P.ldh + c1, dst + (1 + hi) * TR_IMG + 1024);
+    }
+  };
+
+  f32x16 acc[RT];
+#pragma unroll
+  for (int j = 0; j < RT; ++j) acc[j] = f32x16{};
+  if (nt > 0) {
+    const int pre = min(nt, TR_NS - 1);
+    for (int t = 0; t < pre; ++t) dma_tile(t, t);
+    for (int t = 0; t < nt; ++t) {
+      const int slot = t % TR_NS;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot t-1 are done
+      wait_pending<DPT>(min(nt, t + TR_NS - 1) - (t + 1));  // tile t landed (this wave's pieces)
+      __builtin_amdgcn_s_barrier();                         // ... every wave's; slot t-1 free
+      if (t + TR_NS - 1 < nt) dma_tile(t + TR_NS - 1, (t + TR_NS - 1) % TR_NS);
+      const char* ai = smem + slot * SLOT;
+#pragma unroll
+      for (int stp = 0; stp < 2; ++stp) {
+        const int kk = 16 * stp + 4 * hh;
+        const int c0 = 32 * w + (g4 & 1) * 16;
+        const bf16x8 a = cat8(tr_read(ai, kk, c0, l16), tr_read(ai, kk + 8, c0, l16));
+#pragma unroll
+        for (int j = 0; j < RT; ++j) {
+          const char* hi = ai + TR_IMG * (1 + (j >> 2));
+          const int cj = 32 * (j & 3) + (g4 & 1) * 16;
+          const bf16x8 b = cat8(tr_read(hi, kk, cj, l16), tr_read(hi, kk + 8, cj, l16));
+          acc[j] = mfma_bf16_32(a, b, acc[j]);  // D[column of A][column of H]
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // ring consumed: the space takes the fp32 output tile
+  constexpr int TS = R + 4;
+  float* tile = reinterpret_cast<float*>(smem);  // [128 columns of A][R]
+#pragma unroll
+  for (int j = 0; j < RT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tile[(32 * w + acc_row32(r, hh)) * TS + 32 * j + l32] = acc[j][r];
+  __syncthreads();
+  float* ws = P.ws + (int64_t)ks * P.N * R;
+  if (!P.transpose) {  // ws[n][j]: thread -> 4 consecutive j of one n
+    for (int e = tid; e < 128 * R / 4; e += 256) {
+      const int n = e / (R / 4), j4 = (e % (R / 4)) * 4;
+      *reinterpret_cast<f32x4*>(ws + (int64_t)(nb * 128 + n) * R + j4) = *reinterpret_cast<const f32x4*>(&tile[n * TS + j4]);
+    }
+  } else {  // ws[j][n]: thread -> 4 consecutive n of one j
+    for (int e = tid; e < 128 * R / 4; e += 256) {
+      const int j = e / 32, n4 = (e % 32) * 4;
+      f32x4 v;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = tile[(n4 + q) * TS + j];
+      *reinterpret_cast<f32x4*>(ws + (int64_t)j * P.N + nb * 128 + n4) = v;
+    }
+  }
+}
+
+// out[row][col] (+)= alpha * sum_ks ws[ks][row][col], rows x cols = N x R (or R x N transposed)
+__global__ __launch_bounds__(256) void lora_tred_fin_kernel(const LoraTredParams P) {
+  const int64_t rows = P.transpose ? P.R : P.N, cols = P.transpose ? P.N : P.R;
+  const int64_t n4 = rows * cols / 4, plane = (int64_t)P.N * P.R;
+  bf16* out = static_cast<bf16*>(P.out);
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
+    const int64_t row = (4 * e) / cols, col = (4 * e) % cols;
+    f32x4 s = *reinterpret_cast<const f32x4*>(P.ws + 4 * e);
+    for (int k = 1; k < P.ks; ++k) s += *reinterpret_cast<const f32x4*>(P.ws + k * plane + 4 * e);
+    bf16x4* dst = reinterpret_cast<bf16x4*>(out + row * P.ldo + col);
+    bf16x4 o;
+    if (P.accumulate) {
+      const bf16x4 old = *dst;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = static_cast<bf16>(static_cast<float>(old[q]) + P.alpha * s[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = static_cast<bf16>(P.alpha * s[q]);
+    }
+    *dst = o;
+  }
+}
+
+}  // namespace
+
+bool lora_g_supported(int64_t M, int K, int r) { return M > 0 && K > 0 && K % 128 == 0 && r == 64; }
+
+void lora_g(const LoraGParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(lora_g_kernel, dim3((unsigned)((p.M + 31) / 32)), dim3(256), 0, s, p);
+}
+
+bool lora_tred_supported(int64_t M, int N, int R) {
+  return M > 0 && M % 32 == 0 && N > 0 && N % 128 == 0 && (R == 64 || R == 128 || R == 192);
+}
+
+// token splits: enough workgroups for every CU (the ring takes 64 KiB at R <= 128: two per CU),
+// at most 16, each split a whole number of 32-token tiles
+int lora_tred_splits(int64_t M, int N, int R, int cus) {
+  const int nblk = N / 128;
+  const int per_cu = R <= 128 ? 2 : 1;
+  int ks = (int)((per_cu * (int64_t)cus + nblk - 1) / nblk);
+  const int64_t tiles = M / 32;
+  if (ks > 16) ks = 16;
+  if (ks > tiles) ks = (int)tiles;
+  return ks < 1 ? 1 : ks;
+}
+
+void lora_tred(const LoraTredParams& p0, hipStream_t s) {
+  LoraTredParams p = p0;
+  const int64_t tiles = p.M / 32;
+  p.mchunk = 32 * ((tiles + p.ks - 1) / p.ks);
+  const dim3 grid((unsigned)((p.N / 128) * p.ks)), block(256);
+  switch (p.R) {
+    case 64: hipLaunchKernelGGL(lora_tred_kernel<2>, grid, block, 0, s, p); break;
+    case 128: hipLaunchKernelGGL(lora_tred_kernel<4>, grid, block, 0, s, p); break;
+    default: hipLaunchKernelGGL(lora_tred_kernel<6>, grid, block, 0, s, p); break;
+  }
+  const int64_t n4 = (int64_t)p.N * p.R / 4;
+  int64_t fb = (n4 + 255) / 256;
+  if (fb > 1024) fb = 1024;
+  hipLaunchKernelGGL(lora_tred_fin_kernel, dim3((unsigned)fb), block, 0, s, p);
+}
+
+}  // namespace grt

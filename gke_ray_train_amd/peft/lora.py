@@ -117,6 +117,20 @@ def _adapter_then_base_dx(ctx, C, base, dy2, g, acat):
 # folded into the GEMMs' alpha. GRT_LORA_DIRECT_GRAD=0 -> autograd accumulation.
 _LORA_DIRECT_GRAD = os.environ.get("GRT_LORA_DIRECT_GRAD", "1") != "0"
 _LORA_KCAT = os.environ.get("GRT_LORA_KCAT", "1") != "0"
+# The adapter-gradient GEMMs g_i = s dY_i B_i, dB_i = dY_i^T h'_i and dA = g^T x_d on the
+# framework's one-pass kernels (csrc/kernels/lora_grad.hip: each reads its [tokens, features]
+# operand once) instead of hipBLASLt's skinny tiles (2-4 reads per product). GRT_LORA_GRAD_KERNELS=0:
+# library GEMMs.
+_LORA_GRAD_KERNELS = os.environ.get("GRT_LORA_GRAD_KERNELS", "1") != "0"
+
+
+def _bf16_cuda(*ts):
+    return all(t.is_cuda and t.dtype == torch.bfloat16 for t in ts)
+
+
+def _tred_into(C, a, h, out, alpha, accumulate, transpose):
+    """out (+)= alpha a^T h on the one-pass token-reduction kernel; False when it does not apply."""
+    return _LORA_GRAD_KERNELS and _bf16_cuda(a, h, out) and C.lora_tred(a, h, out, alpha, accumulate, transpose)
 
 
 def _packed(ts):
@@ -302,18 +316,25 @@ class _LoraKcatFn(torch.autograd.Function):
         dx = None
         g = torch.empty(M, r * k, device=dy2.device, dtype=dy2.dtype)  # dL/dh (unscaled h) = s dY_i B_i
         dBs: List[Optional[torch.Tensor]] = [None] * k
+        bt = getattr(mod, "_bt", None) if _LORA_GRAD_KERNELS and _bf16_cuda(dy2, hc) else None
         for j, i in enumerate(order):
             off, n, _ = mod._spec[i]
             dyi = dy2[:, off:off + n]
             hj = hc[:, j * r:(j + 1) * r]                    # h' = s h: dB_i = dY_i^T h'_i
-            g[:, j * r:(j + 1) * r].addmm_(dyi, Bs[i], beta=0.0, alpha=s)
+            gj = g[:, j * r:(j + 1) * r]
+            # B_i^T: rows j r .. of the B^T buffer lora_refresh filled in this step's forward
+            if not (bt is not None and C.lora_g(dyi, bt[j * r:(j + 1) * r, off:off + n], gj, s, False)):
+                gj.addmm_(dyi, Bs[i], beta=0.0, alpha=s)
             sl = _slot_of(Bs[i])
             if sl is not None:
-                sl.write(lambda v: v.addmm_(dyi.t(), hj, beta=0.0), lambda v: v.addmm_(dyi.t(), hj))
+                sl.write(lambda v: _tred_into(C, dyi, hj, v, 1.0, False, False) or v.addmm_(dyi.t(), hj, beta=0.0),
+                         lambda v: _tred_into(C, dyi, hj, v, 1.0, True, False) or v.addmm_(dyi.t(), hj))
                 sl.notify(Bs[i])
             else:
-                dBs[i] = torch.mm(dyi.t(), hj)
-        dAs = _lora_dA(g, xd, As, order, r)
+                dBs[i] = torch.empty(n, r, device=dy2.device, dtype=dy2.dtype)
+                if not _tred_into(C, dyi, hj, dBs[i], 1.0, False, False):
+                    dBs[i] = torch.mm(dyi.t(), hj)
+        dAs = _lora_dA(g, xd, As, order, r, C)
         if ctx.needs_input_grad[0]:
             dx = _adapter_then_base_dx(ctx, C, mod.base, dy2, g, acat)
         if ctx.needs_input_grad[0] and dx is None:
@@ -327,7 +348,7 @@ class _LoraKcatFn(torch.autograd.Function):
         return (dx, None, None, None, None, *dAs, *dBs)
 
 
-def _lora_dA(g, xd, As, order, r):
+def _lora_dA(g, xd, As, order, r, C=None):
     """dA_cat = g^T x_d, written into the (adjacent) gradient slots when the engine provides them."""
     k = len(As)
     dAs: List[Optional[torch.Tensor]] = [None] * k
@@ -337,15 +358,19 @@ def _lora_dA(g, xd, As, order, r):
         pk = _packed([sl.view for sl in aslots])
     if pk is not None and pk[0] == list(range(k)):
         dst = pk[1]
-        if aslots[0].fresh:
-            dst.addmm_(g.t(), xd, beta=0.0)
-        else:
-            dst.addmm_(g.t(), xd)
+        fresh = aslots[0].fresh
+        if not (C is not None and _tred_into(C, xd, g, dst, 1.0, not fresh, True)):  # dA^T = x_d^T g
+            if fresh:
+                dst.addmm_(g.t(), xd, beta=0.0)
+            else:
+                dst.addmm_(g.t(), xd)
         for sl, i in zip(aslots, order):
             sl.fresh, sl.direct = False, True
             sl.notify(As[i])
     else:
-        dacat = g.t() @ xd
+        dacat = torch.empty(g.shape[1], xd.shape[1], device=g.device, dtype=g.dtype)
+        if not (C is not None and _tred_into(C, xd, g, dacat, 1.0, False, True)):
+            dacat = g.t() @ xd
         for j, i in enumerate(order):
             rows = dacat[j * r:(j + 1) * r]
             sl = aslots[j]
@@ -383,6 +408,7 @@ class LoraLinear(nn.Module):
         self._spec = [(off, n, name) for name, off, n in self.targets]
         self._wk = None     # K-concatenated weight [out, in + R] (built lazily)
         self._wk_order = None
+        self._bt = None     # [R, out]: the B blocks transposed (adapter-gradient kernel), with W'
 
     @property
     def kcat_pad(self) -> int:
@@ -420,8 +446,15 @@ class LoraLinear(nn.Module):
         bl = [Bs[i].detach() for i in order]
         offs = [self._spec[i][0] for i in order]
         if all(b.is_contiguous() for b in bl):
-            _native.kernels().lora_refresh(bl, offs, self._wk, None, K)
+            # B^T [R, out] for the adapter-gradient kernel (lora_grad.hip lora_g): block j = B_{order[j]}^T
+            if _LORA_GRAD_KERNELS and r == 64 and self._wk.is_cuda:
+                if self._bt is None:
+                    self._bt = torch.zeros(R, self.out_features, device=self._wk.device, dtype=self._wk.dtype)
+                _native.kernels().lora_refresh(bl, offs, self._wk, self._bt, K, 0)
+            else:
+                _native.kernels().lora_refresh(bl, offs, self._wk, None, K)
         else:
+            self._bt = None
             for j, (b, off) in enumerate(zip(bl, offs)):
                 self._wk[off:off + b.shape[0], K + j * r:K + (j + 1) * r].copy_(b)
         return self._wk
