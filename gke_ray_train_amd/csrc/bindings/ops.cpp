@@ -408,12 +408,19 @@ bool lora_g(const Tensor& a, const Tensor& bt, const Tensor& c, double alpha, bo
   if (!rowmajor_bf16(a) || !rowmajor_bf16(bt) || !rowmajor_bf16(c)) return false;
   const int64_t M = a.size(0);
   const int K = (int)a.size(1);
-  if (bt.size(0) != c.size(1) || bt.size(1) != K || c.size(0) != M || !grt::lora_g_supported(M, K, (int)c.size(1)))
+  if (bt.size(0) != c.size(1) || bt.size(1) != K || c.size(0) != M || !grt::lora_g_supported(M, K, (int)c.size(1)) ||
+      c.stride(0) % 4 != 0)
     return false;
   c10::OptionalDeviceGuard dg(c.device());
   grt::LoraGParams p{};
   p.a = a.data_ptr(); p.lda = a.stride(0); p.bt = bt.data_ptr(); p.ldbt = bt.stride(0);
   p.c = c.data_ptr(); p.ldc = c.stride(0); p.M = M; p.K = K; p.alpha = (float)alpha; p.accumulate = accumulate ? 1 : 0;
+  p.ks = grt::lora_g_splits(M, K, device_cus(c.get_device()));
+  Tensor ws;
+  if (p.ks > 1) {
+    ws = at::empty({(int64_t)p.ks * M * 64}, c.options().dtype(at::kFloat));
+    p.ws = ws.data_ptr<float>();
+  }
   grt::lora_g(p, cur_stream(c));
   return true;
 }

@@ -135,8 +135,10 @@ void lora_dx(const LoraDxParams& p, hipStream_t s);
 struct LoraGParams {
   const void* a; int64_t lda; const void* bt; int64_t ldbt; void* c; int64_t ldc;
   int64_t M; int K; float alpha; int accumulate;
+  int ks = 1; float* ws = nullptr;  // k splits (lora_g_splits) through the fp32 workspace [ks][M][64]
 };
 bool lora_g_supported(int64_t M, int K, int r);
+int lora_g_splits(int64_t M, int K, int cus);
 void lora_g(const LoraGParams& p, hipStream_t s);
 // out (+)= alpha * A^T H, A [M][N], H [M][R]: out [N][R] (row stride ldo), or [R][N] when transpose;
 // ks token splits through the fp32 workspace ws [ks][N * R] (lora_tred_splits)

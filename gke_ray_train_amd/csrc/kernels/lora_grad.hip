@@ -13,11 +13,9 @@
 // product; profiles/r3_lora_grad_gemms.md). Here each big operand is read once:
 //
 //   lora_g    C[M][64] (+)= alpha A[M][K] B[K][64], from B^T [64][K] (row stride ldbt).
-//             One workgroup = 32 rows; its 4 waves take interleaved 128-column k-tiles. A tiles are
-//             loaded as whole 256 B rows (16 lanes per row), written to the wave's OWN swizzled LDS
-//             image and read back as MFMA fragments (no barrier in the loop: the image is private,
-//             and one wave's LDS operations execute in order); B^T fragments come from L2. The 4
-//             partial 32x64 tiles are summed through LDS at the end.
+//             One workgroup = 128 rows (32 per wave) x one range of 128-column k-tiles; A and B^T
+//             tiles arrive by LDS-DMA into a 3-slot ring, B^T shared by the 4 waves; k-split fp32
+//             partials are summed by lora_g_fin.
 //   lora_tred C = A^T H, A [M][N], H [M][R] (R = 64 / 128 / 192): the token-reduction products dB
 //             (A = dY_i, H = h'_i) and dA (A = x_d, H = g; stored transposed). One workgroup = 128
 //             columns of A x one range of tokens (split over M to fill the chip); A and H arrive in
@@ -66,92 +64,124 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // ---------------------------------------------------------------------------------------------
 // lora_g
 // ---------------------------------------------------------------------------------------------
+constexpr int G_NS = 3;                     // ring slots
+constexpr int G_SLOT = 4 * 8192 + 16384;    // A image (128 rows = four 32-row images) + B^T image (64 rows)
+
+template <int D>  // D DMA instructions per tile: wait until at most `pending` tiles are in flight
+__device__ __forceinline__ void wait_pending(int pending) {
+  if (pending >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * D) : "memory");
+  else if (pending == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(D) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// One workgroup = 128 rows x one range of k-tiles (split over K to fill the chip). Per 128-column
+// k-tile the A rows (wave w: rows 32w..32w+31) and the 64 B^T rows arrive by LDS-DMA into a 3-slot
+// ring (swizzled images, counted vmcnt across raw s_barriers: attention.hip's pipeline); B^T is
+// shared by the 4 waves. (A per-wave register-staged version, B^T private per wave, ran at ~half the
+// HBM rate: every CU moved 3x the A bytes through its load path.)
 __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 8192];  // one 32x128 image per wave; then 4 fp32 32x64 partials
+  __shared__ __attribute__((aligned(16))) char smem[G_NS * G_SLOT];
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4, l16 = lane & 15;
-  const int64_t m0 = (int64_t)blockIdx.x * 32;
+  const int nrb = (int)((P.M + 127) / 128);
+  const int rb = blockIdx.x % nrb, ksi = blockIdx.x / nrb;
+  const int64_t m0 = (int64_t)rb * 128;
+  const int nkt_all = P.K / 128;
+  const int kt0 = ksi * nkt_all / P.ks;
+  const int nt = (ksi + 1) * nkt_all / P.ks - kt0;
   const bf16* A = static_cast<const bf16*>(P.a);
   const bf16* BT = static_cast<const bf16*>(P.bt);
-  char* img = smem + w * 8192;
-  const int nkt = P.K / 128;
-  // this lane's 8 rows of the 32-row tile (row 4 i + g4) and its 16-byte chunk l16 of each
-  const bf16* arow[8];
+  // DMA sources: wave w fills A image w (its 32 rows, 8 pieces of 4 rows) and B^T rows 16w..16w+15
+  // (4 pieces); piece row 4p + g4, the XOR swizzle on the per-lane source chunk
+  const bf16* asrc[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int64_t m = min(m0 + 4 * i + g4, P.M - 1);
-    arow[i] = A + m * P.lda + 8 * l16;
+  for (int p = 0; p < 8; ++p) {
+    const int r = 4 * p + g4;
+    const int64_t m = min(m0 + 32 * w + r, P.M - 1);
+    asrc[p] = A + m * P.lda + (int64_t)kt0 * 128 + 8 * (l16 ^ swz16(r));
   }
-  const bf16* brow0 = BT + (int64_t)l32 * P.ldbt + 8 * hh;
-  const bf16* brow1 = BT + (int64_t)(32 + l32) * P.ldbt + 8 * hh;
-
-  auto load = [&](int kt, bf16x8 (&ra)[8], bf16x8 (&rb)[16]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ra[i] = *reinterpret_cast<const bf16x8*>(arow[i] + kt * 128);
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      rb[ks] = *reinterpret_cast<const bf16x8*>(brow0 + kt * 128 + 16 * ks);
-      rb[8 + ks] = *reinterpret_cast<const bf16x8*>(brow1 + kt * 128 + 16 * ks);
-    }
-  };
-  f32x16 acc0 = f32x16{}, acc1 = f32x16{};
-  auto compute = [&](const bf16x8 (&ra)[8], const bf16x8 (&rb)[16]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) *reinterpret_cast<bf16x8*>(img + img_byte(4 * i + g4, l16)) = ra[i];
-    bf16x8 af[8];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) af[ks] = *reinterpret_cast<const bf16x8*>(img + img_byte(l32, 2 * ks + hh));
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      acc0 = mfma_bf16_32(af[ks], rb[ks], acc0);
-      acc1 = mfma_bf16_32(af[ks], rb[8 + ks], acc1);
-    }
-  };
-  bf16x8 raA[8], raB[8], rbA[16], rbB[16];
-  int kt = w;  // this wave's k-tiles: w, w + 4, w + 8, ...
-  if (kt < nkt) load(kt, raA, rbA);
-  while (kt < nkt) {
-    if (kt + 4 < nkt) load(kt + 4, raB, rbB);
-    compute(raA, rbA);
-    kt += 4;
-    if (kt >= nkt) break;
-    if (kt + 4 < nkt) load(kt + 4, raA, rbA);
-    compute(raB, rbB);
-    kt += 4;
-  }
-  __syncthreads();  // every wave is done with its image: the space takes the partial tiles
-  float* part = reinterpret_cast<float*>(smem);  // [4 waves][32 rows][64 cols]
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    part[w * 2048 + acc_row32(r, hh) * 64 + l32] = acc0[r];
-    part[w * 2048 + acc_row32(r, hh) * 64 + 32 + l32] = acc1[r];
-  }
-  __syncthreads();
-  const int row = tid >> 3, c8 = (tid & 7) * 8;
-  const int64_t m = m0 + row;
-  if (m >= P.M) return;
-  float s[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) s[e] = 0.f;
+  const bf16* bsrc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(&part[q * 2048 + row * 64 + c8]);
-    const f32x4 b = *reinterpret_cast<const f32x4*>(&part[q * 2048 + row * 64 + c8 + 4]);
-    s[0] += a[0]; s[1] += a[1]; s[2] += a[2]; s[3] += a[3];
-    s[4] += b[0]; s[5] += b[1]; s[6] += b[2]; s[7] += b[3];
+    const int r = 16 * w + 4 * q + g4;
+    bsrc[q] = BT + (int64_t)r * P.ldbt + (int64_t)kt0 * 128 + 8 * (l16 ^ swz16(r));
   }
-  bf16* C = static_cast<bf16*>(P.c) + m * P.ldc + c8;
-  bf16x8 o;
-  if (P.accumulate) {
-    const bf16x8 old = *reinterpret_cast<const bf16x8*>(C);
+  const uint32_t smem0 = lds_addr(smem);
+  auto dma_tile = [&](int t, int slot) {
+    const uint32_t base = smem0 + (uint32_t)(slot * G_SLOT);
+    const uint32_t da = __builtin_amdgcn_readfirstlane(base + (uint32_t)(w * 8192));
+    const uint32_t db = __builtin_amdgcn_readfirstlane(base + (uint32_t)(32768 + 16 * w * 256));
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = static_cast<bf16>(static_cast<float>(old[e]) + P.alpha * s[e]);
-  } else {
+    for (int p = 0; p < 8; ++p) dma16(asrc[p] + t * 128, da + p * 1024);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = static_cast<bf16>(P.alpha * s[e]);
+    for (int q = 0; q < 4; ++q) dma16(bsrc[q] + t * 128, db + q * 1024);
+  };
+  f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+  if (nt > 0) {
+    const int pre = min(nt, G_NS - 1);
+    for (int t = 0; t < pre; ++t) dma_tile(t, t);
+    for (int t = 0; t < nt; ++t) {
+      const int slot = t % G_NS;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of slot t-1 are done
+      wait_pending<12>(min(nt, t + G_NS - 1) - (t + 1));  // tile t landed (this wave's pieces)
+      __builtin_amdgcn_s_barrier();                        // ... every wave's; slot t-1 free
+      if (t + G_NS - 1 < nt) dma_tile(t + G_NS - 1, (t + G_NS - 1) % G_NS);
+      const char* ai = smem + slot * G_SLOT + w * 8192;
+      const char* bi = smem + slot * G_SLOT + 32768;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ai + img_byte(l32, 2 * ks + hh));
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(bi + img_byte(l32, 2 * ks + hh));
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(bi + img_byte(32 + l32, 2 * ks + hh));
+        acc0 = mfma_bf16_32(af, b0, acc0);
+        acc1 = mfma_bf16_32(af, b1, acc1);
+      }
+    }
   }
-  *reinterpret_cast<bf16x8*>(C) = o;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // D[row][col]: lane -> column l32 (acc0) / 32 + l32 (acc1), register r -> row acc_row32(r, hh)
+  if (P.ks > 1) {  // fp32 partial of this k range; lora_g_fin sums them
+    float* ws = P.ws + (int64_t)ksi * P.M * 64;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = m0 + 32 * w + acc_row32(r, hh);
+      if (m < P.M) {
+        ws[m * 64 + l32] = acc0[r];
+        ws[m * 64 + 32 + l32] = acc1[r];
+      }
+    }
+    return;
+  }
+  bf16* C = static_cast<bf16*>(P.c);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int64_t m = m0 + 32 * w + acc_row32(r, hh);
+    if (m < P.M) {
+      bf16* c = C + m * P.ldc;
+      const float o0 = P.alpha * acc0[r] + (P.accumulate ? static_cast<float>(c[l32]) : 0.f);
+      const float o1 = P.alpha * acc1[r] + (P.accumulate ? static_cast<float>(c[32 + l32]) : 0.f);
+      c[l32] = static_cast<bf16>(o0);
+      c[32 + l32] = static_cast<bf16>(o1);
+    }
+  }
+}
+
+// C[m][0..63] (+)= alpha * sum_k ws[k][m][..]
+__global__ __launch_bounds__(256) void lora_g_fin_kernel(const LoraGParams P) {
+  const int64_t n4 = P.M * 16, plane = P.M * 64;
+  bf16* C = static_cast<bf16*>(P.c);
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
+    const int64_t m = e >> 4, c = (e & 15) * 4;
+    f32x4 s = *reinterpret_cast<const f32x4*>(P.ws + 4 * e);
+    for (int k = 1; k < P.ks; ++k) s += *reinterpret_cast<const f32x4*>(P.ws + k * plane + 4 * e);
+    bf16x4* dst = reinterpret_cast<bf16x4*>(C + m * P.ldc + c);
+    bf16x4 o;
+    const bf16x4 old = P.accumulate ? *dst : bf16x4{};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = static_cast<bf16>(P.alpha * s[q] + (P.accumulate ? static_cast<float>(old[q]) : 0.f));
+    *dst = o;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -167,13 +197,6 @@ constexpr int tr_slot() { return TR_IMG * (1 + tr_nhi<RT>()); }
 template <int RT>
 constexpr int tr_lds() {  // ring, or the 128 x (R + 4) fp32 output tile of the epilogue
   return TR_NS * tr_slot<RT>() > 128 * (32 * RT + 4) * 4 ? TR_NS * tr_slot<RT>() : 128 * (32 * RT + 4) * 4;
-}
-
-template <int D>  // D DMA instructions per tile: wait until at most `pending` tiles are in flight
-__device__ __forceinline__ void wait_pending(int pending) {
-  if (pending >= 2) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * D) : "memory");
-  else if (pending == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(D) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <int RT>
@@ -292,20 +315,36 @@ __global__ __launch_bounds__(256) void lora_tred_fin_kernel(const LoraTredParams
 
 bool lora_g_supported(int64_t M, int K, int r) { return M > 0 && K > 0 && K % 128 == 0 && r == 64; }
 
+// k splits: one workgroup per CU (144 KiB of LDS each), at most 8 and at most the k-tiles
+int lora_g_splits(int64_t M, int K, int cus) {
+  const int64_t nrb = (M + 127) / 128;
+  int ks = (int)((cus + nrb - 1) / nrb);
+  if (ks > 8) ks = 8;
+  if (ks > K / 128) ks = K / 128;
+  return ks < 1 ? 1 : ks;
+}
+
 void lora_g(const LoraGParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(lora_g_kernel, dim3((unsigned)((p.M + 31) / 32)), dim3(256), 0, s, p);
+  const dim3 grid((unsigned)(((p.M + 127) / 128) * p.ks)), block(256);
+  hipLaunchKernelGGL(lora_g_kernel, grid, block, 0, s, p);
+  if (p.ks > 1) {
+    int64_t fb = (p.M * 16 + 255) / 256;
+    if (fb > 1024) fb = 1024;
+    hipLaunchKernelGGL(lora_g_fin_kernel, dim3((unsigned)fb), block, 0, s, p);
+  }
 }
 
 bool lora_tred_supported(int64_t M, int N, int R) {
   return M > 0 && M % 32 == 0 && N > 0 && N % 128 == 0 && (R == 64 || R == 128 || R == 192);
 }
 
-// token splits: enough workgroups for every CU (the ring takes 64 KiB at R <= 128: two per CU),
-// at most 16, each split a whole number of 32-token tiles
+// token splits: one workgroup per CU (each split adds an N x R fp32 partial write + read: two per CU
+// at N = 4096, R = 64 made the partials a quarter of the operand's bytes), at most 16, each split a
+// whole number of 32-token tiles
 int lora_tred_splits(int64_t M, int N, int R, int cus) {
+  (void)R;
   const int nblk = N / 128;
-  const int per_cu = R <= 128 ? 2 : 1;
-  int ks = (int)((per_cu * (int64_t)cus + nblk - 1) / nblk);
+  int ks = (int)(((int64_t)cus + nblk - 1) / nblk);
   const int64_t tiles = M / 32;
   if (ks > 16) ks = 16;
   if (ks > tiles) ks = (int)tiles;
