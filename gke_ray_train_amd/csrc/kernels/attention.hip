@@ -971,10 +971,15 @@ static int pair_if_fills(int want, int nblk, int groups, int per_cu) {
 void attn_set_schedule(int s) { g_sched = s; }
 int attn_get_schedule() { return sched_now(); }
 
+// Padding-free packing (cu_seqlens): the grid is sized for the longest sequence, so a shorter one's
+// heavy block of a causal pair exits at once and the pair's work is no longer equal — pairs off
+// (LoRA step at 6656 packed tokens 33.1 -> 31.4 ms per 1K tokens; profiles/r3_varlen_attention.md).
+static int sched_for(const AttnParams& p, int bit) { return p.cu_seqlens ? 0 : (sched_now() >> bit) & 1; }
+
 void attn_fwd(const AttnParams& p0, hipStream_t s) {
   AttnParams p = p0;
   const int nqb = (p.Sq + F3M - 1) / F3M;
-  p.sched = pair_if_fills(sched_now() & 1, nqb, p.B * p.Hq, 2);
+  p.sched = pair_if_fills(sched_for(p, 0), nqb, p.B * p.Hq, 2);
   const dim3 grid(q_grid(p.sched, nqb, p.B * p.Hq));
   // (a 5-slot ring, 3 tiles in flight, spills 41 VGPRs with its 10-step unroll: not instantiated)
   if (p.drop_thresh) hipLaunchKernelGGL((attn_fwd_kernel<true, F3NSLOT>), grid, dim3(F3NT), 0, s, p);
@@ -988,14 +993,13 @@ int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
 
 void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   AttnBwdParams p = p0;
-  const int sc = sched_now();
   const int64_t rows = (int64_t)p.f.B * p.f.Hq * sq_pad(p.f.Sq);
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
   const int nkb = (p.f.Sk + K2N - 1) / K2N;
   const int nqb = (p.f.Sq + Q2M - 1) / Q2M;
   AttnBwdParams pk = p, pq = p;
-  pk.f.sched = pair_if_fills((sc >> 2) & 1, nkb, p.f.B * p.f.Hkv, 1);
-  pq.f.sched = pair_if_fills((sc >> 1) & 1, nqb, p.f.B * p.f.Hq, 2);
+  pk.f.sched = pair_if_fills(sched_for(p.f, 2), nkb, p.f.B * p.f.Hkv, 1);
+  pq.f.sched = pair_if_fills(sched_for(p.f, 1), nqb, p.f.B * p.f.Hq, 2);
   const dim3 g1(q_grid(pk.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(pq.f.sched, nqb, p.f.B * p.f.Hq));
   if (p.f.drop_thresh) {
     hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, pk);

@@ -96,10 +96,11 @@ class SFTConfig:
     # padding-free packing of each fused step (``ops.Varlen``): the step's sequences are concatenated
     # on one token axis (attention inside each sequence, RoPE positions restarting), so no GEMM,
     # norm or loss row is spent on padding; only the total is rounded up to fuse_pad_multiple with
-    # one masked filler segment. Same loss and gradient as the padded batch. None = on when
-    # GRT_SFT_PADDING_FREE=1 (and fused accumulation is on and the model's forward takes ``varlen``):
-    # off by default because the packed token counts leave the offline-tuned GEMM sizes — on the
-    # reference SFT job 27.1 vs 28.8 samples/s (profiles/r3_sft_padding_free_ab.md) until those are tuned.
+    # one masked filler segment. Same loss and gradient as the padded batch. None = on for GPU
+    # models whose forward takes ``varlen`` (with fused accumulation); GRT_SFT_PADDING_FREE=0/1
+    # overrides. Reference SFT job, interleaved on one box: 33.7 / 33.6 vs 33.3 / 33.4 samples/s
+    # padded, once the packed token counts were in the GEMM table and varlen attention dropped the
+    # causal pairs (profiles/r3_lora_grad_gemms.md, r3_varlen_attention.md).
     padding_free: Optional[bool] = None
     # packed steps: micro-batches are grouped while their REAL tokens stay within pack_max_tokens,
     # and the packed length is rounded up to pack_multiple (the token counts the GEMM table is
@@ -421,7 +422,10 @@ class SFTTrainer:
         a = self.args
         if a.padding_free is not None:
             return bool(a.padding_free)
-        if os.environ.get("GRT_SFT_PADDING_FREE", "0") != "1":
+        env = os.environ.get("GRT_SFT_PADDING_FREE")
+        if env is not None and env != "1":
+            return False
+        if env is None and self.device.type != "cuda":  # default: GPU only
             return False
         import inspect
         inner = getattr(self.model, "base_model", self.model)
