@@ -350,7 +350,7 @@ std::vector<Tensor> lora_down(const Tensor& x, const Tensor& a, double p, int64_
   lp.p = (float)p; lp.seed = (uint64_t)seed; lp.offset = (uint64_t)offset;
   lp.ldh = h.stride(0); lp.hscale = (float)hscale;
   static const int split_env = [] { const char* e = getenv("GRT_LORA_DOWN_SPLIT"); return e ? atoi(e) : 0; }();
-  lp.ksplit = split_env > 0 ? std::min(split_env, K / 128) : grt::lora_down_splits(M, K, device_cus(x.device().index()));
+  lp.ksplit = split_env > 0 ? std::min(split_env, K / 128) : grt::lora_down_splits(M, K, R, device_cus(x.device().index()));
   Tensor hpart;
   if (lp.ksplit > 1) {
     hpart = at::empty({(int64_t)lp.ksplit, M, R}, x.options().dtype(at::kFloat));

@@ -105,7 +105,7 @@ struct LoraDownParams {
   int64_t ldh = 0;      // h row stride (0 = R); > R: h is the tail of a [x | h] row buffer
   float hscale = 1.f;   // h = hscale * drop(x) A^T (the LoRA scaling folded in)
 };
-int lora_down_splits(int64_t M, int K, int cus);
+int lora_down_splits(int64_t M, int K, int R, int cus);
 bool lora_down_supported(int64_t M, int K, int R, int ldx, uint64_t offset);
 void lora_down(const LoraDownParams& p, hipStream_t s);
 // dX[M][K] (+)= keep/(1-p) ⊙ (g[M][R] · A[R][K]), given A^T = at [K][R] (same keep mask as lora_down)

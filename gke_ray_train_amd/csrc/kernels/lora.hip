@@ -57,54 +57,68 @@ __device__ __forceinline__ void drop8(bf16x8& v, uint64_t key, uint64_t idx0, ui
   for (int e = 0; e < 8; ++e) v[e] = static_cast<bf16>(kp[e] ? static_cast<float>(v[e]) * sc : 0.f);
 }
 
-template <int RB, int KC>
+template <int RB, int KC, int TB>
 constexpr int lora_down_lds_bytes() {  // x images + A images; the final reduction reuses the space
-  return (2 * 32 * (KC + 8) * 2 + 2 * 32 * RB * (KC + 8) * 2) > 3 * RB * 16 * 64 * 4
-             ? (2 * 32 * (KC + 8) * 2 + 2 * 32 * RB * (KC + 8) * 2) : 3 * RB * 16 * 64 * 4;
+  return (2 * 32 * TB * (KC + 8) * 2 + 2 * 32 * RB * (KC + 8) * 2) > (4 - TB) * RB * 16 * 64 * 4
+             ? (2 * 32 * TB * (KC + 8) * 2 + 2 * 32 * RB * (KC + 8) * 2) : (4 - TB) * RB * 16 * 64 * 4;
 }
 
-// KC: K chunk (128, or 64 for half the LDS: two workgroups per CU at R = 192)
-template <int RB, int KC>  // R = 32 * RB
+// KC: K chunk (128, or 64 for half the LDS: two workgroups per CU at R = 192).
+// TB: 32-token tiles per workgroup. The kernel is bound by the A chunk loads from L2 (one [R][KC]
+// chunk per workgroup per chunk: R / 32 times the x bytes at TB = 1; profiles/r2_perf_experiments.md),
+// so TB = 2 halves them per x byte: wave w takes token tile w % TB and k-slice w / TB of each chunk.
+template <int RB, int KC, int TB>  // R = 32 * RB
 __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) {
   constexpr int R = 32 * RB;
   constexpr int XS = KC + 8;         // LDS row (bf16): +16 B so b128 fragment reads of 32 rows spread over banks
   constexpr int AIMG = R * XS;       // elements per A image
-  constexpr int NV = KC / 64;        // 16 B x vectors per thread per chunk (32 rows x KC / 256 threads / 8)
+  constexpr int XIMG = 32 * TB * XS;  // elements per x image
+  constexpr int NV = KC / 64;        // 16 B x vectors per thread per chunk and token tile (32 rows x KC / 256 threads / 8)
   constexpr int TPA = KC / 8;        // A loader threads per row
   constexpr int NA = R * TPA / 256;  // A vectors per thread per chunk
-  constexpr int KSW = KC / 64;       // 16-wide k-steps per wave per chunk
-  __shared__ __attribute__((aligned(16))) char smem[lora_down_lds_bytes<RB, KC>()];
-  bf16* xs = reinterpret_cast<bf16*>(smem);                    // [2][32][XS]
-  bf16* as = reinterpret_cast<bf16*>(smem + 2 * 32 * XS * 2);  // [2][R][XS]
+  constexpr int NSL = 4 / TB;        // k-slices per chunk (waves per token tile)
+  constexpr int KSW = KC / 16 / NSL;  // 16-wide k-steps per wave per chunk
+  __shared__ __attribute__((aligned(16))) char smem[lora_down_lds_bytes<RB, KC, TB>()];
+  bf16* xs = reinterpret_cast<bf16*>(smem);                  // [2][32 TB][XS]
+  bf16* as = reinterpret_cast<bf16*>(smem + 2 * XIMG * 2);   // [2][R][XS]
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tt = w % TB, ksl = w / TB;  // this wave's token tile and k-slice
   // split-K: blockIdx = split * (token blocks) + token block; this workgroup reduces K chunks
   // [c_lo, c_lo + nch) and writes an fp32 partial when the K range is split (lora_hsum adds them)
-  const int ntb = (int)((P.M + 31) / 32);
+  const int ntb = (int)((P.M + 32 * TB - 1) / (32 * TB));
   const int tb = blockIdx.x % ntb, ksi = blockIdx.x / ntb;
   const int nch_all = P.K / KC;
   const int c_lo = ksi * nch_all / P.ksplit;
   const int nch = (ksi + 1) * nch_all / P.ksplit - c_lo;
-  const int64_t t0 = (int64_t)tb * 32;
-  const int lr = tid >> 3, lc = (tid & 7) * 8 * NV;  // x loader: row, first of 8 NV columns
-  const int64_t ltok = t0 + lr;
-  const bool lok = ltok < P.M;
-  const bf16* src = static_cast<const bf16*>(P.x) + (lok ? ltok : P.M - 1) * (int64_t)P.ldx + c_lo * KC + lc;
-  bf16* xdst = (P.xd != nullptr && lok) ? static_cast<bf16*>(P.xd) + ltok * (int64_t)P.K + c_lo * KC + lc : nullptr;
+  const int64_t t0 = (int64_t)tb * 32 * TB;
+  const int lr = tid >> 3, lc = (tid & 7) * 8 * NV;  // x loader: rows lr + 32 u (u < TB), first of 8 NV columns
+  const bf16* src[TB];
+  bf16* xdst[TB];
+  uint64_t eidx[TB];  // of this thread's first x element in each of its rows
+#pragma unroll
+  for (int u = 0; u < TB; ++u) {
+    const int64_t ltok = t0 + lr + 32 * u;
+    const bool lok = ltok < P.M;
+    src[u] = static_cast<const bf16*>(P.x) + (lok ? ltok : P.M - 1) * (int64_t)P.ldx + c_lo * KC + lc;
+    xdst[u] = (P.xd != nullptr && lok) ? static_cast<bf16*>(P.xd) + ltok * (int64_t)P.K + c_lo * KC + lc : nullptr;
+    eidx[u] = P.offset + (uint64_t)ltok * (uint64_t)P.K + c_lo * KC + lc;
+  }
   const int ar = tid / TPA, ac = (tid % TPA) * 8;  // A loader: rows ar + (256 / TPA) j, 8 columns from ac
   const bf16* asrc = static_cast<const bf16*>(P.a) + (int64_t)ar * P.K + c_lo * KC + ac;
   const bool drop = P.p > 0.f;
   const uint32_t thr = drop_thr(P.p);
   const float sc = drop ? 1.f / (1.f - P.p) : 1.f;
   const uint64_t key = hash_u64(P.seed);
-  const uint64_t eidx = P.offset + (uint64_t)ltok * (uint64_t)P.K + c_lo * KC + lc;  // of this thread's first x element
 
-  bf16x8 ring[LD_PF][NV];
+  bf16x8 ring[LD_PF][TB][NV];
 #pragma unroll
   for (int i = 0; i < LD_PF; ++i)
     if (i < nch) {
 #pragma unroll
-      for (int v = 0; v < NV; ++v) ring[i][v] = *reinterpret_cast<const bf16x8*>(src + i * KC + 8 * v);
+      for (int u = 0; u < TB; ++u)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) ring[i][u][v] = *reinterpret_cast<const bf16x8*>(src[u] + i * KC + 8 * v);
     }
   bf16x8 areg[NA];
 #pragma unroll
@@ -117,16 +131,20 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
     for (int i = 0; i < LD_PF; ++i) {
       const int c = c0 + i;
       if (c < nch) {  // block-uniform
-        bf16x8 xv[NV];
+        bf16x8 xv[TB][NV];
 #pragma unroll
-        for (int v = 0; v < NV; ++v) xv[v] = ring[i][v];
+        for (int u = 0; u < TB; ++u)
+#pragma unroll
+          for (int v = 0; v < NV; ++v) xv[u][v] = ring[i][u][v];
         if (c + LD_PF < nch) {
 #pragma unroll
-          for (int v = 0; v < NV; ++v) ring[i][v] = *reinterpret_cast<const bf16x8*>(src + (c + LD_PF) * KC + 8 * v);
+          for (int u = 0; u < TB; ++u)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) ring[i][u][v] = *reinterpret_cast<const bf16x8*>(src[u] + (c + LD_PF) * KC + 8 * v);
         }
         // buffer c & 1 (c0 is a multiple of LD_PF); the previous reader of this buffer was chunk
         // c - 2, which every wave finished before the barrier of chunk c - 1
-        bf16* xt = xs + (i & 1) * 32 * XS;
+        bf16* xt = xs + (i & 1) * XIMG;
         bf16* at = as + (i & 1) * AIMG;
 #pragma unroll
         for (int j = 0; j < NA; ++j) *reinterpret_cast<bf16x8*>(at + (ar + (256 / TPA) * j) * XS + ac) = areg[j];
@@ -136,16 +154,18 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
             areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * (256 / TPA) * P.K + (c + 1) * KC);
         }
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          if (drop) drop8(xv[v], key, eidx + (uint64_t)c * KC + 8 * v, thr, sc);
-          if (xdst != nullptr) *reinterpret_cast<bf16x8*>(xdst + c * KC + 8 * v) = xv[v];
-          *reinterpret_cast<bf16x8*>(xt + lr * XS + lc + 8 * v) = xv[v];
-        }
+        for (int u = 0; u < TB; ++u)
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            if (drop) drop8(xv[u][v], key, eidx[u] + (uint64_t)c * KC + 8 * v, thr, sc);
+            if (xdst[u] != nullptr) *reinterpret_cast<bf16x8*>(xdst[u] + c * KC + 8 * v) = xv[u][v];
+            *reinterpret_cast<bf16x8*>(xt + (lr + 32 * u) * XS + lc + 8 * v) = xv[u][v];
+          }
         __syncthreads();
 #pragma unroll
         for (int s2 = 0; s2 < KSW; ++s2) {
-          const int kk = (KSW * w + s2) * 16 + 8 * h;
-          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xt + l32 * XS + kk);
+          const int kk = (KSW * ksl + s2) * 16 + 8 * h;
+          const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xt + (32 * tt + l32) * XS + kk);
 #pragma unroll
           for (int rb = 0; rb < RB; ++rb)
             acc[rb] = mfma32x32x16(*reinterpret_cast<const bf16x8*>(at + (rb * 32 + l32) * XS + kk), xf, acc[rb]);
@@ -153,32 +173,38 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
       }
     }
   }
-  // reduce the four waves' k-step partial sums: waves 1-3 -> LDS (over the images), wave 0 sums
+  // reduce the k-slices of each token tile: waves of slice > 0 -> LDS (over the images), the
+  // slice-0 wave of the tile sums
   __syncthreads();
-  float* red = reinterpret_cast<float*>(smem);  // [3][RB * 16 * 64]
-  if (w > 0) {
+  float* red = reinterpret_cast<float*>(smem);  // [TB][NSL - 1][RB * 16 * 64]
+  if (ksl > 0) {
+    float* dst = red + (tt * (NSL - 1) + ksl - 1) * RB * 1024;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[(w - 1) * RB * 1024 + (rb * 16 + r) * 64 + lane] = acc[rb][r];
+      for (int r = 0; r < 16; ++r) dst[(rb * 16 + r) * 64 + lane] = acc[rb][r];
   }
   __syncthreads();
-  const int64_t tok = t0 + l32;
-  if (w == 0 && tok < P.M && P.ksplit > 1) {
+  if (ksl > 0) return;
+  const float* src_red = red + tt * (NSL - 1) * RB * 1024;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ix = (rb * 16 + r) * 64 + lane;
+#pragma unroll
+      for (int q = 0; q < NSL - 1; ++q) acc[rb][r] += src_red[q * RB * 1024 + ix];
+    }
+  const int64_t tok = t0 + 32 * tt + l32;
+  if (tok < P.M && P.ksplit > 1) {
     float* prow = P.hpart + ((int64_t)ksi * P.M + tok) * R;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        f32x4 v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int ix = (rb * 16 + 4 * q + j) * 64 + lane;
-          v[j] = acc[rb][4 * q + j] + red[ix] + red[RB * 1024 + ix] + red[2 * RB * 1024 + ix];
-        }
-        *reinterpret_cast<f32x4*>(prow + rb * 32 + 8 * q + 4 * h) = v;
-      }
-  } else if (w == 0 && tok < P.M) {
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(prow + rb * 32 + 8 * q + 4 * h) =
+            f32x4{acc[rb][4 * q], acc[rb][4 * q + 1], acc[rb][4 * q + 2], acc[rb][4 * q + 3]};
+  } else if (tok < P.M) {
     bf16* hrow = static_cast<bf16*>(P.h) + tok * (P.ldh > 0 ? P.ldh : (int64_t)R);
     const float hs = P.hscale;
 #pragma unroll
@@ -187,10 +213,7 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
       for (int q = 0; q < 4; ++q) {
         bf16x4 v;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int ix = (rb * 16 + 4 * q + j) * 64 + lane;
-          v[j] = static_cast<bf16>((acc[rb][4 * q + j] + red[ix] + red[RB * 1024 + ix] + red[2 * RB * 1024 + ix]) * hs);
-        }
+        for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(acc[rb][4 * q + j] * hs);
         *reinterpret_cast<bf16x4*>(hrow + rb * 32 + 8 * q + 4 * h) = v;
       }
   }
@@ -221,14 +244,20 @@ __global__ __launch_bounds__(256) void lora_hsum_kernel(const float* __restrict_
 // and every thread then finishes four 8-column chunks: mask, scale, add, 16 B store.
 constexpr int DX_TS = 132;  // fp32 tile row: 128 + 4 so the f32x4 writes of 32 rows spread over banks
 
+// R > 128: the images hold a 64-wide slice of R at a time (a loop over the slices), so the
+// workgroup's LDS stays at the fp32 tile's 33 KiB and 4 workgroups fit per CU (R = 192 at full
+// width: 77 KiB, 2 per CU, ~2.8x the dX read-modify-write floor; profiles/r3_pmc_kernel_zoo.md).
+template <int RS>
+constexpr int lora_dx_slice() { return RS > 8 ? 64 : 16 * RS; }
 template <int RS>
 constexpr int lora_dx_lds_bytes() {
-  return (192 * (16 * RS + 8) * 2) > (64 * DX_TS * 4) ? (192 * (16 * RS + 8) * 2) : (64 * DX_TS * 4);
+  return (192 * (lora_dx_slice<RS>() + 8) * 2) > (64 * DX_TS * 4) ? (192 * (lora_dx_slice<RS>() + 8) * 2)
+                                                                    : (64 * DX_TS * 4);
 }
 
 template <int RS>  // R = 16 * RS
 __global__ __launch_bounds__(256) void lora_dx_kernel(const LoraDxParams P) {
-  constexpr int R = 16 * RS, RP = R + 8;  // padded image row (bf16)
+  constexpr int R = 16 * RS, SW = lora_dx_slice<RS>(), RP = SW + 8;  // slice width, padded image row (bf16)
   __shared__ __attribute__((aligned(16))) char smem[lora_dx_lds_bytes<RS>()];
   bf16* gimg = reinterpret_cast<bf16*>(smem);  // [64][RP]
   bf16* aimg = gimg + 64 * RP;                 // [128][RP]
@@ -251,33 +280,37 @@ __global__ __launch_bounds__(256) void lora_dx_kernel(const LoraDxParams P) {
     old[i] = bf16x8{};
     if (P.accumulate && tok < P.M) old[i] = *reinterpret_cast<const bf16x8*>(din + tok * ldi + kb * 128 + col);
   }
-  // images: R / 8 chunks of 16 B per row
-  constexpr int CPR = R / 8;
+  // images: SW / 8 chunks of 16 B per row
+  constexpr int CPR = SW / 8;
   const bf16* g = static_cast<const bf16*>(P.g);
   const bf16* at = static_cast<const bf16*>(P.at) + (int64_t)kb * 128 * R;
-#pragma unroll
-  for (int c = tid; c < 64 * CPR; c += 256) {
-    const int row = c / CPR, col = (c % CPR) * 8;
-    const int64_t tok = tb * 64 + row;
-    *reinterpret_cast<bf16x8*>(gimg + row * RP + col) =
-        *reinterpret_cast<const bf16x8*>(g + (tok < P.M ? tok : P.M - 1) * ldg + col);
-  }
-#pragma unroll
-  for (int c = tid; c < 128 * CPR; c += 256) {
-    const int row = c / CPR, col = (c % CPR) * 8;
-    *reinterpret_cast<bf16x8*>(aimg + row * RP + col) = *reinterpret_cast<const bf16x8*>(at + (int64_t)row * R + col);
-  }
-  __syncthreads();
   const int tl = (w & 1) * 32 + l32;  // this lane's token row within the tile (MFMA B operand)
   f32x16 acc[2];
+  acc[0] = f32x16{};
+  acc[1] = f32x16{};
+  for (int r0 = 0; r0 < R; r0 += SW) {
+    if (r0 > 0) __syncthreads();  // every wave is done with the previous slice's images
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    const int kl = (w >> 1) * 64 + cb * 32;  // column block within the tile
-    acc[cb] = f32x16{};
+    for (int c = tid; c < 64 * CPR; c += 256) {
+      const int row = c / CPR, col = (c % CPR) * 8;
+      const int64_t tok = tb * 64 + row;
+      *reinterpret_cast<bf16x8*>(gimg + row * RP + col) =
+          *reinterpret_cast<const bf16x8*>(g + (tok < P.M ? tok : P.M - 1) * ldg + r0 + col);
+    }
 #pragma unroll
-    for (int s = 0; s < RS; ++s)
-      acc[cb] = mfma32x32x16(*reinterpret_cast<const bf16x8*>(aimg + (kl + l32) * RP + 16 * s + 8 * h),
-                             *reinterpret_cast<const bf16x8*>(gimg + tl * RP + 16 * s + 8 * h), acc[cb]);  // D[k][token]
+    for (int c = tid; c < 128 * CPR; c += 256) {
+      const int row = c / CPR, col = (c % CPR) * 8;
+      *reinterpret_cast<bf16x8*>(aimg + row * RP + col) = *reinterpret_cast<const bf16x8*>(at + (int64_t)row * R + r0 + col);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int kl = (w >> 1) * 64 + cb * 32;  // column block within the tile
+#pragma unroll
+      for (int s = 0; s < SW / 16; ++s)
+        acc[cb] = mfma32x32x16(*reinterpret_cast<const bf16x8*>(aimg + (kl + l32) * RP + 16 * s + 8 * h),
+                               *reinterpret_cast<const bf16x8*>(gimg + tl * RP + 16 * s + 8 * h), acc[cb]);  // D[k][token]
+    }
   }
   __syncthreads();  // images consumed; the fp32 tile reuses the space
 #pragma unroll
@@ -363,27 +396,44 @@ bool lora_down_supported(int64_t M, int K, int R, int ldx, uint64_t offset) {
   return M > 0 && K % 128 == 0 && R % 32 == 0 && R >= 32 && R <= 256 && ldx % 8 == 0 && offset % 4 == 0;
 }
 
-int lora_down_splits(int64_t M, int K, int cus) {
-  // at least ~3 workgroups per CU (one workgroup = 32 tokens): a single 4-wave workgroup per CU
-  // leaves every per-chunk latency (A chunk from L2, barrier, LDS round trip) exposed
-  const int64_t ntb = (M + 31) / 32;
+// 32-token tiles per workgroup: 2 from R = 96 on (the A chunk loads dominate: qkv R = 192 72.8 -> 52.2 us,
+// gate_up R = 128 60.4 -> 45.5 us in the LoRA step); 1 at R = 64, where two tiles cost a workgroup
+// slot per CU (62.7 -> 73.5 us; profiles/r3_lora_grad_gemms.md). GRT_LORA_DOWN_TB=1/2 forces one.
+int lora_down_tb(int R) {
+  static const int env = [] { const char* e = getenv("GRT_LORA_DOWN_TB"); return e ? atoi(e) : 0; }();
+  if (env == 1 || env == 2) return env;
+  return R >= 96 ? 2 : 1;
+}
+
+int lora_down_splits(int64_t M, int K, int R, int cus) {
+  // at least ~3 workgroups per CU at one token tile per workgroup (a single 4-wave workgroup per CU
+  // leaves every per-chunk latency exposed); with two tiles per workgroup the A loads are halved
+  // and one split per workgroup slot (~1-2 per CU) keeps the fp32 partials small
+  const int tbw = lora_down_tb(R);
+  const int64_t ntb = (M + 32 * tbw - 1) / (32 * tbw);
   const int nch = K / 128;
-  int64_t ks = (3 * (int64_t)cus + ntb - 1) / ntb;
+  int64_t ks = ((tbw == 1 ? 3 : 1) * (int64_t)cus + ntb - 1) / ntb;
   if (ks > nch) ks = nch;
   if (ks > 16) ks = 16;
   return ks < 1 ? 1 : (int)ks;
 }
 
 void lora_down(const LoraDownParams& p, hipStream_t s) {
-  const dim3 grid((unsigned)(((p.M + 31) / 32) * p.ksplit)), block(256);
+  const int tbw = lora_down_tb(p.R);
+  const dim3 grid((unsigned)(((p.M + 32 * tbw - 1) / (32 * tbw)) * p.ksplit)), block(256);
   // GRT_LORA_DOWN_KC=64: half the LDS per workgroup (two workgroups per CU up to R = 192); measured
   // neutral on the Llama-2-7B LoRA step (profiles/r2_perf_experiments.md), so 128 by default
   static const int kc_env = [] { const char* e = getenv("GRT_LORA_DOWN_KC"); return e ? atoi(e) : 0; }();
   const bool kc64 = kc_env == 64;
-#define GRT_LD(N)                                                                         \
-  case N:                                                                                 \
-    if (kc64) hipLaunchKernelGGL((lora_down_kernel<N, 64>), grid, block, 0, s, p);        \
-    else hipLaunchKernelGGL((lora_down_kernel<N, 128>), grid, block, 0, s, p);            \
+#define GRT_LD(N)                                                                               \
+  case N:                                                                                       \
+    if (tbw == 1) {                                                                             \
+      if (kc64) hipLaunchKernelGGL((lora_down_kernel<N, 64, 1>), grid, block, 0, s, p);         \
+      else hipLaunchKernelGGL((lora_down_kernel<N, 128, 1>), grid, block, 0, s, p);             \
+    } else { /* R > 192: 64-column chunks (the 128-column images exceed the LDS) */            \
+      if (kc64) hipLaunchKernelGGL((lora_down_kernel<N, 64, 2>), grid, block, 0, s, p);         \
+      else hipLaunchKernelGGL((lora_down_kernel<N, (N >= 7 ? 64 : 128), 2>), grid, block, 0, s, p); \
+    }                                                                                           \
     break;
   switch (p.R / 32) {
     GRT_LD(1) GRT_LD(2) GRT_LD(3) GRT_LD(4) GRT_LD(5) GRT_LD(6) GRT_LD(7)

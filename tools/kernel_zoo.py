@@ -105,7 +105,17 @@ gl = torch.randn(T, 192, device=dev, dtype=bf)
 dxl = torch.randn(T, d, device=dev, dtype=bf)
 alt = al.t().contiguous()
 rep(lambda: C.lora_dx(gl, alt, dxl, 0.1, 1234, 0, True))
-del xl, al, gl, dxl, alt
+# adapter-gradient kernels (lora_grad.hip): g = s dY B (q target: dY column block of the fused qkv
+# gradient), dB = dY^T h', dA = g^T x_d (transposed out)
+dyl = torch.randn(T, 3 * d, device=dev, dtype=bf)
+btl = torch.randn(192, 3 * d, device=dev, dtype=bf) * 0.02
+gq = gl[:, :64]
+rep(lambda: C.lora_g(dyl[:, :d], btl[:64, :d], gq, 0.25, False))
+dbl = torch.empty(d, 64, device=dev, dtype=bf)
+rep(lambda: C.lora_tred(dyl[:, :d], gl[:, :64], dbl, 1.0, False, False))
+dal = torch.empty(192, d, device=dev, dtype=bf)
+rep(lambda: C.lora_tred(xl, gl, dal, 1.0, False, True))
+del xl, al, gl, dxl, alt, dyl, btl, dbl, dal
 
 # decode: GEMV (gate_up of Llama-3.1-8B, 1 token) and split-K decode attention (4K context)
 xw = torch.randn(1, 4096, device=dev, dtype=bf)
