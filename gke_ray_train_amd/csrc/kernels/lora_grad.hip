@@ -13,9 +13,8 @@
 // product; profiles/r3_lora_grad_gemms.md). Here each big operand is read once:
 //
 //   lora_g    C[M][64] (+)= alpha A[M][K] B[K][64], from B^T [64][K] (row stride ldbt).
-//             One workgroup = 128 rows (32 per wave) x one range of 128-column k-tiles; A and B^T
-//             tiles arrive by LDS-DMA into a 3-slot ring, B^T shared by the 4 waves; k-split fp32
-//             partials are summed by lora_g_fin.
+//             One workgroup = 32 rows x all of K; A and B^T tiles arrive by LDS-DMA into a 4-slot
+//             ring shared by the 4 waves, which split each tile's k-steps and sum through LDS.
 //   lora_tred C = A^T H, A [M][N], H [M][R] (R = 64 / 128 / 192): the token-reduction products dB
 //             (A = dY_i, H = h'_i) and dA (A = x_d, H = g; stored transposed). One workgroup = 128
 //             columns of A x one range of tokens (split over M to fill the chip); A and H arrive in
@@ -64,8 +63,8 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // ---------------------------------------------------------------------------------------------
 // lora_g
 // ---------------------------------------------------------------------------------------------
-constexpr int G_NS = 3;                     // ring slots
-constexpr int G_SLOT = 4 * 8192 + 16384;    // A image (128 rows = four 32-row images) + B^T image (64 rows)
+constexpr int G_NS = 4;                     // ring slots
+constexpr int G_SLOT = 8192 + 16384;        // A image (32 rows) + B^T image (64 rows)
 
 template <int D>  // D DMA instructions per tile: wait until at most `pending` tiles are in flight
 __device__ __forceinline__ void wait_pending(int pending) {
@@ -74,32 +73,35 @@ __device__ __forceinline__ void wait_pending(int pending) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// One workgroup = 128 rows x one range of k-tiles (split over K to fill the chip). Per 128-column
-// k-tile the A rows (wave w: rows 32w..32w+31) and the 64 B^T rows arrive by LDS-DMA into a 3-slot
-// ring (swizzled images, counted vmcnt across raw s_barriers: attention.hip's pipeline); B^T is
-// shared by the 4 waves. (A per-wave register-staged version, B^T private per wave, ran at ~half the
-// HBM rate: every CU moved 3x the A bytes through its load path.)
+// One workgroup = 32 rows x all of K, so the grid is M / 32 workgroups and no k-split partials (or
+// finalize launch) are needed at M >= 8 K. Per 128-column k-tile the 32 A rows and the 64 B^T rows
+// arrive by LDS-DMA into a 4-slot ring (swizzled images, counted vmcnt across raw s_barriers:
+// attention.hip's pipeline), both shared by the 4 waves; wave w takes k-steps 2w, 2w + 1 of each
+// tile, and the 4 partial 32x64 tiles are summed through LDS at the end. (Earlier forms, per-wave
+// private images with register staging — B^T re-read per wave — ran at ~half the HBM rate; 128-row
+// workgroups needed a 4-way k-split and a finalize launch per product: profiles/r3_lora_grad_gemms.md.)
+// With fewer than 256 row blocks the k-tiles are split over ks workgroups (fp32 partials, lora_g_fin).
 __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
   __shared__ __attribute__((aligned(16))) char smem[G_NS * G_SLOT];
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4, l16 = lane & 15;
-  const int nrb = (int)((P.M + 127) / 128);
+  const int nrb = (int)((P.M + 31) / 32);
   const int rb = blockIdx.x % nrb, ksi = blockIdx.x / nrb;
-  const int64_t m0 = (int64_t)rb * 128;
+  const int64_t m0 = (int64_t)rb * 32;
   const int nkt_all = P.K / 128;
   const int kt0 = ksi * nkt_all / P.ks;
   const int nt = (ksi + 1) * nkt_all / P.ks - kt0;
   const bf16* A = static_cast<const bf16*>(P.a);
   const bf16* BT = static_cast<const bf16*>(P.bt);
-  // DMA sources: wave w fills A image w (its 32 rows, 8 pieces of 4 rows) and B^T rows 16w..16w+15
+  // DMA sources: wave w fills A rows 8w..8w+7 (2 pieces of 4 rows) and B^T rows 16w..16w+15
   // (4 pieces); piece row 4p + g4, the XOR swizzle on the per-lane source chunk
-  const bf16* asrc[8];
+  const bf16* asrc[2];
 #pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int r = 4 * p + g4;
-    const int64_t m = min(m0 + 32 * w + r, P.M - 1);
-    asrc[p] = A + m * P.lda + (int64_t)kt0 * 128 + 8 * (l16 ^ swz16(r));
+  for (int q = 0; q < 2; ++q) {
+    const int r = 8 * w + 4 * q + g4;
+    const int64_t m = min(m0 + r, P.M - 1);
+    asrc[q] = A + m * P.lda + (int64_t)kt0 * 128 + 8 * (l16 ^ swz16(r));
   }
   const bf16* bsrc[4];
 #pragma unroll
@@ -110,10 +112,10 @@ __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
   const uint32_t smem0 = lds_addr(smem);
   auto dma_tile = [&](int t, int slot) {
     const uint32_t base = smem0 + (uint32_t)(slot * G_SLOT);
-    const uint32_t da = __builtin_amdgcn_readfirstlane(base + (uint32_t)(w * 8192));
-    const uint32_t db = __builtin_amdgcn_readfirstlane(base + (uint32_t)(32768 + 16 * w * 256));
+    const uint32_t da = __builtin_amdgcn_readfirstlane(base + (uint32_t)(8 * w * 256));
+    const uint32_t db = __builtin_amdgcn_readfirstlane(base + (uint32_t)(8192 + 16 * w * 256));
 #pragma unroll
-    for (int p = 0; p < 8; ++p) dma16(asrc[p] + t * 128, da + p * 1024);
+    for (int q = 0; q < 2; ++q) dma16(asrc[q] + t * 128, da + q * 1024);
 #pragma unroll
     for (int q = 0; q < 4; ++q) dma16(bsrc[q] + t * 128, db + q * 1024);
   };
@@ -124,47 +126,56 @@ __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
     for (int t = 0; t < nt; ++t) {
       const int slot = t % G_NS;
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of slot t-1 are done
-      wait_pending<12>(min(nt, t + G_NS - 1) - (t + 1));  // tile t landed (this wave's pieces)
+      wait_pending<6>(min(nt, t + G_NS - 1) - (t + 1));   // tile t landed (this wave's pieces)
       __builtin_amdgcn_s_barrier();                        // ... every wave's; slot t-1 free
       if (t + G_NS - 1 < nt) dma_tile(t + G_NS - 1, (t + G_NS - 1) % G_NS);
-      const char* ai = smem + slot * G_SLOT + w * 8192;
-      const char* bi = smem + slot * G_SLOT + 32768;
+      const char* ai = smem + slot * G_SLOT;
+      const char* bi = ai + 8192;
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ai + img_byte(l32, 2 * ks + hh));
-        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(bi + img_byte(l32, 2 * ks + hh));
-        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(bi + img_byte(32 + l32, 2 * ks + hh));
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int ch = 2 * (2 * w + s2) + hh;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ai + img_byte(l32, ch));
+        const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(bi + img_byte(l32, ch));
+        const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(bi + img_byte(32 + l32, ch));
         acc0 = mfma_bf16_32(af, b0, acc0);
         acc1 = mfma_bf16_32(af, b1, acc1);
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // D[row][col]: lane -> column l32 (acc0) / 32 + l32 (acc1), register r -> row acc_row32(r, hh)
-  if (P.ks > 1) {  // fp32 partial of this k range; lora_g_fin sums them
-    float* ws = P.ws + (int64_t)ksi * P.M * 64;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int64_t m = m0 + 32 * w + acc_row32(r, hh);
-      if (m < P.M) {
-        ws[m * 64 + l32] = acc0[r];
-        ws[m * 64 + 32 + l32] = acc1[r];
-      }
-    }
-    return;
-  }
-  bf16* C = static_cast<bf16*>(P.c);
+  __syncthreads();  // ring consumed: the space takes the 4 partial tiles
+  float* part = reinterpret_cast<float*>(smem);  // [4 waves][32 rows][64 cols]
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const int64_t m = m0 + 32 * w + acc_row32(r, hh);
-    if (m < P.M) {
-      bf16* c = C + m * P.ldc;
-      const float o0 = P.alpha * acc0[r] + (P.accumulate ? static_cast<float>(c[l32]) : 0.f);
-      const float o1 = P.alpha * acc1[r] + (P.accumulate ? static_cast<float>(c[32 + l32]) : 0.f);
-      c[l32] = static_cast<bf16>(o0);
-      c[32 + l32] = static_cast<bf16>(o1);
-    }
+    part[w * 2048 + acc_row32(r, hh) * 64 + l32] = acc0[r];
+    part[w * 2048 + acc_row32(r, hh) * 64 + 32 + l32] = acc1[r];
   }
+  __syncthreads();
+  const int row = tid >> 3, c8 = (tid & 7) * 8;
+  const int64_t m = m0 + row;
+  if (m >= P.M) return;
+  float sum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sum[e] = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(&part[q * 2048 + row * 64 + c8]);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(&part[q * 2048 + row * 64 + c8 + 4]);
+    sum[0] += a[0]; sum[1] += a[1]; sum[2] += a[2]; sum[3] += a[3];
+    sum[4] += b[0]; sum[5] += b[1]; sum[6] += b[2]; sum[7] += b[3];
+  }
+  if (P.ks > 1) {  // fp32 partial of this k range; lora_g_fin sums them
+    float* ws = P.ws + ((int64_t)ksi * P.M + m) * 64 + c8;
+    *reinterpret_cast<f32x4*>(ws) = f32x4{sum[0], sum[1], sum[2], sum[3]};
+    *reinterpret_cast<f32x4*>(ws + 4) = f32x4{sum[4], sum[5], sum[6], sum[7]};
+    return;
+  }
+  bf16* C = static_cast<bf16*>(P.c) + m * P.ldc + c8;
+  bf16x8 o;
+  const bf16x8 old = P.accumulate ? *reinterpret_cast<const bf16x8*>(C) : bf16x8{};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = static_cast<bf16>(P.alpha * sum[e] + (P.accumulate ? static_cast<float>(old[e]) : 0.f));
+  *reinterpret_cast<bf16x8*>(C) = o;
 }
 
 // C[m][0..63] (+)= alpha * sum_k ws[k][m][..]
@@ -315,9 +326,10 @@ __global__ __launch_bounds__(256) void lora_tred_fin_kernel(const LoraTredParams
 
 bool lora_g_supported(int64_t M, int K, int r) { return M > 0 && K > 0 && K % 128 == 0 && r == 64; }
 
-// k splits: one workgroup per CU (144 KiB of LDS each), at most 8 and at most the k-tiles
+// k splits: only when the 32-row blocks leave a quarter of the CUs idle (one 96 KiB workgroup per CU); at most 8
 int lora_g_splits(int64_t M, int K, int cus) {
-  const int64_t nrb = (M + 127) / 128;
+  const int64_t nrb = (M + 31) / 32;
+  if (4 * nrb >= 3 * (int64_t)cus) return 1;  // >= 3/4 of the CUs busy: no partials, no finalize launch
   int ks = (int)((cus + nrb - 1) / nrb);
   if (ks > 8) ks = 8;
   if (ks > K / 128) ks = K / 128;
@@ -325,7 +337,7 @@ int lora_g_splits(int64_t M, int K, int cus) {
 }
 
 void lora_g(const LoraGParams& p, hipStream_t s) {
-  const dim3 grid((unsigned)(((p.M + 127) / 128) * p.ks)), block(256);
+  const dim3 grid((unsigned)(((p.M + 31) / 32) * p.ks)), block(256);
   hipLaunchKernelGGL(lora_g_kernel, grid, block, 0, s, p);
   if (p.ks > 1) {
     int64_t fb = (p.M * 16 + 255) / 256;
