@@ -353,11 +353,17 @@ class Dataset:
         addr, key = obj[0]
         return StreamSplit(addr, key, rank, world)
 
-    def shard_for_rank(self, rank: int, world: int) -> "DataIterator":
-        """Static block-level shard: rank r executes only source blocks r, r + world, ... (1/world
-        of the work, no coordinator). Row counts match across ranks when blocks are equal-sized
-        and the transforms keep lengths; use ``streaming_split`` for exact balancing."""
-        return DataIterator(self, rank, world, True)
+    def shard_for_rank(self, rank: int, world: int, equal: bool = True) -> "DataIterator":
+        """Static per-rank shard without a coordinator.
+
+        ``equal=True`` (what ``train.get_dataset_shard`` uses): every rank gets exactly
+        floor(rows / world) rows — rank r takes row r of every complete round of ``world`` rows of
+        the one execution order — so data-parallel ranks run the same number of steps (unequal
+        counts would hang DDP collectives) whatever the block sizes or length-changing transforms.
+        Each rank executes the whole pipeline for that. ``equal=False``: rank r executes only source
+        blocks r, r + world, ... (1/world of the work); counts can differ. ``streaming_split`` gives
+        exact balance with one execution."""
+        return DataIterator(self, rank, world, equal)
 
     # ------------------------------------------------------------------ iteration
     def iter_rows(self):
@@ -419,14 +425,26 @@ def _window_shuffle(blocks: Iterator[Block], seed: int, window: int) -> Iterator
 
 
 class DataIterator:
-    """Static per-rank shard (``Dataset.shard_for_rank``): executes source blocks rank::world."""
+    """Static per-rank shard (``Dataset.shard_for_rank``): equal row rounds, or source blocks
+    rank::world when ``equal`` is False."""
 
     def __init__(self, ds: Dataset, rank: int, world: int, equal: bool = True):
         self.ds, self.rank, self.world, self.equal = ds, rank, world, equal
 
     def _blocks(self):
-        order = self.ds._source_order()
-        yield from self.ds._stream(source=order[self.rank::self.world])
+        if not self.equal or self.world == 1:
+            order = self.ds._source_order()
+            yield from self.ds._stream(source=order[self.rank::self.world])
+            return
+        carry: Block = {}
+        for b in self.ds._stream():
+            cur = _concat([carry, b]) if _block_len(carry) else b
+            n = _block_len(cur)
+            full = n // self.world * self.world
+            if full:
+                yield {k: v[self.rank:full:self.world] for k, v in cur.items()}
+            carry = _slice(cur, full, n)
+        # the incomplete last round is dropped on every rank
 
     def iter_rows(self):
         for b in self._blocks():
@@ -477,6 +495,7 @@ class _CoordinatorState:
         self.cv = threading.Condition()
         self.epoch = -1
         self.finished = [True] * n              # split i received the end of the current epoch
+        self.abandoned = [False] * n            # split i stopped consuming the current epoch early
         self.queues = [collections.deque() for _ in range(n)]
         self.qbytes = [0] * n
         self.done = True
@@ -488,6 +507,7 @@ class _CoordinatorState:
         self.epoch += 1
         self.stats["epochs"] += 1
         self.finished = [False] * self.n
+        self.abandoned = [False] * self.n
         self.queues = [collections.deque() for _ in range(self.n)]
         self.qbytes = [0] * self.n
         self.done = False
@@ -498,7 +518,7 @@ class _CoordinatorState:
             while any(q > self.cap for q in self.qbytes) and not self.error:
                 self.cv.wait(0.5)  # backpressure: a slow consumer's queue is full
             for i, p in enumerate(parts):
-                if _block_len(p):
+                if _block_len(p) and not self.abandoned[i]:
                     self.queues[i].append(p)
                     self.qbytes[i] += sum(v.nbytes for v in p.values())
                     self.stats["rows_dealt"][i] += _block_len(p)
@@ -541,6 +561,8 @@ class _CoordinatorState:
             while True:
                 if self.error:
                     return ("error", self.error)
+                if self.abandoned[i]:
+                    return ("end", None)
                 if self.queues[i]:
                     b = self.queues[i].popleft()
                     self.qbytes[i] -= sum(v.nbytes for v in b.values())
@@ -552,6 +574,17 @@ class _CoordinatorState:
                     return ("end", None)
                 self.cv.wait(0.5)
 
+    def _abandon(self, i: int, epoch: int):
+        """Split i stopped iterating epoch ``epoch``: drop its queue, count it as finished."""
+        with self.cv:
+            if epoch != self.epoch or self.finished[i]:
+                return
+            self.abandoned[i] = True
+            self.finished[i] = True
+            self.queues[i].clear()
+            self.qbytes[i] = 0
+            self.cv.notify_all()
+
     def _client(self, conn):
         from ..runtime import object_store
         try:
@@ -560,6 +593,9 @@ class _CoordinatorState:
                 if msg[0] == "next":
                     kind, val = self._next(msg[1], msg[2])
                     conn.send_bytes(object_store.pack((kind, val)))
+                elif msg[0] == "abandon":
+                    self._abandon(msg[1], msg[2])
+                    conn.send_bytes(object_store.pack(("ok", None)))
                 elif msg[0] == "stats":
                     conn.send_bytes(object_store.pack(("stats", dict(self.stats, epoch=self.epoch))))
                 elif msg[0] == "close":
@@ -637,12 +673,16 @@ class StreamSplit:
         self._epoch = -1
         self._coordinator = None
 
-    def _call(self, msg):
+    def _connect(self):
         from multiprocessing.connection import Client
+        return Client(tuple(self.address), authkey=self.authkey)
 
+    def _call(self, msg):
+        """Control requests (stats, abandon) on this handle's own connection; the per-epoch block
+        stream uses a separate connection, so the two never interleave."""
         from ..runtime import object_store
         if self._conn is None:
-            self._conn = Client(tuple(self.address), authkey=self.authkey)
+            self._conn = self._connect()
         self._conn.send(msg)
         return object_store.unpack(self._conn.recv_bytes())
 
@@ -650,28 +690,63 @@ class StreamSplit:
         return self._call(("stats",))[1]
 
     def _blocks(self, ahead: int = 2) -> Iterator[Block]:
+        """One epoch. A consumer may stop early (break on max_steps): closing this generator stops
+        the pull thread and tells the coordinator the split abandoned the epoch, so epoch e + 1 can
+        start for every split (Ray starts the next epoch the same way, on the remaining requests)."""
+        from ..runtime import object_store
         self._epoch += 1
         epoch = self._epoch
         q: "queue.Queue" = queue.Queue(maxsize=max(1, ahead))
+        stop = threading.Event()
+
+        def put(item) -> bool:
+            while not stop.is_set():
+                try:
+                    q.put(item, timeout=0.2)
+                    return True
+                except queue.Full:
+                    continue
+            return False
 
         def pull():  # overlap the next request's round trip with the consumer's work
+            conn = None
             try:
-                while True:
-                    kind, val = self._call(("next", self.index, epoch))
-                    q.put((kind, val))
-                    if kind != "block":
+                conn = self._connect()
+                while not stop.is_set():
+                    conn.send(("next", self.index, epoch))
+                    kind, val = object_store.unpack(conn.recv_bytes())
+                    if not put((kind, val)) or kind != "block":
                         return
             except BaseException:
-                q.put(("error", traceback.format_exc()))
+                if not stop.is_set():
+                    put(("error", traceback.format_exc()))
+            finally:
+                if conn is not None:
+                    try:
+                        conn.send(("close",))
+                        conn.close()
+                    except OSError:
+                        pass
         threading.Thread(target=pull, daemon=True, name="grt-split-pull").start()
-        while True:
-            kind, val = q.get()
-            if kind == "block":
-                yield val
-            elif kind == "end":
-                return
-            else:
-                raise RuntimeError(f"streaming_split coordinator failed:\n{val}")
+        ended = False
+        try:
+            while True:
+                kind, val = q.get()
+                if kind == "block":
+                    yield val
+                elif kind == "end":
+                    ended = True
+                    return
+                else:
+                    ended = True
+                    raise RuntimeError(f"streaming_split coordinator failed:\n{val}")
+        finally:
+            stop.set()
+            if not ended:
+                try:
+                    self._call(("abandon", self.index, epoch))
+                except (OSError, EOFError):
+                    pass
 
     def iter_rows(self):
         for b in self._blocks():
@@ -732,29 +807,63 @@ def _fmt(b: Block, fmt: str):
     return b
 
 
+class _Handoff:
+    """Bounded producer -> consumer queue of a background thread. When the consumer stops early
+    (its generator is closed), ``stop`` is set and the producer's ``put`` gives up instead of
+    blocking forever; the producer then closes its own source so upstream stages (a streaming
+    split's pull thread, the coordinator's epoch) are released too."""
+
+    def __init__(self, depth: int):
+        self.q: "queue.Queue" = queue.Queue(maxsize=max(1, depth))
+        self.stop = threading.Event()
+
+    def put(self, item) -> bool:
+        while not self.stop.is_set():
+            try:
+                self.q.put(item, timeout=0.2)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def close_source(self, it):
+        if self.stop.is_set() and hasattr(it, "close"):
+            try:
+                it.close()
+            except BaseException:  # noqa: BLE001 - best effort on an abandoned source
+                pass
+
+
 def _prefetch(it: Iterator, depth: int) -> Iterator:
     """Run ``it`` on a background thread ``depth`` items ahead (``prefetch_batches``)."""
     if depth <= 0:
         yield from it
         return
-    q: "queue.Queue" = queue.Queue(maxsize=depth)
+    h = _Handoff(depth)
     end = object()
 
     def run():
         try:
             for x in it:
-                q.put((True, x))
-            q.put((True, end))
+                if not h.put((True, x)):
+                    break
+            else:
+                h.put((True, end))
         except BaseException as e:  # noqa: BLE001 - re-raised in the consumer
-            q.put((False, e))
+            h.put((False, e))
+        finally:
+            h.close_source(it)
     threading.Thread(target=run, daemon=True, name="grt-prefetch").start()
-    while True:
-        ok, x = q.get()
-        if not ok:
-            raise x
-        if x is end:
-            return
-        yield x
+    try:
+        while True:
+            ok, x = h.q.get()
+            if not ok:
+                raise x
+            if x is end:
+                return
+            yield x
+    finally:
+        h.stop.set()
 
 
 _NP_OF_TORCH = None
@@ -815,7 +924,7 @@ class _PinnedH2D:
         nslot = self.depth + 1
         slots: List[Dict[str, torch.Tensor]] = [dict() for _ in range(nslot)]
         done: List[Optional[torch.cuda.Event]] = [None] * nslot
-        q: "queue.Queue" = queue.Queue(maxsize=self.depth)
+        h = _Handoff(self.depth)
         end = object()
 
         def produce():
@@ -851,25 +960,32 @@ class _PinnedH2D:
                     ev = torch.cuda.Event()
                     ev.record(copy)
                     done[s] = ev
-                    q.put((True, (out, ev)))
-                q.put((True, end))
+                    if not h.put((True, (out, ev))):
+                        break
+                else:
+                    h.put((True, end))
             except BaseException as e:  # noqa: BLE001
-                q.put((False, e))
+                h.put((False, e))
+            finally:
+                h.close_source(batches)
 
         threading.Thread(target=produce, daemon=True, name="grt-h2d").start()
-        while True:
-            ok, item = q.get()
-            if not ok:
-                raise item
-            if item is end:
-                return
-            out, ev = item
-            cur = torch.cuda.current_stream(dev)
-            cur.wait_event(ev)
-            for t in out.values():
-                if isinstance(t, torch.Tensor) and t.is_cuda:
-                    t.record_stream(cur)
-            yield out
+        try:
+            while True:
+                ok, item = h.q.get()
+                if not ok:
+                    raise item
+                if item is end:
+                    return
+                out, ev = item
+                cur = torch.cuda.current_stream(dev)
+                cur.wait_event(ev)
+                for t in out.values():
+                    if isinstance(t, torch.Tensor) and t.is_cuda:
+                        t.record_stream(cur)
+                yield out
+        finally:
+            h.stop.set()
 
 
 # module-level constructors (ray.data.from_items / range / read_text ...)

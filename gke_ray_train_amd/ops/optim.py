@@ -273,15 +273,23 @@ class OffloadedAdamW(FusedAdamW):
         comp.wait_stream(up)
 
 
+_EIGHT_BIT = ("paged_adamw_8bit", "adamw_8bit", "adamw_bnb_8bit", "paged_adamw8bit", "adamw8bit")
+
+
 def make_optimizer(name: str, params, lr: float, weight_decay: float, betas=(0.9, 0.999), eps=1e-8,
                    master_weights=False, offload: bool = False):
     """Optimizer by HF ``optim`` name. ``offload=True`` keeps AdamW moments in pinned host memory
     (OffloadedAdamW) — only worthwhile when HBM cannot hold them (e.g. 70B on one node)."""
     name = (name or "adamw_torch").lower()
+    if name in _EIGHT_BIT:
+        # bitsandbytes' 8-bit AdamW keeps block-quantized moments: a different algorithm and memory
+        # footprint. Substituting 32-bit states silently would change both, so refuse loudly.
+        raise ValueError(f"optimizer {name!r} (8-bit block-quantized AdamW states) is not implemented; use "
+                         "'paged_adamw_32bit' / 'adamw_torch' (fp32 states, the reference config's choice)")
     if offload and name.startswith(("adamw", "paged_adamw", "fused_adamw")):
         return OffloadedAdamW(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
     if name in ("adamw", "adamw_torch", "adamw_hf", "adamw_32bit", "paged_adamw_32bit", "adamw_torch_fused",
-                "fused_adamw", "paged_adamw_8bit", "adamw_8bit"):
+                "fused_adamw"):
         return FusedAdamW(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
                           master_weights=master_weights)
     if name == "sgd":

@@ -118,7 +118,8 @@ def activation_bytes(cfg, tokens: int, checkpointing: bool, dtype_bytes: int = 2
 def plan_memory(cfg, world: int, parallel: str = "ddp", offload: bool = False, peft: str = "none",
                 micro_batch: int = 8, seq: int = 1024, zero: Optional[bool] = None, checkpointing: bool = False,
                 lora_r: int = 64, overlap_opt: Optional[bool] = None, hbm_capacity: Optional[float] = None,
-                host_capacity: Optional[float] = None, offload_chunk_elems: int = 1 << 26) -> MemoryPlan:
+                host_capacity: Optional[float] = None, offload_chunk_elems: int = 1 << 26,
+                lora_dropout: float = 0.1, lora_kcat: Optional[bool] = None) -> MemoryPlan:
     """Per-rank memory plan for ``cfg`` (a ``LlamaConfig``) at ``world`` ranks."""
     P = float(cfg.num_params())
     B = 2.0  # bf16 parameters / gradients
@@ -161,19 +162,35 @@ def plan_memory(cfg, world: int, parallel: str = "ddp", offload: bool = False, p
         return plan
     # DDP (replicated parameters)
     if peft in ("lora", "qlora"):
-        t = cfg.num_hidden_layers * lora_r * (  # A [r, in] + B [out, r] for q, k, v, o, gate, up, down
-            (cfg.hidden_size + cfg.hidden_size) * 2 + (cfg.hidden_size + cfg.num_key_value_heads * cfg.head_dim) * 2
-            + (cfg.hidden_size + cfg.intermediate_size) * 3)
-        lin = cfg.num_hidden_layers * (cfg.hidden_size * (cfg.hidden_size * 2 + 2 * cfg.num_key_value_heads * cfg.head_dim)
-                                       + 3 * cfg.hidden_size * cfg.intermediate_size)
-        if peft == "qlora":  # NF4 codes (0.5 B) + fp32 absmax per 64 + the bf16 embeddings / head / norms
-            hbm["frozen_base"] = lin * (0.5 + 4.0 / 64) + (P - lin) * B
+        h, f = cfg.hidden_size, cfg.intermediate_size
+        kvd = cfg.num_key_value_heads * cfg.head_dim
+        L, r = cfg.num_hidden_layers, lora_r
+        t = L * r * (  # A [r, in] + B [out, r] for q, k, v, o, gate, up, down
+            (h + h) * 2 + (h + kvd) * 2 + (h + f) * 3)
+        lin = L * (h * (h * 2 + 2 * kvd) + 3 * h * f)
+        # adapted modules per layer (peft/lora.py LoraLinear on the fused projections):
+        # (out_features, R = r x targets): qkv, o, gate_up, down
+        mods = [(h + 2 * kvd, 3 * r), (h, r), (2 * f, 2 * r), (h, r)]
+        kcat = (r % 64 == 0 and h % 128 == 0 and f % 128 == 0 and os.environ.get("GRT_LORA_KCAT", "1") != "0") \
+            if lora_kcat is None else lora_kcat
+        tails = L * sum(o * R for o, R in mods)
+        if peft == "qlora":  # NF4 codes (0.5 B) + fp32 absmax per 64
+            hbm["frozen_nf4_codes"] = lin * (0.5 + 4.0 / 64)
+        hbm["frozen_unadapted"] = (P - lin) * B  # embeddings, LM head, norms
+        if kcat:
+            # K-concatenated W' = [W | B blocks] (bf16; for LoRA the base weight is a view of it, for
+            # QLoRA it replaces the dequant cache) + the B^T buffer of the adapter-gradient kernel
+            hbm["frozen_kcat_weight"] = (lin + tails) * B
+            hbm["lora_bt"] = tails * B if r == 64 else 0.0
         else:
-            hbm["frozen_base"] = P * B
-        hbm["frozen_base_transposed"] = lin * B if peft == "lora" else 0.0  # cached W^T for TN dX GEMMs
+            hbm["frozen_base"] = lin * B  # bf16 weight, or the resident NF4 dequant cache
+        hbm["frozen_base_transposed"] = lin * B  # cached W^T of the TN dX GEMMs (both peft kinds)
         hbm["adapters"] = t * B
         hbm["adapter_grads"] = t * B
         hbm["adam_moments_fp32"] = 8.0 * t
+        # adapter activations: the dropped inputs x_d kept for dA (dropout > 0) and the h' tails
+        xd = L * (3 * h + f) * B if lora_dropout > 0 else 0.0
+        hbm["adapter_activations"] = tokens * (xd + L * sum(R for _, R in mods) * B)
         return plan
     zero = (world > 1) if zero is None else zero
     hbm["params"] = P * B

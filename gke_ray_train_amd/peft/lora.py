@@ -440,6 +440,11 @@ class LoraLinear(nn.Module):
             self._wk = wk
             if isinstance(self.base, NF4Linear):  # W' replaces the forward dequant cache (dX keeps W^T's)
                 self.base._w_cache = None
+            else:
+                # the frozen bf16 weight becomes a view of W'[:, :K]: its own storage is released, so
+                # the projection is held once (W') plus its W^T, not three times
+                del w
+                self.base.weight.data = wk[:, :K]
         if self._wk_order != list(order):  # block positions moved: clear the whole tail once
             self._wk[:, K:].zero_()
             self._wk_order = list(order)

@@ -447,11 +447,16 @@ class SFTTrainer:
                 L = int(L)
                 if L == 0:
                     continue
-                ids.append(b["input_ids"][r, :L])
-                labs.append(b["labels"][r, :L])
+                keep = b["attention_mask"][r] != 0
+                if bool(keep[:L].all()):  # right padding (the reference collator's): the row's prefix
+                    rid, rlab = b["input_ids"][r, :L], b["labels"][r, :L]
+                else:  # any other mask (left padding, holes): select the real tokens by the mask
+                    rid, rlab = b["input_ids"][r][keep], b["labels"][r][keep]
+                ids.append(rid)
+                labs.append(rlab)
                 wts.append(torch.full((L,), w))
                 lens.append(L)
-                ntarget += int((b["labels"][r, 1:L] != -100).sum())
+                ntarget += int((rlab[1:] != -100).sum())
         T = sum(lens)
         pad = (-T) % max(1, mult)
         mask = torch.ones(T + pad, dtype=torch.long)
@@ -491,7 +496,9 @@ class SFTTrainer:
         a = self.args
         if a.eval_padding_free is not None:
             return bool(a.eval_padding_free)
-        if os.environ.get("GRT_SFT_EVAL_PADDING_FREE", "1") == "0" or self.device.type != "cuda":
+        if os.environ.get("GRT_SFT_EVAL_PADDING_FREE", "1") == "0":
+            return False
+        if self.device.type != "cuda":
             return self._padding_free_enabled()
         import inspect
         inner = getattr(self.model, "base_model", self.model)

@@ -15,6 +15,8 @@ Run: ``python jobs/pytorch_llm_ray.py`` (all GPUs of the node) or
 from __future__ import annotations
 
 import argparse
+import hashlib
+import json
 import math
 import os
 import sys
@@ -46,6 +48,36 @@ def warmup_cosine(total_steps: int, warmup_ratio: float, min_lr_ratio: float):
     return f
 
 
+def _file_digest(path: str) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def _atomic_write(path: str, text: str) -> None:
+    tmp = f"{path}.tmp{os.getpid()}"
+    with open(tmp, "w") as f:
+        f.write(text)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
+def _prep_is_current(done_f: str, raw_digest: str, products) -> bool:
+    """True when the sentinel names this raw text and every product still has its recorded digest."""
+    try:
+        with open(done_f) as f:
+            rec = json.load(f)
+        if rec.get("raw_sha256") != raw_digest:
+            return False
+        return all(os.path.exists(p) and rec["products"].get(os.path.basename(p)) == _file_digest(p)
+                   for p in products)
+    except (OSError, ValueError, KeyError, AttributeError, TypeError):
+        return False  # missing, legacy "done" text, or torn: redo
+
+
 def _prepare_char_data(cfg, rank):
     """Rank 0 tokenizes the raw text once; the others wait on a store barrier (not a 5 s poll)."""
     import torch.distributed as dist
@@ -58,23 +90,29 @@ def _prepare_char_data(cfg, rank):
     done_f = os.path.join(out_dir, "_DATA_PREP_DONE")
     if rank == 0:
         os.makedirs(out_dir, exist_ok=True)
-        if not os.path.exists(done_f):
-            raw = cfg["raw_data_path"]
-            if not os.path.exists(raw):
-                wikitext.prepare(os.path.dirname(raw), scale=cfg.get("synthetic_scale", 1.0))
+        raw = cfg["raw_data_path"]
+        if not os.path.exists(raw):
+            wikitext.prepare(os.path.dirname(raw), scale=cfg.get("synthetic_scale", 1.0))
+        raw_digest = _file_digest(raw)
+        # The reference trusts any existing sentinel (ray-jobs/pytorch_llm_ray.py:160,176), so a
+        # changed raw file or a half-written earlier run is silently reused. Here the sentinel records
+        # the digests of the raw text and of every product; a mismatch redoes the preparation.
+        if not _prep_is_current(done_f, raw_digest, (ids_f, vocab_f, vs_f)):
             with open(raw, encoding="utf-8") as f:
                 text = f.read()
             tok = CharTokenizer()
             tok.fit_on_text(text)
-            tok.save_vocab(vocab_f)
+            tmp = vocab_f + ".tmp"
+            tok.save_vocab(tmp)
+            os.replace(tmp, vocab_f)
             ids = torch.from_numpy(tok.encode_np(text))
             tmp = ids_f + ".tmp"
             torch.save(ids, tmp)
             os.replace(tmp, ids_f)
-            with open(vs_f, "w") as f:
-                f.write(str(tok.vocab_size))
-            with open(done_f, "w") as f:
-                f.write("done")
+            _atomic_write(vs_f, str(tok.vocab_size))
+            record = {"raw": os.path.abspath(raw), "raw_sha256": raw_digest,
+                      "products": {os.path.basename(p): _file_digest(p) for p in (ids_f, vocab_f, vs_f)}}
+            _atomic_write(done_f, json.dumps(record, sort_keys=True))
             print(f"rank0: prepared {len(ids):,} chars, vocab {tok.vocab_size}", flush=True)
     if dist.is_initialized():
         dist.barrier()

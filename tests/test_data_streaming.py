@@ -70,7 +70,7 @@ def test_streaming_split_unequal_keeps_every_row():
     splits[0].shutdown()
 
 
-def test_shard_for_rank_executes_only_its_blocks():
+def test_shard_for_rank_partitions_rows():
     seen = []
     ds = Dataset.from_numpy({"x": np.arange(80)}, parallelism=8).map_batches(lambda b: {"x": b["x"]})
     parts = [[int(v) for b in ds.shard_for_rank(r, 2).iter_batches(batch_size=5) for v in b["x"]] for r in range(2)]
@@ -104,3 +104,48 @@ def test_torch_trainer_hands_each_worker_a_coordinated_split(tmp_path):
     finally:
         rt.shutdown()
     assert res.metrics["rows"] == 120 and res.metrics["kind"] == "StreamSplit"
+
+
+def test_streaming_split_consumer_breaks_early_then_next_epoch_runs():
+    """A split that stops iterating an epoch early (max_steps) must not wedge the coordinator:
+    the next epoch starts for every split and carries all rows again."""
+    import threading
+    ds = Dataset.from_numpy({"x": np.arange(400)}, parallelism=8)
+    splits = ds.streaming_split(2)
+    try:
+        got = {}
+
+        def consume(i, limit):
+            n = 0
+            for b in splits[i].iter_batches(batch_size=10):
+                n += len(b["x"])
+                if limit and n >= limit:
+                    break  # early exit in epoch 0
+            got[(i, 0)] = n
+            got[(i, 1)] = sorted(int(v) for b in splits[i].iter_batches(batch_size=10) for v in b["x"])
+
+        ts = [threading.Thread(target=consume, args=(0, 30)), threading.Thread(target=consume, args=(1, 0))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert not any(t.is_alive() for t in ts), "epoch 1 never started after an early break"
+        assert got[(0, 0)] == 30 and got[(1, 0)] == 200
+        assert len(got[(0, 1)]) == len(got[(1, 1)]) == 200
+        assert sorted(got[(0, 1)] + got[(1, 1)]) == list(range(400))
+    finally:
+        splits[0].shutdown()
+
+
+def test_shard_for_rank_equal_counts_with_uneven_blocks_and_filters():
+    """equal=True gives every rank the same row count even when blocks are uneven and a filter
+    changes lengths (unequal counts hang DDP collectives)."""
+    ds = Dataset.from_numpy({"x": np.arange(103)}, parallelism=5).filter(lambda r: r["x"] % 7 != 0)
+    parts = [[int(v) for b in ds.shard_for_rank(r, 3).iter_batches(batch_size=4) for v in b["x"]] for r in range(3)]
+    kept = [v for v in range(103) if v % 7 != 0]
+    assert len(parts[0]) == len(parts[1]) == len(parts[2]) == len(kept) // 3
+    assert sorted(parts[0] + parts[1] + parts[2]) == kept[: len(kept) // 3 * 3]
+    # equal=False: block-level shards (cheap), counts may differ
+    blk = [[int(v) for b in ds.shard_for_rank(r, 3, equal=False).iter_batches(batch_size=4) for v in b["x"]]
+           for r in range(3)]
+    assert sorted(blk[0] + blk[1] + blk[2]) == kept

@@ -49,3 +49,44 @@ def test_basic_llm_job_two_cpu_workers(tmp_path):
     rows = [json.loads(l) for l in open(os.path.join(trial, "result.json"))]
     assert [r["epoch"] for r in rows] == [1, 2]
     assert rows[1]["loss"] < rows[0]["loss"] + 1.0
+
+
+def test_data_prep_sentinel_is_atomic_and_tracks_the_raw_text(tmp_path):
+    """The sentinel records digests of the raw text and every product: a changed raw file, a legacy
+    "done" sentinel or a tampered product redoes the preparation (the reference trusts any sentinel,
+    ray-jobs/pytorch_llm_ray.py:160,176)."""
+    import torch
+    import pytorch_llm_ray as job
+    raw = tmp_path / "raw.txt"
+    raw.write_text("hello world\n" * 50)
+    cfg = {"processed_data_dir": str(tmp_path / "proc"), "raw_data_path": str(raw)}
+    ids, vocab = job._prepare_char_data(cfg, 0)
+    done = tmp_path / "proc" / "_DATA_PREP_DONE"
+    rec = json.loads(done.read_text())
+    assert rec["raw_sha256"] == job._file_digest(str(raw)) and set(rec["products"]) == {
+        "train.ids.pt", "char_vocab.json", "vocab_size.txt"}
+    assert not [f for f in os.listdir(tmp_path / "proc") if ".tmp" in f]
+    mtime = os.path.getmtime(tmp_path / "proc" / "train.ids.pt")
+    job._prepare_char_data(cfg, 0)  # unchanged: reused
+    assert os.path.getmtime(tmp_path / "proc" / "train.ids.pt") == mtime
+    raw.write_text("different text, new characters: XYZ\n" * 40)  # changed raw text: redone
+    ids2, vocab2 = job._prepare_char_data(cfg, 0)
+    assert vocab2 != vocab and len(ids2) == len(raw.read_text())
+    done.write_text("done")  # legacy / torn sentinel: redone, not trusted
+    job._prepare_char_data(cfg, 0)
+    assert json.loads(done.read_text())["raw_sha256"] == job._file_digest(str(raw))
+    torch.save(torch.zeros(3, dtype=torch.int64), tmp_path / "proc" / "train.ids.pt")  # tampered product
+    ids3, _ = job._prepare_char_data(cfg, 0)
+    assert len(ids3) == len(raw.read_text())
+
+
+def test_eight_bit_optimizers_refuse_loudly():
+    """paged_adamw_8bit / adamw_8bit are a different algorithm (block-quantized states): refused with
+    a message instead of silently running 32-bit AdamW."""
+    import torch
+    from gke_ray_train_amd.ops import make_optimizer
+    p = [torch.nn.Parameter(torch.zeros(4))]
+    for name in ("paged_adamw_8bit", "adamw_8bit"):
+        with pytest.raises(ValueError, match="8-bit"):
+            make_optimizer(name, p, lr=1e-3, weight_decay=0.0)
+    assert make_optimizer("paged_adamw_32bit", p, lr=1e-3, weight_decay=0.0) is not None

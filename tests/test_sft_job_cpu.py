@@ -214,3 +214,25 @@ def test_padding_free_eval_matches_padded(tmp_path):
                         train_dataset=rows, eval_dataset=rows)
         losses.append(tr.evaluate()["eval_loss"])
     assert abs(losses[0] - losses[1]) < 1e-5 * max(1.0, abs(losses[0])), losses
+
+
+def test_padding_free_pack_selects_tokens_by_mask_for_left_padding(tmp_path, monkeypatch):
+    """A user collator that LEFT-pads: the packed row must hold each sequence's real tokens (chosen
+    by the attention mask), not its first L positions (pads); and GRT_SFT_EVAL_PADDING_FREE=0 turns
+    packed evaluation off."""
+    import torch
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
+    rows = [{"text": "abc " * (3 + i)} for i in range(4)]
+    tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path), per_device_train_batch_size=2, gradient_accumulation_steps=1,
+                                 fuse_accumulation=True, pack_multiple=1, padding_free=True), train_dataset=rows)
+    pad = tr.pad_id
+    ids = torch.tensor([[pad, pad, 5, 6, 7], [8, 9, 10, 11, 12]])
+    mask = torch.tensor([[0, 0, 1, 1, 1], [1, 1, 1, 1, 1]])
+    labels = ids.masked_fill(mask == 0, -100)
+    out, w = tr._pack([{"input_ids": ids, "labels": labels, "attention_mask": mask}], 1, True)
+    assert out["input_ids"][0].tolist() == [5, 6, 7, 8, 9, 10, 11, 12]
+    assert out["lengths"] == [3, 5] and out["ntarget"] == 2 + 4
+    monkeypatch.setenv("GRT_SFT_EVAL_PADDING_FREE", "0")
+    assert tr._eval_padding_free() is False
