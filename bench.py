@@ -78,6 +78,11 @@ def parse():
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-rank collective path even at world 1 (one-rank RCCL process group: "
                          "ZeRO reduce-scatter / all-gather, FSDP gathers) — one-GPU rehearsal of the 8-GPU data plane")
+    ap.add_argument("--proxy-world", type=int, default=0,
+                    help="one-GPU rehearsal of rank 0 of an N-rank ZeRO job: buckets, optimizer shard (1/N of "
+                         "AdamW) and forward-time W^T exactly as at world N, collectives replaced by local "
+                         "copies of this rank's chunk (xGMI time excluded; loss not meaningful). Reports the "
+                         "per-rank step with n_gpus 1 and proxy_world N")
     ap.add_argument("--layers", type=int, default=0,
                     help="rehearsal only: keep the first N decoder layers of --model (the JSON names the model "
                          "'<model>[N/L layers]', so it is never mistaken for the full model's number)")
@@ -120,8 +125,10 @@ def build(a, cfg, dev, dtype, world):
         if a.peft == "qlora":
             quantize_model_(model, BitsAndBytesConfig(bnb_4bit_compute_dtype=dtype))
         fwd = get_peft_model(model, LoraConfig(r=a.lora_r, lora_alpha=16, lora_dropout=0.1))
-    zero = a.zero == "on" or (a.zero == "auto" and (world > 1 or a.force_collectives))
-    eng = DistributedDataParallel(fwd, bucket_cap_mb=a.bucket_mb or None, shard_optimizer=zero)
+    proxy = a.proxy_world > 1 and world == 1
+    zero = a.zero == "on" or (a.zero == "auto" and (world > 1 or a.force_collectives or proxy))
+    eng = DistributedDataParallel(fwd, bucket_cap_mb=a.bucket_mb or None, shard_optimizer=zero,
+                                  proxy_world=a.proxy_world if proxy else 0)
     opt = FusedAdamW(eng.optimizer_param_groups(weight_decay=0.0), lr=a.lr)
     if a.overlap_opt == "on" or (a.overlap_opt == "auto" and not zero and dev.type == "cuda"):
         from gke_ray_train_amd.parallel.overlap import OverlappedOptimizer
@@ -243,8 +250,9 @@ def run(a):
         cfg = get_config(a.model, num_hidden_layers=a.layers)
         cfg.name = f"{cfg.name}[{a.layers}/{full} layers]"
     from gke_ray_train_amd.parallel.planner import GiB, plan_memory
-    plan = plan_memory(cfg, world, a.parallel, offload=a.offload, peft=a.peft, micro_batch=a.micro_batch or a.batch,
-                       seq=a.seq, zero=(a.zero == "on" or (a.zero == "auto" and (world > 1 or a.force_collectives))),
+    plan_world = a.proxy_world if (a.proxy_world > 1 and world == 1) else world
+    plan = plan_memory(cfg, plan_world, a.parallel, offload=a.offload, peft=a.peft, micro_batch=a.micro_batch or a.batch,
+                       seq=a.seq, zero=(a.zero == "on" or (a.zero == "auto" and (plan_world > 1 or a.force_collectives))),
                        checkpointing=a.checkpointing, lora_r=a.lora_r,
                        hbm_capacity=None if not cpu else float("inf"))
     if a.plan_only:
@@ -390,7 +398,9 @@ def run(a):
     if a.peft != "none":
         fpt = fpt * 2.0 / 3.0  # frozen base: no weight-gradient GEMMs (adapter FLOPs are negligible)
     mfu = tps / world * fpt / 2.5e15
-    par = f"{'fsdp' if fsdp else 'dp'}{world // a.sp}" + (f"+sp{a.sp}" if a.sp > 1 else "") + ("+zero1" if getattr(eng, "zero", False) else "") + \
+    proxy = getattr(eng, "proxy", False)
+    par = f"{'fsdp' if fsdp else 'dp'}{world // a.sp}" + (f"-proxy{a.proxy_world}" if proxy else "") + \
+        (f"+sp{a.sp}" if a.sp > 1 else "") + ("+zero1" if getattr(eng, "zero", False) else "") + \
         ("+offload" if a.offload else "") + \
         ("" if a.peft == "none" else f"+{a.peft}")
     if rank == 0:
@@ -419,6 +429,7 @@ def run(a):
             "pg_world_size": pg_world,
             "pg_backend": dist.get_backend() if dist.is_initialized() else "none",
             "launcher": a.launcher,
+            "proxy_world": a.proxy_world if proxy else None,
             "mfu_bf16_dense": round(mfu, 4),
             "hbm_plan_gib": round(plan.hbm_total / GiB, 1),
             "hbm_peak_gib": round(torch.cuda.max_memory_allocated(dev) / GiB, 1) if not cpu else None,

@@ -884,6 +884,75 @@ bool gemm_wgrad(const Tensor& x, const Tensor& y, const Tensor& out, bool accumu
   return true;
 }
 
+// ------------------------------------------------------------------ projection GEMM
+// out[M][N] (+)= a[M][K] @ b[N][K]^T on the hand-written MFMA kernel; returns false (nothing
+// launched) when the shape / layout is outside what the kernel tiles, so callers can fall back.
+bool gemm_supported(const Tensor& a, const Tensor& b, const Tensor& out) {
+  if (a.dim() != 2 || b.dim() != 2 || out.dim() != 2) return false;
+  if (a.scalar_type() != at::kBFloat16 || b.scalar_type() != at::kBFloat16 || out.scalar_type() != at::kBFloat16)
+    return false;
+  if (!a.is_cuda() || !b.is_cuda() || !out.is_cuda()) return false;
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  if (b.size(1) != K || out.size(0) != M || out.size(1) != N) return false;
+  if (a.stride(1) != 1 || b.stride(1) != 1 || out.stride(1) != 1) return false;
+  if (a.stride(0) % 8 || b.stride(0) % 8 || out.stride(0) % 8) return false;
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&a, &b, &out})
+    if (reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) return false;
+  // the kernel's buffer descriptors address A and B with 32-bit byte offsets
+  if (M * a.stride(0) * 2 >= (int64_t(1) << 31) || N * b.stride(0) * 2 >= (int64_t(1) << 31)) return false;
+  return grt::gemm_nt_supported(M, N, K);
+}
+
+bool gemm_nt(const Tensor& a, const Tensor& b, const Tensor& out, bool accumulate, int64_t variant) {
+  if (!gemm_supported(a, b, out)) return false;
+  c10::OptionalDeviceGuard g(a.device());
+  grt::GemmParams p{a.data_ptr(), b.data_ptr(), out.data_ptr(), (int)a.size(0), (int)b.size(0), (int)a.size(1),
+                    a.stride(0), b.stride(0), out.stride(0), accumulate ? 1 : 0, grt::GEMM_EPI_STORE, (int)variant};
+  grt::gemm_nt(p, cur_stream(a));
+  return true;
+}
+
+// out[P][Q] (+)= x[R][P]^T @ y[R][Q] (dW = dY^T X) on the half-tile MFMA kernel reading the
+// token-major operands through transposed LDS reads; false when the shape does not tile
+bool gemm_wgrad2(const Tensor& x, const Tensor& y, const Tensor& out, bool accumulate) {
+  if (x.dim() != 2 || y.dim() != 2 || out.dim() != 2) return false;
+  if (x.scalar_type() != at::kBFloat16 || y.scalar_type() != at::kBFloat16 || out.scalar_type() != at::kBFloat16)
+    return false;
+  if (!x.is_cuda() || !y.is_cuda() || !out.is_cuda()) return false;
+  const int64_t R = x.size(0), P = x.size(1), Q = y.size(1);
+  if (y.size(0) != R || out.size(0) != P || out.size(1) != Q) return false;
+  if (x.stride(1) != 1 || y.stride(1) != 1 || out.stride(1) != 1) return false;
+  if (x.stride(0) % 8 || y.stride(0) % 8 || out.stride(0) % 8) return false;
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&x, &y, &out})
+    if (reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) return false;
+  if (P % 256 || Q % 256 || R % 64 || R == 0 || P > INT32_MAX || Q > INT32_MAX || R > INT32_MAX) return false;
+  c10::OptionalDeviceGuard g(x.device());
+  grt::GemmParams p{x.data_ptr(), y.data_ptr(), out.data_ptr(), (int)P, (int)Q, (int)R,
+                    x.stride(0), y.stride(0), out.stride(0), accumulate ? 1 : 0, grt::GEMM_EPI_STORE, 0};
+  grt::gemm_tt2(p, cur_stream(x));
+  return true;
+}
+
+// out[M][N] (+)= a[M][K] @ b[K][N] (dX = dY W on W as stored [N_out][K_in]); false when unsupported
+bool gemm_nn(const Tensor& a, const Tensor& b, const Tensor& out, bool accumulate) {
+  if (a.dim() != 2 || b.dim() != 2 || out.dim() != 2) return false;
+  if (a.scalar_type() != at::kBFloat16 || b.scalar_type() != at::kBFloat16 || out.scalar_type() != at::kBFloat16)
+    return false;
+  if (!a.is_cuda() || !b.is_cuda() || !out.is_cuda()) return false;
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(1);
+  if (b.size(0) != K || out.size(0) != M || out.size(1) != N) return false;
+  if (a.stride(1) != 1 || b.stride(1) != 1 || out.stride(1) != 1) return false;
+  if (a.stride(0) % 8 || b.stride(0) % 8 || out.stride(0) % 8) return false;
+  for (const Tensor* t : std::initializer_list<const Tensor*>{&a, &b, &out})
+    if (reinterpret_cast<uintptr_t>(t->data_ptr()) % 16) return false;
+  if (M % 256 || N % 256 || K % 64 || K == 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX) return false;
+  c10::OptionalDeviceGuard g(a.device());
+  grt::GemmParams p{a.data_ptr(), b.data_ptr(), out.data_ptr(), (int)M, (int)N, (int)K,
+                    a.stride(0), b.stride(0), out.stride(0), accumulate ? 1 : 0, grt::GEMM_EPI_STORE, 0};
+  grt::gemm_nn(p, cur_stream(a));
+  return true;
+}
+
 // ------------------------------------------------------------------ xGMI IPC collectives
 int64_t ipc_alloc(int64_t nbytes, bool fine_grained, int64_t device) {
   c10::DeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
@@ -1049,6 +1118,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("gemm_wgrad", &gemm_wgrad, py::arg("x"), py::arg("y"), py::arg("out"), py::arg("accumulate"),
         py::arg("mode") = 0);
+  m.def("gemm_supported", &gemm_supported, py::arg("a"), py::arg("b"), py::arg("out"));
+  m.def("gemm_nt", &gemm_nt, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("accumulate") = false,
+        py::arg("variant") = 0);
+  m.def("gemm_wgrad2", &gemm_wgrad2, py::arg("x"), py::arg("y"), py::arg("out"), py::arg("accumulate") = false);
+  m.def("gemm_nn", &gemm_nn, py::arg("a"), py::arg("b"), py::arg("out"), py::arg("accumulate") = false);
   m.def("ipc_alloc", &ipc_alloc);
   m.def("ipc_free", &ipc_free_ptr);
   m.def("ipc_handle", &ipc_handle);

@@ -238,6 +238,30 @@ struct GemmTTParams {
 bool gemm_tt_supported(int P, int Q, int R);
 void gemm_tt(const GemmTTParams& p, hipStream_t stream, int mode = 0);  // mode != 0: diagnostics
 
+// ---------------- projection GEMM (gemm_mfma.hip) ----------------
+// C[M][N] (+)= sum_k A[M][K] * B[N][K]; A, B, C row-major bf16 with row strides lda/ldb/ldc.
+enum GemmEpilogue : int {
+  GEMM_EPI_STORE = 0,   // C = AB^T (beta = 1: C += AB^T)
+};
+struct GemmParams {
+  const void* a;
+  const void* b;
+  void* c;
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  int beta;
+  int epi;
+  int variant;  // pipeline variant (A/B experiments); 0 = default
+};
+bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
+void gemm_nt(const GemmParams& p, hipStream_t stream);
+// weight-gradient form on token-major operands: C[M][N] (+)= sum_k A[k][m] * B[k][n] (a = A [K][M],
+// b = B [K][N]); M % 256 == 0, N % 256 == 0, K % 64 == 0
+void gemm_tt2(const GemmParams& p, hipStream_t stream);
+// input-gradient form without a transposed copy: C[M][N] (+)= sum_k A[M][k] * B[k][N] (a = A [M][K]
+// row-major, b = B [K][N] row-major, i.e. dX = dY W on the weight as stored)
+void gemm_nn(const GemmParams& p, hipStream_t stream);
+
 // ---------------- transpose (transpose.hip) ----------------
 // dst [cols][rows] = src [rows][cols]^T, bf16, rows and cols multiples of 64, row-major contiguous
 void transpose_bf16(const void* src, void* dst, int rows, int cols, hipStream_t s);

@@ -49,6 +49,13 @@ from ..ops.linear import Embedding as _DirectEmbedding, GradSlot, Linear as _Dir
 from .comm import plan_bucket_bytes, small_all_reduce
 
 
+class _DoneWork:
+    """Stand-in for a collective's Work in proxy mode (the local copy already ran in stream order)."""
+
+    def wait(self):
+        return None
+
+
 def shared_param_ids(module: nn.Module) -> set:
     """ids of parameters owned by more than one module (tied embeddings): their gradient has two
     producers, so they must not use the single-writer direct gradient slots."""
@@ -127,20 +134,30 @@ class DistributedDataParallel(nn.Module):
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  broadcast_params: bool = True, grad_dtype: Optional[torch.dtype] = None,
-                 split_decay: bool = True, shard_optimizer: bool = False, force_collectives: Optional[bool] = None):
+                 split_decay: bool = True, shard_optimizer: bool = False, force_collectives: Optional[bool] = None,
+                 proxy_world: int = 0):
         super().__init__()
         self.module = module
         self.pg = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(process_group) if self.world_size > 1 else 0
+        # proxy_world = N on ONE process (no process group): lay out the buckets, ZeRO shards and the
+        # optimizer state exactly as rank 0 of an N-rank job and run its per-rank compute; the
+        # collectives become local copies of this rank's chunk (reduce-scatter output, all-gather
+        # input), i.e. the step an N-GPU run executes minus the xGMI transfers (bench.py --proxy-world).
+        # Only rank 0's shard is updated, so the loss is not meaningful in this mode.
+        self.proxy = int(proxy_world) > 1 and self.world_size == 1
+        if self.proxy:
+            self.world_size, self.rank = int(proxy_world), 0
         if force_collectives is None:
             force_collectives = os.environ.get("GRT_FORCE_COLLECTIVES", "0") == "1"
         # comm: the collective code path runs (world > 1, or forced at world 1 for rehearsal)
-        self.comm = self.world_size > 1 or (bool(force_collectives) and dist.is_available() and dist.is_initialized())
+        self.comm = self.proxy or self.world_size > 1 or (
+            bool(force_collectives) and dist.is_available() and dist.is_initialized())
         self.zero = bool(shard_optimizer) and self.comm
         # gloo branch: list-based collectives. GRT_GLOO_TENSOR_COLLECTIVES=1 runs the RCCL code path
         # (reduce_scatter_tensor / all_gather_into_tensor) over gloo so CPU tests exercise it.
-        self.gloo = (self.comm and dist.get_backend(process_group) == "gloo"
+        self.gloo = (self.comm and not self.proxy and dist.get_backend(process_group) == "gloo"
                      and os.environ.get("GRT_GLOO_TENSOR_COLLECTIVES", "0") != "1")
         self._sync = True
         self._hooks = []
@@ -184,7 +201,7 @@ class DistributedDataParallel(nn.Module):
         for (dtype, decay), items in groups.items():
             items = list(reversed(items))
             self.groups.append(self._flatten(items, dtype, decay, grad_dtype or dtype))
-        if broadcast_params and self.world_size > 1:
+        if broadcast_params and self.world_size > 1 and not self.proxy:
             with torch.no_grad():
                 for g in self.groups:
                     dist.broadcast(g.flat, src=dist.get_global_rank(process_group, 0) if process_group else 0,
@@ -353,6 +370,12 @@ class DistributedDataParallel(nn.Module):
     def _launch(self, g: _FlatGroup, b: _Bucket):
         if b.work is not None:
             return
+        if self.proxy:  # this rank's reduce-scatter output: its chunk of the bucket
+            c = (b.end - b.start) // self.world_size
+            if self.zero:
+                g.shard_grad[b.shard_off:b.shard_off + c].copy_(g.grad[b.start + self.rank * c:b.start + (self.rank + 1) * c])
+            b.work = _DoneWork()
+            return
         if not self.zero or self.gloo:  # gloo has no reduce-scatter: all-reduce, keep our chunk later
             b.work = dist.all_reduce(g.grad[b.start:b.end], op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         else:
@@ -431,7 +454,10 @@ class DistributedDataParallel(nn.Module):
             return _clip(self.grad_buffers(), max_norm, prescale=1.0 / W)
         st = _clip(self.grad_buffers(), 0.0, prescale=1.0)
         ss = (st.buf[0] ** 2).reshape(1)
-        small_all_reduce(ss, group=self.pg)
+        if self.proxy:
+            ss = ss * W  # the other ranks' shards, modelled as equal to this one
+        else:
+            small_all_reduce(ss, group=self.pg)
         total = ss[0].sqrt() / W
         coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(total)
         st.buf[0] = total
@@ -447,7 +473,10 @@ class DistributedDataParallel(nn.Module):
             for b in reversed(g.buckets):  # buckets are in backward order; forward needs the last first
                 c = (b.end - b.start) // W
                 src = g.shard_param[b.shard_off:b.shard_off + c]
-                if self.gloo:
+                if self.proxy:  # the local part of the all-gather
+                    g.flat[b.start + self.rank * c:b.start + (self.rank + 1) * c].copy_(src)
+                    b.ag_work = _DoneWork()
+                elif self.gloo:
                     b.ag_work = dist.all_gather(list(g.flat[b.start:b.end].chunk(W)), src, group=self.pg,
                                                 async_op=True)
                 else:

@@ -325,11 +325,24 @@ class SFTTrainer:
         torch.manual_seed(args.seed)
         random.seed(args.seed)
         np.random.seed(args.seed)
-        self.engine = DistributedDataParallel(model, broadcast_params=True)
+        # The engine choices of bench.py's headline step (the same config #2 path): full fine-tuning
+        # at world > 1 shards the AdamW state (ZeRO: bucketed reduce-scatter during backward, the
+        # updated shards all-gathered under the next forward, W^T written at forward time); at world 1
+        # (and for adapter models, whose replicated update is small) the AdamW update runs per module
+        # on a side stream overlapped with the next forward and writes W^T for the TN dX GEMMs
+        # (parallel/overlap.py). GRT_SFT_ZERO=0 / GRT_SFT_OVERLAP_OPT=0 select the plain paths.
+        adapters = hasattr(getattr(model, "base_model", model), "lora_modules") or hasattr(model, "lora_modules")
+        zero = self.world > 1 and not adapters and os.environ.get("GRT_SFT_ZERO", "1") != "0"
+        self.engine = DistributedDataParallel(model, broadcast_params=True, shard_optimizer=zero)
         self.optimizer = make_optimizer(args.optim, self.engine.optimizer_param_groups(args.weight_decay),
                                         lr=args.learning_rate, weight_decay=args.weight_decay,
                                         betas=(args.adam_beta1, args.adam_beta2), eps=args.adam_epsilon,
                                         master_weights=args.master_weights)
+        from ..ops.optim import FusedAdamW
+        if (self.device.type == "cuda" and not self.engine.zero and type(self.optimizer) is FusedAdamW
+                and os.environ.get("GRT_SFT_OVERLAP_OPT", "1") != "0"):
+            from ..parallel.overlap import OverlappedOptimizer
+            self.optimizer = OverlappedOptimizer(self.engine, self.optimizer)
         self._snapshot = _HostSnapshot()
         if self.device.type == "cuda":
             self._prepare_device()
@@ -567,7 +580,8 @@ class SFTTrainer:
         steps_per_epoch = max(1, math.ceil(micro_per_epoch / accum))
         total = a.max_steps if a.max_steps > 0 else math.ceil(a.num_train_epochs * steps_per_epoch)
         warm = a.warmup_steps or math.ceil(a.warmup_ratio * total)
-        self.scheduler = get_scheduler(a.lr_scheduler_type, self.optimizer, warm, total)
+        # LambdaLR needs the torch optimizer; an OverlappedOptimizer shares its param_groups
+        self.scheduler = get_scheduler(a.lr_scheduler_type, getattr(self.optimizer, "opt", self.optimizer), warm, total)
         start_step = 0
         if resume_from_checkpoint:
             start_step = self._load_checkpoint(resume_from_checkpoint)
@@ -625,8 +639,11 @@ class SFTTrainer:
                 with roctx.range("grad_sync"):
                     self.engine.finish_gradient_sync()
                 with roctx.range("optimizer"):
-                    st = clip_grad_norm_(self.engine.grad_buffers(), a.max_grad_norm, prescale=1.0 / self.world)
+                    # global norm of the averaged gradient (early per-bucket norms at world 1, the
+                    # sharded all-reduce under ZeRO), applied by the fused update on device
+                    st = self.engine.clip_grad_norm_(a.max_grad_norm)
                     self.optimizer.step(grad_scale=st)
+                    self.engine.after_optimizer_step()  # ZeRO: all-gather the updated shards
                 self.scheduler.step()
                 self.engine.zero_grad()
                 if trace is not None:
@@ -668,6 +685,7 @@ class SFTTrainer:
                 self._save_checkpoint(step)
             if done:
                 break
+        self._settle()
         self._finish_save()  # the runtime includes the last checkpoint's write
         if self.device.type == "cuda":
             torch.cuda.synchronize()
@@ -691,6 +709,12 @@ class SFTTrainer:
         if self.tb is not None:
             self.tb.flush()
         return TrainOutput(step, train_loss, metrics)
+
+    def _settle(self):
+        """Parameters final: pending overlapped chunk updates and ZeRO all-gathers complete."""
+        if hasattr(self.optimizer, "synchronize"):
+            self.optimizer.synchronize()
+        self.engine.wait_params()
 
     def _sync(self):
         if self.device.type == "cuda":
@@ -777,11 +801,13 @@ class SFTTrainer:
         ``train`` returns and before a checkpoint is loaded."""
         tm = [time.time()]
         self._finish_save()
+        self._settle()
         tm.append(time.time())
         a = self.args
         d = os.path.join(a.output_dir, f"checkpoint-{step}")
         job = None
         err = None
+        sharded_opt = bool(getattr(self.engine, "zero", False))
         if self.rank == 0:
             try:
                 os.makedirs(d, exist_ok=True)
@@ -824,6 +850,8 @@ class SFTTrainer:
         try:
             os.makedirs(d, exist_ok=True)
             torch.save(_rng_snapshot(), os.path.join(d, f"rng_state_{self.rank}.pth"))
+            if sharded_opt:  # ZeRO: each rank holds 1/world of the AdamW state; rank 0's is also optimizer.pt
+                torch.save(_to_host(self.optimizer.state_dict()), os.path.join(d, f"optimizer_rank{self.rank}.pt"))
         except Exception as e:
             err = err or e
         # every rank reaches this exchange, so a failed snapshot raises everywhere (no hang)
@@ -885,8 +913,12 @@ class SFTTrainer:
             from ..models.hub import from_pretrained
             loaded = from_pretrained(d, device=self.device, torch_dtype=next(m.parameters()).dtype)
             m.load_state_dict(loaded.state_dict())
-        self.optimizer.load_state_dict(torch.load(os.path.join(d, "optimizer.pt"), map_location=self.device,
-                                                  weights_only=True))
+        shard = os.path.join(d, f"optimizer_rank{self.rank}.pt")
+        if getattr(self.engine, "zero", False) and not os.path.exists(shard):
+            raise FileNotFoundError(f"{d}: sharded (ZeRO) optimizer state for rank {self.rank} is missing "
+                                    f"(checkpoint written at another world size?)")
+        opt_f = shard if getattr(self.engine, "zero", False) else os.path.join(d, "optimizer.pt")
+        self.optimizer.load_state_dict(torch.load(opt_f, map_location=self.device, weights_only=True))
         self.scheduler.load_state_dict(torch.load(os.path.join(d, "scheduler.pt"), weights_only=True))
         with open(os.path.join(d, "trainer_state.json")) as f:
             st = json.load(f)

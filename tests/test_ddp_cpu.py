@@ -146,3 +146,34 @@ def test_zero_sharded_optimizer_matches_ddp(tensor_coll):
     for n in p_ref:
         d = abs(p_ref[n] - p_zero[n]).max()
         assert d < 1e-5, f"{n}: {d}"
+
+
+def test_proxy_world_lays_out_rank0_of_an_n_rank_zero_job():
+    """DistributedDataParallel(proxy_world=8) on one process (no process group): buckets and ZeRO
+    shards exactly as rank 0 of 8 (1/8 of the optimizer state), collectives replaced by local copies
+    of rank 0's chunk; a step runs end to end (bench.py --proxy-world)."""
+    import torch
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.ops import FusedAdamW
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=0)
+    eng = DistributedDataParallel(m, shard_optimizer=True, proxy_world=8)
+    assert eng.proxy and eng.zero and eng.world_size == 8 and eng.rank == 0
+    for g in eng.groups:
+        assert g.shard_grad.numel() * 8 == g.grad.numel()
+    opt = FusedAdamW(eng.optimizer_param_groups(0.0), lr=1e-3)
+    assert sum(p.numel() for grp in opt.param_groups for p in grp["params"]) * 8 == sum(g.flat.numel() for g in eng.groups)
+    ids = torch.randint(0, m.config.vocab_size, (2, 32))
+    before = [g.flat.clone() for g in eng.groups]
+    loss = m(ids, labels=ids)["loss"]
+    loss.backward()
+    eng.finish_gradient_sync()
+    st = eng.clip_grad_norm_(1.0)
+    opt.step(grad_scale=st)
+    eng.after_optimizer_step()
+    eng.wait_params()
+    for g, b0 in zip(eng.groups, before):
+        for b in g.buckets:
+            c = (b.end - b.start) // 8
+            assert not torch.equal(g.flat[b.start:b.start + c], b0[b.start:b.start + c])  # rank 0's chunk updated
+            assert torch.equal(g.flat[b.start + c:b.end], b0[b.start + c:b.end])          # the rest: other ranks'

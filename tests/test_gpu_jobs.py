@@ -167,3 +167,39 @@ def test_graph_decode_matches_eager_decode():
     e2 = m.generate(ids, max_new_tokens=40, use_graph=False, eos_token_id=eos, pad_token_id=0)
     g2 = m.generate(ids, max_new_tokens=40, use_graph=True, eos_token_id=eos, pad_token_id=0, sync_every=7)
     assert e2.shape == g2.shape and (e2 == g2).float().mean().item() > 0.98
+
+
+def test_sft_full_ft_overlapped_engine_matches_plain_path(tmp_path, monkeypatch):
+    """Full fine-tuning through SFTTrainer on the bench's engine (AdamW per module on a side stream,
+    overlapped with the next forward and writing W^T for the TN dX GEMMs; early per-bucket grad
+    norm) gives the losses and parameters of the plain serial update (GRT_SFT_OVERLAP_OPT=0) to
+    bf16 rounding, and the checkpoint layout is unchanged."""
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.parallel.overlap import OverlappedOptimizer
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    rows = [{"text": "select a, b from t%d where c > %d order by b" % (i, 3 * i)} for i in range(48)]
+    runs = []
+    for overlap in ("1", "0"):
+        monkeypatch.setenv("GRT_SFT_OVERLAP_OPT", overlap)
+        torch.manual_seed(0)
+        m = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=3)
+        out = tmp_path / f"o{overlap}"
+        tr = SFTTrainer(m, SFTConfig(output_dir=str(out), per_device_train_batch_size=2, gradient_accumulation_steps=2,
+                                     learning_rate=1e-3, max_steps=6, logging_steps=2, save_steps=3,
+                                     save_strategy="steps", max_seq_length=64, optim="adamw_torch",
+                                     report_to="none", seed=1), train_dataset=rows)
+        assert isinstance(tr.optimizer, OverlappedOptimizer) == (overlap == "1")
+        res = tr.train()
+        torch.cuda.synchronize()
+        losses = [h["loss"] for h in tr.state["log_history"] if "loss" in h]
+        runs.append((losses, {k: v.float().clone() for k, v in m.state_dict().items()}, res))
+        ck = sorted(p.name for p in out.glob("checkpoint-*"))
+        assert ck == ["checkpoint-3", "checkpoint-6"]
+        assert {"optimizer.pt", "scheduler.pt", "trainer_state.json", "model.safetensors"} <= \
+            {p.name for p in (out / "checkpoint-6").iterdir()}
+    for a, b in zip(runs[0][0], runs[1][0]):
+        assert abs(a - b) <= 2e-2 * abs(b), (runs[0][0], runs[1][0])
+    for k, v in runs[1][1].items():
+        d = (runs[0][1][k] - v).abs().max().item()
+        assert d < 3e-2 * max(1.0, v.abs().max().item()), (k, d)
+    assert runs[0][2].metrics["train_tokens_per_second"] > 0
