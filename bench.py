@@ -78,6 +78,13 @@ def parse():
     ap.add_argument("--force-collectives", action="store_true",
                     help="run the multi-rank collective path even at world 1 (one-rank RCCL process group: "
                          "ZeRO reduce-scatter / all-gather, FSDP gathers) — one-GPU rehearsal of the 8-GPU data plane")
+    ap.add_argument("--offload-resident", default="auto",
+                    help="--offload: share of the AdamW moments kept in HBM (0..1), 'auto' = what the memory "
+                         "planner says fits beside everything else (the rest streams over the host link, "
+                         "overlapped with the next forward, parallel/offload.py)")
+    ap.add_argument("--offload-overlap", default="on", choices=["on", "off"],
+                    help="--offload: per-unit update overlapped with the next forward (on) or the serial "
+                         "after-backward stream (off)")
     ap.add_argument("--proxy-world", type=int, default=0,
                     help="one-GPU rehearsal of rank 0 of an N-rank ZeRO job: buckets, optimizer shard (1/N of "
                          "AdamW) and forward-time W^T exactly as at world N, collectives replaced by local "
@@ -110,7 +117,8 @@ def build(a, cfg, dev, dtype, world):
         if a.checkpointing:
             model.gradient_checkpointing_enable()
         eng = FullyShardedDataParallel(model, param_init_fn=init, device=dev, cpu_offload=a.offload)
-        opt = eng.build_optimizer(lr=a.lr)
+        opt = eng.build_optimizer(lr=a.lr, overlap=a.offload_overlap == "on",
+                                  resident_fraction=getattr(a, "resident_fraction", 0.0))
         return model, eng, eng, opt
     from gke_ray_train_amd.parallel import DistributedDataParallel
     model = build_llama(cfg, device=dev, dtype=dtype, seed=1234)
@@ -261,6 +269,13 @@ def run(a):
         if dist.is_initialized():
             dist.destroy_process_group()
         return
+    a.resident_fraction = 0.0
+    if a.offload and a.parallel == "fsdp":
+        if a.offload_resident == "auto":
+            from gke_ray_train_amd.parallel.offload import resident_fraction_from_plan
+            a.resident_fraction = resident_fraction_from_plan(plan, None)
+        else:
+            a.resident_fraction = float(a.offload_resident)
     if not plan.fits:  # refuse up front with the numbers instead of an allocator error mid-step
         print(f"bench.py: memory preflight failed for {cfg.name} {a.parallel} world={world}: "
               + "; ".join(plan.problems()), file=sys.stderr, flush=True)
@@ -430,6 +445,8 @@ def run(a):
             "pg_backend": dist.get_backend() if dist.is_initialized() else "none",
             "launcher": a.launcher,
             "proxy_world": a.proxy_world if proxy else None,
+            "offload_resident_units": getattr(opt, "resident_units", None) if a.offload else None,
+            "offload_units": len(getattr(opt, "segments", [])) if a.offload else None,
             "mfu_bf16_dense": round(mfu, 4),
             "hbm_plan_gib": round(plan.hbm_total / GiB, 1),
             "hbm_peak_gib": round(torch.cuda.max_memory_allocated(dev) / GiB, 1) if not cpu else None,

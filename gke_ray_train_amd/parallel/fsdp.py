@@ -191,6 +191,27 @@ class FullyShardedDataParallel(nn.Module):
                 u.module.register_forward_hook(self._make_post_fwd(u))
         self._root_unit = next((u for u in self.units if u.module is module), None)
         self._offload_state = None
+        # overlapped offloaded optimizer (parallel/offload.py): per-unit "shard updated" events,
+        # waited for before the unit's next all-gather / forward; it also zeroes the grad shards
+        self._update_events: Dict[int, torch.cuda.Event] = {}
+        self._grad_zero_by_optimizer = False
+        self._gstream = None
+
+    # ================================================================ optimizer hand-off
+    def set_update_events(self, events):
+        self._update_events = {id(u): ev for u, ev in events.items()}
+
+    def _wait_update(self, u: _Unit, stream=None):
+        ev = self._update_events.pop(id(u), None)
+        if ev is not None:
+            (stream or torch.cuda.current_stream(self.device)).wait_event(ev)
+
+    def wait_updates(self):
+        """The current stream waits for every pending unit update (checkpointing, eval, step)."""
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        for ev in self._update_events.values():
+            cur.wait_event(ev)
+        self._update_events.clear()
 
     # ================================================================ sharding helpers
     @torch.no_grad()
@@ -258,15 +279,30 @@ class FullyShardedDataParallel(nn.Module):
         if u.full is not None or u.gather_work is not None or not self.comm:
             return
         buf = self._acquire(u.total)
+        if id(u) in self._update_events and self.device.type == "cuda":
+            # the shard is still being updated on the optimizer's stream: issue the gather from a
+            # side stream that waits for that update, so the compute stream (still running the
+            # previous unit) never blocks on a later unit's optimizer work
+            if self._gstream is None:
+                self._gstream = torch.cuda.Stream(self.device)
+            self._gstream.wait_stream(torch.cuda.current_stream(self.device))  # buffer reuse order
+            self._wait_update(u, self._gstream)
+            with torch.cuda.stream(self._gstream):
+                self._gather_into(u, buf)
+        else:
+            self._gather_into(u, buf)
+        u._pending_buf = buf
+
+    def _gather_into(self, u: _Unit, buf):
         if self.gloo:
             parts = list(buf.chunk(self.world))
             u.gather_work = dist.all_gather(parts, u.shard, group=self.pg, async_op=True)
         else:
             u.gather_work = dist.all_gather_into_tensor(buf, u.shard, group=self.pg, async_op=True)
-        u._pending_buf = buf
 
     def _wait_gather(self, u: _Unit):
         if not self.comm:
+            self._wait_update(u)  # world 1: the shard is the parameter; wait for its update
             return
         if u.full is None and u.gather_work is None:
             self._issue_gather(u)
@@ -468,8 +504,9 @@ class FullyShardedDataParallel(nn.Module):
     def zero_grad(self, set_to_none: bool = True):
         for u in self.units:
             u.acc_started = False
-        self.grad_store.zero_()
-        self.rep_grad.zero_()
+        if not self._grad_zero_by_optimizer:  # else: zeroed per unit on the update stream
+            self.grad_store.zero_()
+            self.rep_grad.zero_()
         o = 0
         for _, p in self.replicated:  # a caller may have set .grad = None: re-attach the views
             p.grad = self.rep_grad[o:o + p.numel()].view_as(p)
@@ -483,14 +520,26 @@ class FullyShardedDataParallel(nn.Module):
     def world_size(self) -> int:
         return self.world
 
-    def build_optimizer(self, lr: float, weight_decay: float = 0.0, betas=(0.9, 0.999), eps=1e-8):
-        """Fused AdamW over this rank's shards; with ``cpu_offload`` the moments live in pinned host
-        memory and stream through the GPU kernel (ops.optim.OffloadedAdamW)."""
+    def build_optimizer(self, lr: float, weight_decay: float = 0.0, betas=(0.9, 0.999), eps=1e-8,
+                        overlap: Optional[bool] = None, resident_fraction: Optional[float] = None):
+        """Fused AdamW over this rank's shards. With ``cpu_offload`` the moments live in pinned host
+        memory: by default the update is split by unit and overlapped with the next forward, with
+        the first ``resident_fraction`` of the moments kept in HBM (parallel/offload.py);
+        ``overlap=False`` / GRT_OFFLOAD_OVERLAP=0 is the serial after-backward stream
+        (ops.optim.OffloadedAdamW)."""
         from ..ops.optim import FusedAdamW, OffloadedAdamW
-        groups = self.optimizer_param_groups(weight_decay)
         if self.cpu_offload and self.device.type == "cuda":
-            return OffloadedAdamW(groups, chunk_elems=self.offload_chunk, lr=lr, betas=betas, eps=eps)
-        return FusedAdamW(groups, lr=lr, betas=betas, eps=eps)
+            if overlap is None:
+                overlap = os.environ.get("GRT_OFFLOAD_OVERLAP", "1") != "0"
+            if overlap:
+                from .offload import OverlappedOffloadAdamW
+                if resident_fraction is None:
+                    resident_fraction = float(os.environ.get("GRT_OFFLOAD_RESIDENT", "0"))
+                return OverlappedOffloadAdamW(self, chunk_elems=self.offload_chunk, resident_fraction=resident_fraction,
+                                              lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+            return OffloadedAdamW(self.optimizer_param_groups(weight_decay), chunk_elems=self.offload_chunk, lr=lr,
+                                  betas=betas, eps=eps)
+        return FusedAdamW(self.optimizer_param_groups(weight_decay), lr=lr, betas=betas, eps=eps)
 
     def optimizer_param_groups(self, weight_decay: float = 0.0):
         sp = nn.Parameter(self.shard_store, requires_grad=False)
@@ -517,6 +566,7 @@ class FullyShardedDataParallel(nn.Module):
     @torch.no_grad()
     def full_state_dict(self) -> Dict[str, torch.Tensor]:
         """Gathered (unsharded) state dict on every rank, module parameter names."""
+        self.wait_updates()
         out = {}
         for u in self.units:
             self._wait_gather(u)
@@ -570,6 +620,7 @@ class FullyShardedDataParallel(nn.Module):
             raise KeyError(f"missing keys in state dict: {missing[:8]}")
 
     def sharded_state_dict(self) -> Dict[str, torch.Tensor]:
+        self.wait_updates()
         return {"shard_store": self.shard_store.detach().clone(), "rep_flat": self.rep_flat.detach().clone(),
                 "rank": torch.tensor(self.rank), "world": torch.tensor(self.world)}
 

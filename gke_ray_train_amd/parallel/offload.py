@@ -1,0 +1,205 @@
+"""Offloaded AdamW for FSDP, overlapped with the next forward (BASELINE config #5).
+
+Not in the reference (SURVEY §2.4 CPU offload, §7.4 item 5). ``ops.optim.OffloadedAdamW`` streams
+every chunk of the fp32 moments host -> HBM -> host AFTER backward, serially with compute; at 8 B of
+moments per parameter each way that exposes the whole host-link transfer every step.
+
+MI355X design:
+* the update is split by FSDP unit and issued at ``step()`` time on side streams in FORWARD order
+  (root unit — embeddings / LM head — first, then the decoder blocks): uploads on one stream,
+  the fused AdamW kernel on another, downloads on a third, so chunk i+1's H2D and chunk i-1's D2H
+  overlap chunk i's update (the host link is full duplex) and the whole pipeline runs under the
+  next forward. Each unit records an event; FSDP waits for it right before the unit's next
+  all-gather (issued from a gather stream, so the compute stream never blocks on a later unit's
+  update) or, at world 1, before the unit's forward;
+* the global clip stays exact: the coefficient computed at the end of backward is on the compute
+  stream before the entry event every update stream waits for;
+* RESIDENCY: the offload is a capacity valve, not an end in itself. 288 GB of HBM holds the moments
+  of most units even at 70B / 8 ranks, so the first ``resident_units`` units in forward order keep
+  their moments in HBM (updated with no host traffic; they are the units needed soonest) and only
+  the rest stream. ``resident_fraction`` (bench.py ``--offload-resident auto``) is derived from the
+  memory planner: the share of the moments that fits beside everything else;
+* gradient shards of a unit are zeroed on the update stream right after its update (FSDP's
+  ``zero_grad`` would otherwise memset them on the compute stream while updates still read them).
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, List, Optional
+
+import torch
+
+from .. import _native
+from ..ops.optim import GradClipState, OffloadedAdamW
+
+
+class OverlappedOffloadAdamW(OffloadedAdamW):
+    NSLOT = 3
+
+    def __init__(self, fsdp, chunk_elems: int = 1 << 26, resident_fraction: float = 0.0, **kw):
+        groups = fsdp.optimizer_param_groups(kw.pop("weight_decay", 0.0))
+        super().__init__(groups, chunk_elems=chunk_elems, **kw)
+        self.fsdp = fsdp
+        root = [u for u in fsdp.units if u.module is fsdp.module]
+        blocks = [u for u in fsdp.units if u.module is not fsdp.module]
+        off, ranges = 0, {}
+        for u in fsdp.units:  # shard store layout order
+            ranges[id(u)] = (off, off + u.shard_numel)
+            off += u.shard_numel
+        self.segments = [(u,) + ranges[id(u)] for u in root + blocks]  # forward order
+        total = sum(hi - lo for _, lo, hi in self.segments)
+        budget = float(resident_fraction) * total
+        self.resident = set()
+        acc = 0
+        for u, lo, hi in self.segments:
+            if acc + (hi - lo) > budget:
+                break
+            self.resident.add(id(u))
+            acc += hi - lo
+        self._dev_m: Dict[int, torch.Tensor] = {}
+        self._dev_v: Dict[int, torch.Tensor] = {}
+        self._streams = None
+        self._slot_free: List[Optional[torch.cuda.Event]] = [None] * self.NSLOT
+        fsdp._grad_zero_by_optimizer = True
+
+    @property
+    def resident_units(self) -> int:
+        return len(self.resident)
+
+    def _state(self, p):
+        st = self.state[p]
+        if len(st) == 0:
+            n = p.numel()
+            st["step"] = torch.tensor(0.0)
+            st["exp_avg"] = torch.zeros(n, dtype=torch.float32).pin_memory()
+            st["exp_avg_sq"] = torch.zeros(n, dtype=torch.float32).pin_memory()
+        return st
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: Optional[GradClipState] = None):
+        fs = self.fsdp
+        dev = fs.device
+        if dev.type != "cuda":
+            return super().step(closure, grad_scale)
+        C = _native.kernels()
+        if self._streams is None:
+            self._streams = tuple(torch.cuda.Stream(dev) for _ in range(3))  # up, update, down
+            self._stage = [(torch.empty(self.chunk, device=dev), torch.empty(self.chunk, device=dev))
+                           for _ in range(self.NSLOT)]
+        up, upd, down = self._streams
+        comp = torch.cuda.current_stream(dev)
+        fs.wait_updates()  # the previous step's updates all landed (normally long done)
+        hbs, work = [], []
+        for gi, group in enumerate(self.param_groups):
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                st = self._state(p)
+                st["step"] += 1
+                step = float(st["step"])
+                hb = self._hyper_buf(p.device, (gi,))
+                hb.copy_(torch.tensor([group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** step,
+                                       1.0 - b2 ** step, 1.0, self._sr(), step]), non_blocking=True)
+                work.append((p, st, hb))
+        entry = torch.cuda.Event()
+        entry.record(comp)  # gradients, clip coefficient and hyper-parameters of this step
+        gs = None if grad_scale is None else grad_scale.buf
+        (sp, sst, shb), (rp, rst, rhb) = work[0], work[1]
+        for s in (up, upd, down):
+            s.wait_event(entry)
+        up.wait_stream(down)  # host moments of the previous step fully downloaded
+        # replicated 1-D parameters (norm weights): tiny, device moments, first on the update stream
+        with torch.cuda.stream(upd):
+            if "dev_m" not in rst:
+                rst["dev_m"] = rst["exp_avg"].to(dev)
+                rst["dev_v"] = rst["exp_avg_sq"].to(dev)
+            C.adamw(rp.data, rp.grad, rst["dev_m"], rst["dev_v"], None, rhb, gs, 0, 0)
+            rp.grad.zero_()
+        pf, gf = sp.data.view(-1), sp.grad.view(-1)
+        m_h, v_h = sst["exp_avg"], sst["exp_avg_sq"]
+        slot = 0
+        events = {}
+        for u, lo, hi in self.segments:
+            if id(u) in self.resident:
+                with torch.cuda.stream(upd):
+                    if id(u) not in self._dev_m:
+                        self._dev_m[id(u)] = m_h[lo:hi].to(dev)
+                        self._dev_v[id(u)] = v_h[lo:hi].to(dev)
+                    C.adamw(pf[lo:hi], gf[lo:hi], self._dev_m[id(u)], self._dev_v[id(u)], None, shb, gs, 0, lo)
+                    gf[lo:hi].zero_()
+            else:
+                for s in range(lo, hi, self.chunk):
+                    e = min(hi, s + self.chunk)
+                    mb, vb = self._stage[slot]
+                    with torch.cuda.stream(up):
+                        if self._slot_free[slot] is not None:
+                            up.wait_event(self._slot_free[slot])
+                        mb[:e - s].copy_(m_h[s:e], non_blocking=True)
+                        vb[:e - s].copy_(v_h[s:e], non_blocking=True)
+                        landed = torch.cuda.Event()
+                        landed.record(up)
+                    with torch.cuda.stream(upd):
+                        upd.wait_event(landed)
+                        C.adamw(pf[s:e], gf[s:e], mb[:e - s], vb[:e - s], None, shb, gs, 0, s)
+                        gf[s:e].zero_()
+                        done = torch.cuda.Event()
+                        done.record(upd)
+                    with torch.cuda.stream(down):
+                        down.wait_event(done)
+                        m_h[s:e].copy_(mb[:e - s], non_blocking=True)
+                        v_h[s:e].copy_(vb[:e - s], non_blocking=True)
+                        free = torch.cuda.Event()
+                        free.record(down)
+                    self._slot_free[slot] = free
+                    slot = (slot + 1) % self.NSLOT
+            ev = torch.cuda.Event()
+            ev.record(upd)
+            events[u] = ev
+        fs.set_update_events(events)
+
+    def synchronize(self):
+        """Current stream waits for every pending unit update and the moment downloads."""
+        self.fsdp.wait_updates()
+        if self._streams is not None:
+            torch.cuda.current_stream(self.fsdp.device).wait_stream(self._streams[2])
+
+    def state_dict(self):
+        """Moments of resident units are copied into the host tensors, so the layout is the plain
+        OffloadedAdamW one (full-size host exp_avg / exp_avg_sq)."""
+        self.synchronize()
+        torch.cuda.synchronize(self.fsdp.device)
+        if self._dev_m:
+            sp = self.param_groups[0]["params"][0]
+            st = self.state[sp]
+            for u, lo, hi in self.segments:
+                if id(u) in self._dev_m:
+                    st["exp_avg"][lo:hi].copy_(self._dev_m[id(u)])
+                    st["exp_avg_sq"][lo:hi].copy_(self._dev_v[id(u)])
+        rp = self.param_groups[1]["params"][0]
+        rst = self.state.get(rp, {})
+        if "dev_m" in rst:
+            rst["exp_avg"].copy_(rst["dev_m"])
+            rst["exp_avg_sq"].copy_(rst["dev_v"])
+        sd = super().state_dict()
+        for s in sd["state"].values():  # device mirrors are not part of the checkpoint
+            s.pop("dev_m", None)
+            s.pop("dev_v", None)
+        return sd
+
+    def load_state_dict(self, sd):
+        self.synchronize()
+        super().load_state_dict(sd)
+        self._dev_m.clear()
+        self._dev_v.clear()
+        for st in self.state.values():
+            st.pop("dev_m", None)
+            st.pop("dev_v", None)
+
+
+def resident_fraction_from_plan(plan_offload, plan_resident, margin_bytes: float = 8 * (1 << 30)) -> float:
+    """Share of the offloaded moments that fits in HBM: capacity minus the offload plan's total
+    (which already holds the staging chunks) minus a margin, over the moments the offload moved."""
+    moved = plan_offload.host_per_rank.get("adam_moments_fp32", 0.0)
+    if moved <= 0:
+        return 1.0
+    room = plan_offload.hbm_capacity - plan_offload.hbm_total - margin_bytes
+    return max(0.0, min(1.0, room / moved))

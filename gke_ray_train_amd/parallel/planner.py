@@ -188,9 +188,10 @@ def plan_memory(cfg, world: int, parallel: str = "ddp", offload: bool = False, p
         hbm["adapters"] = t * B
         hbm["adapter_grads"] = t * B
         hbm["adam_moments_fp32"] = 8.0 * t
-        # adapter activations: the dropped inputs x_d kept for dA (dropout > 0) and the h' tails
-        xd = L * (3 * h + f) * B if lora_dropout > 0 else 0.0
-        hbm["adapter_activations"] = tokens * (xd + L * sum(R for _, R in mods) * B)
+        # adapter activations: the h' tails of the [x | h'] rows. The dropped inputs x_d kept for dA
+        # take the place of the adapted projections' inputs, which the frozen base no longer saves
+        # for weight gradients (both are in `activations`)
+        hbm["adapter_activations"] = tokens * L * sum(R for _, R in mods) * B
         return plan
     zero = (world > 1) if zero is None else zero
     hbm["params"] = P * B
