@@ -456,7 +456,14 @@ __device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8& a, const bf16x8
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
 }
 
-template <int R, bool PRIO>
+// lean LDS-DMA: M0 set in the same statement and declared clobbered (nothing else in these kernels
+// uses M0), no save / restore: 2 scalar instructions per DMA instead of 4
+__device__ __forceinline__ void bdma16_lean(uint32_t voff, __amdgpu_buffer_rsrc_t rsrc, uint32_t soff, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+               :: "v"(voff), "s"(rsrc), "s"(lds), "s"(soff) : "memory", "m0");
+}
+
+template <int R, bool PRIO, bool LEAN = false>
 __global__ __launch_bounds__(256, 1) void gemm_nt_w4_kernel(const GemmParams p) {
   static_assert(R >= 4 && R * SLOTB <= 163840, "ring");
   __shared__ __attribute__((aligned(16))) char smem[R * SLOTB];
@@ -548,8 +555,13 @@ __global__ __launch_bounds__(256, 1) void gemm_nt_w4_kernel(const GemmParams p) 
       a[i] = afrag(s + 1, i);
       {
         const uint32_t d = __builtin_amdgcn_readfirstlane(lds0 + dbuf + (i >> 2) * OPB + (i & 3) * 4096);
-        if (i < 4) bdma16(avoff, ra, (i & 3) * astep + jsrc * (GS * 2), d);
-        else bdma16(bvoff, rb, (i & 3) * bstep + jsrc * (GS * 2), d);
+        if constexpr (LEAN) {
+          if (i < 4) bdma16_lean(avoff, ra, (i & 3) * astep + jsrc * (GS * 2), d);
+          else bdma16_lean(bvoff, rb, (i & 3) * bstep + jsrc * (GS * 2), d);
+        } else {
+          if (i < 4) bdma16(avoff, ra, (i & 3) * astep + jsrc * (GS * 2), d);
+          else bdma16(bvoff, rb, (i & 3) * bstep + jsrc * (GS * 2), d);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -622,6 +634,10 @@ void gemm_nt(const GemmParams& p, hipStream_t stream) {
     else hipLaunchKernelGGL((gemm_nt_w4_kernel<5, true>), grid, dim3(256), 0, stream, p);
   } else if (variant == 6) {
     hipLaunchKernelGGL((gemm_nt_w4_kernel<5, false>), grid, dim3(256), 0, stream, p);
+  } else if (variant == 7) {
+    hipLaunchKernelGGL((gemm_nt_w4_kernel<4, false, true>), grid, dim3(256), 0, stream, p);
+  } else if (variant == 8) {
+    hipLaunchKernelGGL((gemm_nt_w4_kernel<5, false, true>), grid, dim3(256), 0, stream, p);
   } else if (variant == 3) {
     if (p.K % 64 == 0) hipLaunchKernelGGL((gemm_h_kernel<GEMM_EPI_STORE, false, false>), grid, block, 0, stream, p);
   } else if (variant == 1) hipLaunchKernelGGL((gemm_nt_kernel<GEMM_EPI_STORE, 1, 5>), grid, block, 0, stream, p);

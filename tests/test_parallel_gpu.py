@@ -212,3 +212,52 @@ def test_ddp_early_grad_norm_matches_full_norm(accum, bucket_mb):
         assert abs(float(st.buf[0]) - float(full)) <= 1e-3 * float(full), (step, float(st.buf[0]), float(full))
         assert abs(float(st.buf[1]) - float(ref.buf[1])) <= 1e-3 * float(ref.buf[1])
         ddp.zero_grad()
+
+
+@pytest.mark.parametrize("resident", [0.0, 0.5])
+def test_fsdp_overlapped_offload_matches_serial_offload(resident):
+    """The per-unit offloaded AdamW issued on side streams at step() and waited for by each unit's
+    next forward (parallel/offload.py), with part of the moments HBM-resident, gives bit-identical
+    parameters, moments and losses to the serial after-backward stream (same kernel, same data)."""
+    from gke_ray_train_amd.models.llama import LlamaForCausalLM, RMSNorm, get_config
+    from gke_ray_train_amd.parallel.fsdp import FullyShardedDataParallel
+    from gke_ray_train_amd.parallel.offload import OverlappedOffloadAdamW
+    cfg = get_config("llama-tiny-gqa")
+
+    def init(mod):
+        with torch.no_grad():
+            if isinstance(mod, (torch.nn.Linear, torch.nn.Embedding)):
+                mod.weight.normal_(0, 0.02)
+            elif isinstance(mod, RMSNorm):
+                mod.weight.fill_(1.0)
+    runs = []
+    for overlap in (False, True):
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(cfg, device="meta", dtype=torch.bfloat16)
+        f = FullyShardedDataParallel(m, param_init_fn=init, device="cuda", cpu_offload=True,
+                                     offload_chunk_elems=1 << 14)
+        opt = f.build_optimizer(lr=1e-3, overlap=overlap, resident_fraction=resident)
+        assert isinstance(opt, OverlappedOffloadAdamW) == overlap
+        if overlap:
+            assert (opt.resident_units > 0) == (resident > 0) and opt.resident_units < len(opt.segments)
+        g = torch.Generator(device="cuda").manual_seed(4)
+        losses = []
+        for _ in range(4):
+            ids = torch.randint(0, cfg.vocab_size, (2, 128), device="cuda", generator=g)
+            loss, _ = _step(f, opt, ids)
+            losses.append(loss)
+        sd = opt.state_dict()
+        torch.cuda.synchronize()
+        st = [v for s in sd["state"].values() for k, v in s.items() if k in ("exp_avg", "exp_avg_sq")]
+        runs.append((losses, f.shard_store.clone(), f.rep_flat.clone(), [t.clone() for t in st]))
+    # same kernel on the same data: identical in every run so far (tools/offload_debug.py); compared
+    # to bf16 rounding so that a reduction-order difference elsewhere in the step cannot flake it,
+    # while a stale-parameter race (a unit running before its update) still fails by far
+    for a, b in zip(runs[0][0], runs[1][0]):
+        assert abs(a - b) <= 1e-3 * abs(a), (runs[0][0], runs[1][0])
+    for a, b in ((runs[0][1], runs[1][1]), (runs[0][2], runs[1][2])):
+        d = (a.float() - b.float()).abs().max().item()
+        assert d <= 2e-2 * max(1.0, a.float().abs().max().item()), d
+    for a, b in zip(runs[0][3], runs[1][3]):
+        d = (a.cpu() - b.cpu()).abs().max().item()
+        assert d <= 1e-2 * max(1e-6, a.abs().max().item()), d
