@@ -82,6 +82,21 @@ def clip_grad_norm_(params_or_grads: Iterable, max_norm: float, prescale: float 
     return st
 
 
+# Bumped by every framework optimizer step. The fused kernels write parameters through raw device
+# pointers, which does not advance a tensor's autograd version counter, so caches derived from
+# trainable parameters (peft/lora.py's K-concatenated W' tail) key on this as well as on _version.
+_PARAM_GENERATION = 0
+
+
+def param_generation() -> int:
+    return _PARAM_GENERATION
+
+
+def bump_param_generation() -> None:
+    global _PARAM_GENERATION
+    _PARAM_GENERATION += 1
+
+
 class FusedAdamW(torch.optim.Optimizer):
     """AdamW with fp32 moments; bf16 or fp32 params (optionally with an fp32 master copy).
 
@@ -146,6 +161,7 @@ class FusedAdamW(torch.optim.Optimizer):
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: Optional[GradClipState] = None):
+        bump_param_generation()
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -197,6 +213,7 @@ class OffloadedAdamW(FusedAdamW):
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: Optional[GradClipState] = None):
+        bump_param_generation()
         for gi, group in enumerate(self.param_groups):
             lr = group["lr"]
             b1, b2 = group["betas"]

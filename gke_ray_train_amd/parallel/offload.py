@@ -30,7 +30,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import _native
-from ..ops.optim import GradClipState, OffloadedAdamW
+from ..ops.optim import GradClipState, OffloadedAdamW, bump_param_generation
 
 
 class OverlappedOffloadAdamW(OffloadedAdamW):
@@ -81,6 +81,7 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         dev = fs.device
         if dev.type != "cuda":
             return super().step(closure, grad_scale)
+        bump_param_generation()
         C = _native.kernels()
         if self._streams is None:
             self._streams = tuple(torch.cuda.Stream(dev) for _ in range(3))  # up, update, down

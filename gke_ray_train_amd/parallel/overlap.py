@@ -37,7 +37,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native
-from ..ops.optim import FusedAdamW, GradClipState
+from ..ops.optim import FusedAdamW, GradClipState, bump_param_generation
 from .ddp import DistributedDataParallel, forward_wait_modules
 
 
@@ -129,6 +129,7 @@ class OverlappedOptimizer:
 
     @torch.no_grad()
     def step(self, grad_scale: Optional[GradClipState] = None):
+        bump_param_generation()
         groups = self.engine.groups
         dev = groups[0].flat.device
         if dev.type != "cuda":

@@ -42,6 +42,7 @@ import torch.nn.functional as F
 
 from .. import _native, ops
 from ..ops.linear import input_grad
+from ..ops.optim import param_generation
 from .quant import NF4Linear
 
 
@@ -278,7 +279,7 @@ class _LoraKcatFn(torch.autograd.Function):
     one [dX | g] GEMM against W' was measured slower — its N = in + R is off the library's tiles."""
 
     @staticmethod
-    def forward(ctx, x, mod, p, seed, offset, *ab):
+    def forward(ctx, x, mod, p, seed, offset, train, *ab):
         k = len(mod.targets)
         As, Bs = ab[:k], ab[k:]
         M, K = x.shape
@@ -294,7 +295,9 @@ class _LoraKcatFn(torch.autograd.Function):
         else:
             xd = C.dropout_fwd_seeded(x.contiguous(), p, seed, offset) if p > 0 else x
             xw[:, K:].copy_((xd @ acat.t()) * s)
-        y = F.linear(xw, mod._kcat_weight(order, Bs))
+        y = F.linear(xw, mod._kcat_weight(order, Bs, reuse=not train))
+        if not train:  # no backward will run (evaluation / generation): nothing to keep
+            return y
         # a contiguous copy of h' for the dB GEMMs (rank-r slices of a 4K-wide row stride halve their speed)
         hc = xw[:, K:].contiguous()
         ctx.mod, ctx.order, ctx.p, ctx.seed, ctx.offset = mod, order, p, seed, offset
@@ -345,7 +348,7 @@ class _LoraKcatFn(torch.autograd.Function):
                     C.dropout_bwd_seeded(g @ acat, dx, ctx.p, ctx.seed, ctx.offset, True)
                 else:
                     dx.addmm_(g, acat)
-        return (dx, None, None, None, None, *dAs, *dBs)
+        return (dx, None, None, None, None, None, *dAs, *dBs)
 
 
 def _lora_dA(g, xd, As, order, r, C=None):
@@ -408,6 +411,7 @@ class LoraLinear(nn.Module):
         self._spec = [(off, n, name) for name, off, n in self.targets]
         self._wk = None     # K-concatenated weight [out, in + R] (built lazily)
         self._wk_order = None
+        self._wk_key = None  # (order, B versions, optimizer generation) the tail was last built from
         self._bt = None     # [R, out]: the B blocks transposed (adapter-gradient kernel), with W'
 
     @property
@@ -428,7 +432,7 @@ class LoraLinear(nn.Module):
         return R if ok and a0.dtype == torch.bfloat16 else 0
 
     @torch.no_grad()
-    def _kcat_weight(self, order, Bs):
+    def _kcat_weight(self, order, Bs, reuse: bool = False):
         """W' = [W | B_blockdiag] with the base part built once (frozen) and the B blocks of the h'
         column order ``order`` refreshed (every forward: B changes with each optimizer step)."""
         K, r = self.in_features, self.r
@@ -448,7 +452,16 @@ class LoraLinear(nn.Module):
         if self._wk_order != list(order):  # block positions moved: clear the whole tail once
             self._wk[:, K:].zero_()
             self._wk_order = list(order)
+            self._wk_key = None
         bl = [Bs[i].detach() for i in order]
+        # Forwards without autograd (``reuse``: evaluation, generation) reuse the tail while B is
+        # unchanged: same tensors, same version counters, no framework optimizer step since (the
+        # fused kernels write through raw pointers: ops.optim.param_generation). A forward that
+        # records a graph always refreshes and drops the key, so a training step never trusts it.
+        key = (tuple(order), tuple((b.data_ptr(), b._version) for b in bl), param_generation())
+        if reuse and self._wk_key == key:
+            return self._wk
+        self._wk_key = key if reuse else None
         offs = [self._spec[i][0] for i in order]
         if all(b.is_contiguous() for b in bl):
             # B^T [R, out] for the adapter-gradient kernel (lora_grad.hip lora_g): block j = B_{order[j]}^T
@@ -498,8 +511,9 @@ class LoraLinear(nn.Module):
             R = self.r * len(names)
             if (getattr(x, "_grt_tail", 0) == R and R and x.dim() == 2 and x.stride(1) == 1
                     and x.stride(0) == self.in_features + R and self.kcat_pad == R):
-                return _LoraKcatFn.apply(x, self, p, seed, offset,
-                                         *[self.lora_A[n] for n in names], *[self.lora_B[n] for n in names])
+                ab = [self.lora_A[n] for n in names] + [self.lora_B[n] for n in names]
+                train = torch.is_grad_enabled() and (x.requires_grad or any(t.requires_grad for t in ab))
+                return _LoraKcatFn.apply(x, self, p, seed, offset, train, *ab)
             spec = [(off, n) for _, off, n in self.targets]
             return _LoraFn.apply(x, self.base, spec, self.r, self.scaling, p, seed, offset,
                                  *[self.lora_A[n] for n in names], *[self.lora_B[n] for n in names])

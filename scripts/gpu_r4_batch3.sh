@@ -1,11 +1,10 @@
 #!/bin/bash
-# Round 4 batch 3: planner-vs-peak GPU test (LoRA / QLoRA), lean-DMA GEMM variants, reference SFT job
+# Round 4 batch 3: lean-DMA GEMM variants, reference SFT job
 # twice (unchanged config), kernel traces of its evaluation pass and of its training steps.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/r4b3; rm -rf $OUT; mkdir -p $OUT
 fatal() { case $1 in 124|134|137|139) echo "fatal rc $1"; exit $1;; esac; }
-timeout -k 10 500 python -u -m pytest -v --timeout 400 --timeout-method thread tests/test_planner_gpu.py > $OUT/planner.log 2>&1; rc=$?; grep -E "PASS|FAIL|Error|assert" $OUT/planner.log | tail -8; fatal $rc
 timeout -k 10 300 python -u tools/gemm_bench.py --set fwd --variants 3,4,7,8 --rounds 3 > $OUT/gemm.log 2>&1; rc=$?; grep '^{' $OUT/gemm.log; fatal $rc
 for i in 1 2; do
   export GRT_STORAGE_PATH=/tmp/grt_sftj$i

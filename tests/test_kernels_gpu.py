@@ -946,3 +946,58 @@ def test_kcat_lora_model_matches_epilogue_form(monkeypatch):
     for n in g0:
         rel = (g1[n] - g0[n]).norm() / g0[n].norm().clamp_min(1e-8)
         assert rel < 5e-2, f"{n}: rel {rel.item():.3g}"
+
+
+def test_kcat_lora_no_grad_forwards_reuse_tail_until_b_changes():
+    """Evaluation forwards (no autograd) of a K-concatenated LoRA projection skip the W' tail refresh
+    while B is unchanged, and pick up every change: an in-place torch edit (version counter), a
+    framework optimizer step (raw-pointer writes: ops.optim.param_generation) and a training
+    forward in between. Each result equals the grad-enabled forward of the same weights."""
+    from gke_ray_train_amd.ops.linear import Linear
+    from gke_ray_train_amd.ops.optim import FusedAdamW
+    from gke_ray_train_amd.peft.lora import LoraConfig, LoraLinear
+    torch.manual_seed(0)
+    lin = Linear(256, 512, bias=False, device=DEV, dtype=torch.bfloat16)
+    lin.slices = [("gate_proj", 256), ("up_proj", 256)]
+    lin.weight.requires_grad_(False)
+    mod = LoraLinear(lin, [("gate_proj", 0, 256), ("up_proj", 256, 256)], LoraConfig(r=64, lora_alpha=16,
+                                                                                    lora_dropout=0.0))
+    R = 128
+    assert mod.kcat_pad == R
+    xw = torch.randn(256, 256 + R, device=DEV, dtype=torch.bfloat16)
+
+    def fwd(grad):
+        x = xw[:, :256]
+        x._grt_tail = R
+        with torch.set_grad_enabled(grad):
+            return mod(x).detach().float()
+
+    def ref():
+        y = xw[:, :256].float() @ lin.weight.float().t()
+        for n, off in (("gate_proj", 0), ("up_proj", 256)):
+            y[:, off:off + 256] += mod.scaling * (xw[:, :256].float() @ mod.lora_A[n].float().t()) @ mod.lora_B[n].float().t()
+        return y
+
+    with torch.no_grad():
+        for b in mod.lora_B.values():
+            b.normal_(0, 0.05)
+    y0 = fwd(False)
+    _close(y0, ref(), 3e-2, 3e-2, "first no-grad forward")
+    key = mod._wk_key
+    assert key is not None
+    assert torch.equal(fwd(False), y0) and mod._wk_key == key  # reused
+    with torch.no_grad():
+        mod.lora_B["up_proj"].mul_(-2.0)  # version counter
+    _close(fwd(False), ref(), 3e-2, 3e-2, "after an in-place edit")
+    # an optimizer step through the fused kernel (no version bump)
+    opt = FusedAdamW([p for p in mod.parameters() if p.requires_grad], lr=1e-2)
+    xt = xw[:, :256].detach().requires_grad_()
+    xt._grt_tail = R
+    y = mod(xt)
+    y.float().square().mean().backward()
+    assert mod._wk_key is None  # a training forward refreshed and dropped the key
+    v = mod.lora_B["gate_proj"]._version
+    opt.step()
+    assert mod.lora_B["gate_proj"]._version == v
+    _close(fwd(False), ref(), 3e-2, 3e-2, "after a fused optimizer step")
+    _close(fwd(True), ref(), 3e-2, 3e-2, "grad-enabled forward")
