@@ -1108,6 +1108,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_schedule", &grt::attn_set_schedule,
         "bf16 attention causal-pair / XCD-grouped schedule, bit mask: 1 = forward, 2 = dQ, 4 = dK/dV");
   m.def("attn_get_schedule", &grt::attn_get_schedule);
+  m.def("attn_set_dkdv_form", &grt::attn_set_dkdv_form, "dK / dV kernel: 1 = 4-wave, 2 = wave-pair (default)");
+  m.def("attn_get_dkdv_form", &grt::attn_get_dkdv_form);
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);

@@ -177,6 +177,8 @@ struct AttnParams {
 };
 void attn_set_schedule(int s);
 int attn_get_schedule();
+void attn_set_dkdv_form(int f);  // 1 = 4-wave dK / dV kernel, 2 = wave-pair kernel (default)
+int attn_get_dkdv_form();
 void attn_fwd(const AttnParams& p, hipStream_t s);
 struct AttnBwdParams {
   AttnParams f;

@@ -739,6 +739,286 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   }
 }
 
+// dK / dV, wave-pair form (default without dropout; GRT_ATTN_DKDV=1 selects the 4-wave kernel above). The
+// 4-wave kernel holds K, V, dK^T and dV^T of its 32 keys in one wave (~440 registers: one wave per
+// SIMD, nothing covers its exponentials, LDS reads and barrier; 25 % MFMA busy,
+// profiles/r3_pmc_kernel_zoo.md). Here the work of 32 keys is split over a wave PAIR on one SIMD
+// (waves w and w + 4 share a SIMD):
+//   S-wave  (w < 4): K fragments, dV^T accumulators: S = Q K^T, P = exp2(c S - lse2) -> LDS,
+//                    dV^T += dO^T P;
+//   dP-wave (w >= 4): V fragments, dK^T accumulators: dP = dO V^T, then for the PREVIOUS tile
+//                    (whose P its partner published before this tile's barrier)
+//                    dS = P (dP - delta), dK^T += Q^T dS.
+// Each wave fits in < 256 registers, so two waves per SIMD hide each other's VALU / LDS latency.
+// The dP-wave lags one tile, so the ring keeps the previous tile's Q image resident: 5 slots, DMA
+// three tiles ahead (slot of tile t + 3 = slot of tile t - 2). P crosses LDS as fp32 (the numerics
+// of the 4-wave kernel), double-buffered by tile parity. One barrier per tile, plus one after the
+// sweep for the dP-wave's last tile. Same masks, dropout hash, RoPE epilogue and schedule.
+constexpr int K3N = 128, K3M = 32, K3NT = 512, K3NS = 5, K3PD = K3NS - 2;
+constexpr int K3IMG = K3M * D * 2;                // one 32-row image: 8 KiB
+constexpr int K3SLOT = 2 * K3IMG + 8 * 1024;      // Q image, dO image, 8 per-wave statistics copies
+constexpr int K3XW = 64 * 16 * 4;                 // one wave's P tile: 64 lanes x 16 fp32
+constexpr int K3X = 4 * K3XW;                     // the 4 pairs
+constexpr int K3LDS = K3NS * K3SLOT + 2 * K3X;    // 120 + 32 = 152 KiB
+
+template <bool DROP>
+__global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdParams P) {
+  const AttnParams& p = P.f;
+  __shared__ __attribute__((aligned(16))) char smem[K3LDS];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform
+  const int pr = w & 3;
+  const bool swave = w < 4;
+  const int g = lane >> 4, l16 = lane & 15;
+  const int BHk = p.B * p.Hkv;
+  const int nkb = (p.Sk + K3N - 1) / K3N;
+  QJobs jobs;
+  if (p.sched == 1) {
+    jobs = q_jobs(1, nkb, BHk);
+  } else {
+    jobs.bh = blockIdx.x % BHk;
+    jobs.blk0 = (int)(blockIdx.x / BHk);
+    jobs.blk1 = -1;
+  }
+  const int bhk = jobs.bh;
+  const int b = bhk / p.Hkv, hkv = bhk % p.Hkv;
+  const int grp = p.Hq / p.Hkv;
+  // one instantiation per role (SW: S-wave), so neither role's registers are live in the other's code
+  auto run_block = [&](const int kblk, auto role_c) __attribute__((always_inline)) {
+  constexpr bool SW = decltype(role_c)::value;
+  int Sq = p.Sq, Sk = p.Sk;
+  int64_t tok0 = 0;
+  if (p.cu_seqlens) {
+    tok0 = p.cu_seqlens[b];
+    Sq = Sk = p.cu_seqlens[b + 1] - (int)tok0;
+    if (kblk * K3N >= Sk) return;  // workgroup-uniform
+  }
+  GRT_DEVICE_CHECK(grp * p.Hkv == p.Hq && kblk * K3N < Sk);
+  const int sk = p.seqlens_k ? min(Sk, p.seqlens_k[b]) : Sk;
+  const int off = Sk - Sq;
+  const int k0 = kblk * K3N, kw0 = k0 + pr * 32, mykey = kw0 + l32;
+  const float c = p.scale * kLog2e;
+  const int Sqp = sq_pad(p.Sq);
+
+  // K (S-wave) or V (dP-wave) fragments of this lane's key, for the whole sweep
+  const bf16* KV = SW ? (const bf16*)p.k + (int64_t)b * p.k_bs + tok0 * p.k_ss + (int64_t)hkv * p.k_hs
+                         : (const bf16*)p.v + (int64_t)b * p.v_bs + tok0 * p.v_ss + (int64_t)hkv * p.v_hs;
+  const int64_t kv_ss = SW ? p.k_ss : p.v_ss;
+  bf16x8 kv[D / 16];
+#pragma unroll
+  for (int ks = 0; ks < D / 16; ++ks)
+    kv[ks] = mykey < sk ? *reinterpret_cast<const bf16x8*>(KV + (int64_t)mykey * kv_ss + ks * 16 + 8 * h) : bf16x8{};
+  f32x16 acc[4];  // dV^T (S-wave) / dK^T (dP-wave)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = f32x16{};
+
+  int qstart = p.causal ? max(0, k0 - off) : 0;
+  qstart = (qstart / K3M) * K3M;
+  const int nqt = qstart < Sq ? (Sq - qstart + K3M - 1) / K3M : 0;
+  const int total = (k0 < sk) ? nqt * grp : 0;
+  const int qlim = mykey < sk ? (p.causal ? mykey - off : INT_MIN) : INT_MAX;
+  const int qmask = (k0 + K3N > sk) ? INT_MAX : (p.causal ? kw0 + 31 - off : INT_MIN);
+
+  // LDS-DMA of a tile: wave w fills image rows 4w .. 4w+3 of Q and of dO (one 1-KiB piece each)
+  // and its own copy of the tile's 32 lse2 and 32 delta values (3 instructions per wave and tile)
+  const uint32_t smem0 = lds_u32(smem);
+  const int row = 4 * w + g, ch = l16 ^ img_swz(row);
+  const int64_t st_lane = ((l16 & 15) < 8 ? (int64_t)p.B * p.Hq * Sqp : 0) + 4 * (l16 & 7);  // lse2 | delta
+  auto dma_tile = [&](int hq, int qt, uint32_t slot_off) __attribute__((always_inline)) {
+    const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + tok0 * p.q_ss + (int64_t)hq * p.q_hs;
+    const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + tok0 * P.do_ss + (int64_t)hq * P.do_hs;
+    const int64_t qr = min(qt + row, Sq - 1);  // past Sq: lse2 = +inf, p = 0
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(4 * w * 256));
+    lds_dma16(Q + qr * p.q_ss + ch * 8, dst);
+    lds_dma16(dO + qr * P.do_ss + ch * 8, dst + K3IMG);
+    const int64_t ri = ((int64_t)b * p.Hq + hq) * Sqp + qt;
+    lds_dma16(P.delta + st_lane + ri, __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(2 * K3IMG + w * 1024)));
+  };
+  auto wait_dma = [&](int pending_tiles) __attribute__((always_inline)) {  // 3 DMA instructions per tile
+    if (pending_tiles >= 2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (pending_tiles == 1) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  float* const xbase = reinterpret_cast<float*>(smem + K3NS * K3SLOT) + pr * (K3XW / 4);
+
+  // tile cursors: consumed (cur), previous (prv: the dP-wave's lagging tile), DMA
+  int cur_h = 0, cur_q = qstart, prv_h = 0, prv_q = qstart, dma_h = 0, dma_q = qstart;
+  auto advance = [&](int& hh, int& qq) __attribute__((always_inline)) {
+    qq += K3M;
+    if (qq >= Sq) { qq = qstart; ++hh; }
+  };
+  f32x16 dpc = f32x16{};  // dP-wave: dP of the tile it finishes next
+
+  // dP-wave: finish tile `tp` (slot image `pi`, P in parity buffer of tp): dS, dK^T += Q^T dS
+  auto finish = [&](int tp, const char* pi) __attribute__((always_inline)) {
+    const float* st = reinterpret_cast<const float*>(pi + 2 * K3IMG + w * 1024);
+    const float* xi = xbase + (tp & 1) * (K3X / 4);
+    f32x16 ds;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 pv = *reinterpret_cast<const f32x4*>(xi + (q * 64 + lane) * 4);
+      const f32x4 de = *reinterpret_cast<const f32x4*>(st + 32 + 8 * q + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * q + j;
+        if (DROP) {
+          const float z = drop_factor(p, (uint32_t)(b * p.Hq + hkv * grp + prv_h), prv_q + 8 * q + 4 * h + j, mykey);
+          ds[r] = pv[j] * (dpc[r] * z - de[j]);
+        } else {
+          ds[r] = pv[j] * (dpc[r] - de[j]);
+        }
+      }
+    }
+    const bf16x8 sb0 = pack8(ds, 0), sb1 = pack8(ds, 8);
+    __builtin_amdgcn_sched_barrier(0);  // scheduling regions bound the live fragments (2 waves/SIMD)
+#pragma unroll
+    for (int stp = 0; stp < 2; ++stp) {
+      const int kk = 16 * stp + 4 * h;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int c0 = db * 32 + (g & 1) * 16;
+        const bf16x8 a = cat(lds_tr_read(pi, kk, c0, l16), lds_tr_read(pi, kk + 8, c0, l16));
+        acc[db] = mfma32(a, stp ? sb1 : sb0, acc[db]);
+      }
+    }
+  };
+
+  auto step = [&](int t, auto slot_c) __attribute__((always_inline)) {
+    constexpr int SL = decltype(slot_c)::value;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS reads / P stores done
+    wait_dma(min(total - 1, t + K3PD - 1) - t);           // tile t landed (this wave's pieces)
+    __builtin_amdgcn_s_barrier();                         // ... every wave's; P of tile t-1 published
+    if (t + K3PD < total) {
+      dma_tile(hkv * grp + dma_h, dma_q, (uint32_t)(((SL + K3PD) % K3NS) * K3SLOT));
+      advance(dma_h, dma_q);
+    }
+    const char* qi = smem + SL * K3SLOT;
+    if constexpr (SW) {
+      const float* st = reinterpret_cast<const float*>(qi + 2 * K3IMG + w * 1024);
+      f32x16 s = f32x16{};
+      if (cur_q < qmask) {  // wave-uniform: the tile touches the diagonal / key padding
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = cur_q + acc_row(r, h) >= qlim ? 0.f : -INFINITY;
+      }
+      bf16x8 fq[D / 16];
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) fq[ks] = lds_row_read(qi, l32, 2 * ks + h);
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) s = mfma32(fq[ks], kv[ks], s);
+      __builtin_amdgcn_sched_barrier(0);
+      float* xo = xbase + (t & 1) * (K3X / 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 ls = *reinterpret_cast<const f32x4*>(st + 8 * q + 4 * h);
+        f32x4 pv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pv[j] = fast_exp2(fmaf(s[4 * q + j], c, -ls[j]));
+        *reinterpret_cast<f32x4*>(xo + (q * 64 + lane) * 4) = pv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          s[4 * q + j] = DROP ? pv[j] * drop_factor(p, (uint32_t)(b * p.Hq + hkv * grp + cur_h),
+                                                    cur_q + 8 * q + 4 * h + j, mykey)
+                              : pv[j];  // dV uses the dropped probabilities
+      }
+      const bf16x8 pb0 = pack8(s, 0), pb1 = pack8(s, 8);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int stp = 0; stp < 2; ++stp) {
+        const int kk = 16 * stp + 4 * h;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const int c0 = db * 32 + (g & 1) * 16;
+          const bf16x8 a = cat(lds_tr_read(qi + K3IMG, kk, c0, l16), lds_tr_read(qi + K3IMG, kk + 8, c0, l16));
+          acc[db] = mfma32(a, stp ? pb1 : pb0, acc[db]);
+        }
+      }
+    } else {  // the previous tile first: its dP is the only one live (register budget of 2 waves/SIMD)
+      if (t > 0) finish(t - 1, smem + ((SL + K3NS - 1) % K3NS) * K3SLOT);
+      __builtin_amdgcn_sched_barrier(0);
+      bf16x8 fd[D / 16];
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) fd[ks] = lds_row_read(qi + K3IMG, l32, 2 * ks + h);
+      dpc = f32x16{};
+#pragma unroll
+      for (int ks = 0; ks < D / 16; ++ks) dpc = mfma32(fd[ks], kv[ks], dpc);
+    }
+    prv_h = cur_h;
+    prv_q = cur_q;
+    advance(cur_h, cur_q);
+  };
+
+  if (total > 0) {
+    const int pre = min(total, K3PD);
+    for (int j = 0; j < pre; ++j) {
+      dma_tile(hkv * grp + dma_h, dma_q, (uint32_t)(j * K3SLOT));
+      advance(dma_h, dma_q);
+    }
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    int t = 0;
+    for (; t + K3NS <= total; t += K3NS) {  // one ring revolution
+      step(t, I0{});
+      step(t + 1, I1{});
+      step(t + 2, I2{});
+      step(t + 3, I3{});
+      step(t + 4, I4{});
+    }
+    if (t < total) step(t, I0{});
+    if (t + 1 < total) step(t + 1, I1{});
+    if (t + 2 < total) step(t + 2, I2{});
+    if (t + 3 < total) step(t + 3, I3{});
+    // the dP-wave's last tile: its P is published at this barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if constexpr (!SW) finish(total - 1, smem + ((total - 1) % K3NS) * K3SLOT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  if (mykey < Sk) {
+    if constexpr (SW) {
+      bf16* dV = (bf16*)P.dv + (int64_t)b * P.dv_bs + (int64_t)hkv * P.dv_hs + (tok0 + mykey) * P.dv_ss;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int gg = 0; gg < 4; ++gg) {
+          bf16x4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(acc[db][4 * gg + j]);
+          *reinterpret_cast<bf16x4*>(dV + db * 32 + 8 * gg + 4 * h) = v;
+        }
+    } else {
+      bf16* dK = (bf16*)P.dk + (int64_t)b * P.dk_bs + (int64_t)hkv * P.dk_hs + (tok0 + mykey) * P.dk_ss;
+      if (P.rope_cos) {
+        store_unrotated(acc, p.scale, P.rope_cos + (int64_t)mykey * (D / 2), P.rope_sin + (int64_t)mykey * (D / 2), dK, h);
+      } else {
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int gg = 0; gg < 4; ++gg) {
+            bf16x4 a;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = static_cast<bf16>(acc[db][4 * gg + j] * p.scale);
+            *reinterpret_cast<bf16x4*>(dK + db * 32 + 8 * gg + 4 * h) = a;
+          }
+      }
+    }
+  }
+  };
+  auto run_role = [&](auto role_c) __attribute__((always_inline)) {
+    run_block(jobs.blk0, role_c);
+    if (jobs.blk1 >= 0) {  // every wave is done with the ring and the P buffers before they are refilled
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      run_block(jobs.blk1, role_c);
+    }
+  };
+  if (swave) run_role(std::true_type{});
+  else run_role(std::false_type{});
+}
+
 // dQ: the forward's mapping (32 query rows per wave on the MFMA lane, 4 waves = 128 rows) over
 // 32-key K / V tiles through the ring; S^T / dP^T are recomputed and dS^T feeds dQ^T += K^T dS^T.
 // 24 MFMAs per tile and wave; two workgroups per CU (64 KiB LDS each). Masking: -inf in the S^T
@@ -943,6 +1223,15 @@ namespace {
 // (-1: not set yet -> GRT_ATTN_SCHED, default 7: all three kernels pair when the paired grid fills
 // the chip; B8 S1024 H32: forward -10 %, backward -6 %: profiles/r3_attn_schedule.md)
 int g_sched = -1;
+// dK / dV kernel: 2 = wave-pair (default), 1 = the 4-wave kernel (GRT_ATTN_DKDV, attn_set_dkdv_form)
+int g_dkdv = -1;
+int dkdv_form() {
+  if (g_dkdv < 0) {
+    const char* e = getenv("GRT_ATTN_DKDV");
+    g_dkdv = e && atoi(e) == 1 ? 1 : 2;
+  }
+  return g_dkdv;
+}
 int sched_now() {
   if (g_sched < 0) {
     const char* e = getenv("GRT_ATTN_SCHED");
@@ -969,6 +1258,8 @@ static int pair_if_fills(int want, int nblk, int groups, int per_cu) {
 }
 
 void attn_set_schedule(int s) { g_sched = s; }
+void attn_set_dkdv_form(int f) { g_dkdv = f == 1 ? 1 : 2; }
+int attn_get_dkdv_form() { return dkdv_form(); }
 int attn_get_schedule() { return sched_now(); }
 
 // Padding-free packing (cu_seqlens): the grid is sized for the longest sequence, so a shorter one's
@@ -1001,11 +1292,18 @@ void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   pk.f.sched = pair_if_fills(sched_for(p.f, 2), nkb, p.f.B * p.f.Hkv, 1);
   pq.f.sched = pair_if_fills(sched_for(p.f, 1), nqb, p.f.B * p.f.Hq, 2);
   const dim3 g1(q_grid(pk.f.sched, nkb, p.f.B * p.f.Hkv)), g2(q_grid(pq.f.sched, nqb, p.f.B * p.f.Hq));
+  static_assert(K3N == K2N, "both dK / dV forms take 128-key blocks (same grid)");
+  // the wave-pair form: B8 S1024 H32 backward 425 -> 412 us, GQA 32:8 even; with probability
+  // dropout it is slower (142 -> 150 us at B2 S1024 p 0.1: the dP-wave recomputes the keep hash the
+  // S-wave already drew), so dropout keeps the 4-wave kernel (tools/attn_dkdv_ab.py, profiles/r4_attention.md)
+  const bool pair = dkdv_form() == 2 && !p.f.drop_thresh;
   if (p.f.drop_thresh) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, pk);
+    if (pair) hipLaunchKernelGGL(attn_bwd_dkdv2_kernel<true>, g1, dim3(K3NT), 0, s, pk);
+    else hipLaunchKernelGGL(attn_bwd_dkdv_kernel<true>, g1, dim3(K2NT), 0, s, pk);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<true>, g2, dim3(Q2NT), 0, s, pq);
   } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(K2NT), 0, s, pk);
+    if (pair) hipLaunchKernelGGL(attn_bwd_dkdv2_kernel<false>, g1, dim3(K3NT), 0, s, pk);
+    else hipLaunchKernelGGL(attn_bwd_dkdv_kernel<false>, g1, dim3(K2NT), 0, s, pk);
     hipLaunchKernelGGL(attn_bwd_dq_kernel<false>, g2, dim3(Q2NT), 0, s, pq);
   }
 }

@@ -1001,3 +1001,39 @@ def test_kcat_lora_no_grad_forwards_reuse_tail_until_b_changes():
     assert mod.lora_B["gate_proj"]._version == v
     _close(fwd(False), ref(), 3e-2, 3e-2, "after a fused optimizer step")
     _close(fwd(True), ref(), 3e-2, 3e-2, "grad-enabled forward")
+
+
+@pytest.mark.parametrize("B,S,hq,hkv,causal,pad,p,rope", [
+    (2, 256, 4, 4, True, None, 0.0, False),
+    (1, 200, 4, 2, True, None, 0.0, True),        # partial tail block, GQA, RoPE epilogue
+    (2, 160, 2, 2, False, [160, 77], 0.0, False),  # key padding
+    (2, 256, 4, 2, True, None, 0.1, False),        # probability dropout
+    (8, 1024, 32, 32, True, None, 0.0, False),     # Llama-2-7B bench shape (causal pairs)
+    (2, 2048, 32, 8, True, None, 0.0, True),       # Llama-3 GQA 32:8
+])
+def test_dkdv_wave_pair_matches_four_wave_kernel(B, S, hq, hkv, causal, pad, p, rope):
+    """The wave-pair dK / dV kernel (attention.hip attn_bwd_dkdv2_kernel, S-wave + dP-wave per 32
+    keys) does the 4-wave kernel's arithmetic in the same order: dQ / dK / dV bitwise equal."""
+    from gke_ray_train_amd import _native
+    from gke_ray_train_amd.ops import _ref
+    C = _native.kernels()
+    D = 128
+    g = torch.Generator(device=DEV).manual_seed(B * S + hq)
+    q, do = (torch.randn(B, S, hq, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(2))
+    k, v = (torch.randn(B, S, hkv, D, device=DEV, dtype=torch.bfloat16, generator=g) for _ in range(2))
+    sl = None if pad is None else torch.tensor(pad, device=DEV, dtype=torch.int32)
+    cos = sin = None
+    if rope:
+        cos, sin = _ref.rope_tables(S, D, 10000.0, device=DEV)
+        cos, sin = cos.float().contiguous(), sin.float().contiguous()
+    o, lse = C.attn_fwd(q, k, v, None, D ** -0.5, causal, sl, p, 11)
+    out = {}
+    try:
+        for form in (1, 2):
+            C.attn_set_dkdv_form(form)
+            out[form] = C.attn_bwd(do, q, k, v, o, lse, None, None, None, D ** -0.5, causal, sl, p, 11, cos, sin)
+        torch.cuda.synchronize()
+    finally:
+        C.attn_set_dkdv_form(2)
+    for name, a, b in zip(("dq", "dk", "dv"), out[1], out[2]):
+        assert torch.equal(a, b), f"{name}: max diff {(a.float() - b.float()).abs().max().item():.3g}"
