@@ -1,7 +1,7 @@
 #!/bin/bash
 # BASELINE config #2 through the reference SFT job (full FT, Llama-2-7B): log every library GEMM the
 # shipped table misses (padding-free packed steps of 4.5-8 K tokens, multiples of 512), tune them
-# offline (poison-checked), then A/B the job and bench.py at the job's tokens/step on both tables.
+# offline (poison-checked). The A/B of the job / bench.py on both tables is scripts/gpu_sft_full_ab.sh.
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r4ft}; rm -rf $O; mkdir -p $O
@@ -12,14 +12,6 @@ GRT_TUNED_GEMM_RECORD_UNTUNED=$PWD/$O/untuned.csv timeout -k 10 300 $FT > $O/rec
 grep -E "tokens_per_sec|training finished" $O/record.log | cut -c1-200; fatal $rc; [ $rc = 0 ] || exit $rc
 GRT_TUNED_GEMM_RECORD_UNTUNED=$PWD/$O/untuned_b6.csv timeout -k 10 200 python3 bench.py --batch 6 --steps 3 --warmup 2 > $O/record_b6.log 2>&1; rc=$?; fatal $rc
 ls $O; cat $O/untuned*.csv | grep -c Gemm
-timeout -k 10 1500 python3 tools/tune_untuned.py "$O/untuned*.csv" --out $O/tuned.csv > $O/tune.log 2>&1; rc=$?
-tail -3 $O/tune.log; fatal $rc; [ $rc = 0 ] || exit $rc
-for r in 1 2; do
-  timeout -k 10 300 $FT > $O/ab_old_$r.log 2>&1; rc=$?; fatal $rc
-  GRT_TUNED_GEMM_FILE=$PWD/$O/tuned.csv timeout -k 10 300 $FT > $O/ab_new_$r.log 2>&1; rc=$?; fatal $rc
-  grep -h "tokens_per_sec" $O/ab_old_$r.log | tail -3 | cut -c1-160
-  grep -h "tokens_per_sec" $O/ab_new_$r.log | tail -3 | cut -c1-160
-done
-timeout -k 10 200 python3 bench.py --batch 6 --steps 20 --warmup 5 > $O/b6_old.log 2>&1; rc=$?; tail -1 $O/b6_old.log | cut -c1-200; fatal $rc
-GRT_TUNED_GEMM_FILE=$PWD/$O/tuned.csv timeout -k 10 200 python3 bench.py --batch 6 --steps 20 --warmup 5 > $O/b6_new.log 2>&1; rc=$?; tail -1 $O/b6_new.log | cut -c1-200; fatal $rc
+timeout -k 10 ${TUNE_S:-840} python3 tools/tune_untuned.py "$O/untuned*.csv" --out $O/tuned.csv > $O/tune.log 2>&1; rc=$?
+tail -3 $O/tune.log; fatal $rc
 echo done

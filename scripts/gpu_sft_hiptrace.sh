@@ -1,0 +1,15 @@
+#!/bin/bash
+# HIP runtime API trace + kernel trace of the reference SFT job's worker loop (QLoRA, 160 samples =
+# 20 optimizer steps, no eval / save): which host calls block between steps.
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/${1:-sfthip}
+rm -rf $O; mkdir -p $O
+export GRT_STORAGE_PATH=/tmp/grt_sfth
+cd /tmp && timeout -k 10 400 rocprofv3 --hip-trace --kernel-trace --output-format csv -d $O -o run \
+  -- python3 $GRAFT_REPO_ROOT/tools/sft_inproc.py --set NUM_TRAIN_SAMPLES=160 --set EVAL_STEPS_SFT=1000 --set SAVE_STEPS_SFT=1000 --set OUTPUT_DIR_BASE=/tmp/grt_sfth/out > $O/log.txt 2>&1
+rc=$?
+cd $GRAFT_REPO_ROOT
+grep "train_samples_per_second" $O/log.txt | tail -1 | cut -c1-200
+find $O -name "*.csv" -size +20M -exec gzip {} \;
+ls -la $O
+exit $rc
