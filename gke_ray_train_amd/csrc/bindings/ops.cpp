@@ -3,6 +3,7 @@
 // Every op launches on the caller's current HIP stream (graph-capturable: no allocation
 // besides the torch caching allocator, no synchronisation) and checks shapes/strides on the
 // host BEFORE launch so a hand-written kernel never sees operands its grid does not expect.
+#include <climits>
 #include <torch/extension.h>
 
 #include <algorithm>
@@ -404,45 +405,101 @@ static bool rowmajor_bf16(const Tensor& t) {
 
 // c [M, 64] (+)= alpha * a [M, K] @ bt^T, bt = B^T [64, K] (lora_grad.hip); all row-major with unit
 // column stride (row-strided views allowed). Returns false (nothing done) when unsupported.
-bool lora_g(const Tensor& a, const Tensor& bt, const Tensor& c, double alpha, bool accumulate) {
-  if (!rowmajor_bf16(a) || !rowmajor_bf16(bt) || !rowmajor_bf16(c)) return false;
-  const int64_t M = a.size(0);
-  const int K = (int)a.size(1);
-  if (bt.size(0) != c.size(1) || bt.size(1) != K || c.size(0) != M || !grt::lora_g_supported(M, K, (int)c.size(1)) ||
-      c.stride(0) % 4 != 0)
-    return false;
-  c10::OptionalDeviceGuard dg(c.device());
+// lora_g_group: up to 4 such products of the same M (one adapted module's targets) in one launch.
+static bool lora_g_impl(const std::vector<Tensor>& as, const std::vector<Tensor>& bts, const std::vector<Tensor>& cs,
+                        double alpha, bool accumulate) {
+  const int n = (int)as.size();
+  if (n < 1 || n > grt::kLoraGMax || (int)bts.size() != n || (int)cs.size() != n) return false;
   grt::LoraGParams p{};
-  p.a = a.data_ptr(); p.lda = a.stride(0); p.bt = bt.data_ptr(); p.ldbt = bt.stride(0);
-  p.c = c.data_ptr(); p.ldc = c.stride(0); p.M = M; p.K = K; p.alpha = (float)alpha; p.accumulate = accumulate ? 1 : 0;
-  p.ks = grt::lora_g_splits(M, K, device_cus(c.get_device()));
+  const int64_t M = as[0].size(0);
+  int kmax = 0;
+  for (int t = 0; t < n; ++t) {
+    const Tensor &a = as[t], &bt = bts[t], &c = cs[t];
+    if (!rowmajor_bf16(a) || !rowmajor_bf16(bt) || !rowmajor_bf16(c)) return false;
+    const int K = (int)a.size(1);
+    if (a.size(0) != M || bt.size(0) != c.size(1) || bt.size(1) != K || c.size(0) != M ||
+        !grt::lora_g_supported(M, K, (int)c.size(1)) || c.stride(0) % 4 != 0 || c.get_device() != cs[0].get_device())
+      return false;
+    p.a[t] = a.data_ptr(); p.lda[t] = a.stride(0); p.bt[t] = bt.data_ptr(); p.ldbt[t] = bt.stride(0);
+    p.c[t] = c.data_ptr(); p.ldc[t] = c.stride(0); p.K[t] = K;
+    kmax = std::max(kmax, K);
+  }
+  for (int t = n; t < grt::kLoraGMax; ++t) {  // unused slots mirror product 0 (never indexed)
+    p.a[t] = p.a[0]; p.lda[t] = p.lda[0]; p.bt[t] = p.bt[0]; p.ldbt[t] = p.ldbt[0];
+    p.c[t] = p.c[0]; p.ldc[t] = p.ldc[0]; p.K[t] = p.K[0];
+  }
+  const Tensor& c0 = cs[0];
+  c10::OptionalDeviceGuard dg(c0.device());
+  p.nprod = n; p.M = M; p.alpha = (float)alpha; p.accumulate = accumulate ? 1 : 0;
+  int kmin = kmax;
+  for (int t = 0; t < n; ++t) kmin = std::min(kmin, p.K[t]);
+  p.ks = grt::lora_g_splits(M, kmin, device_cus(c0.get_device()), n);
   Tensor ws;
   if (p.ks > 1) {
-    ws = at::empty({(int64_t)p.ks * M * 64}, c.options().dtype(at::kFloat));
+    ws = at::empty({(int64_t)n * p.ks * M * 64}, c0.options().dtype(at::kFloat));
     p.ws = ws.data_ptr<float>();
   }
-  grt::lora_g(p, cur_stream(c));
+  grt::lora_g(p, cur_stream(c0));
   return true;
+}
+
+bool lora_g(const Tensor& a, const Tensor& bt, const Tensor& c, double alpha, bool accumulate) {
+  return lora_g_impl({a}, {bt}, {c}, alpha, accumulate);
+}
+
+bool lora_g_group(const std::vector<Tensor>& as, const std::vector<Tensor>& bts, const std::vector<Tensor>& cs,
+                  double alpha, bool accumulate) {
+  return lora_g_impl(as, bts, cs, alpha, accumulate);
 }
 
 // out (+)= alpha * a^T @ h, a [M, N], h [M, R]: out [N, R], or [R, N] when transpose (lora_grad.hip);
 // fp32 token-split partials in a workspace from the caching allocator. False when unsupported.
-bool lora_tred(const Tensor& a, const Tensor& h, const Tensor& out, double alpha, bool accumulate, bool transpose) {
-  if (!rowmajor_bf16(a) || !rowmajor_bf16(h) || !rowmajor_bf16(out)) return false;
-  const int64_t M = a.size(0);
-  const int N = (int)a.size(1), R = (int)h.size(1);
-  if (h.size(0) != M || !grt::lora_tred_supported(M, N, R)) return false;
-  if (transpose ? (out.size(0) != R || out.size(1) != N) : (out.size(0) != N || out.size(1) != R)) return false;
-  if (out.stride(0) % 4 != 0) return false;
-  c10::OptionalDeviceGuard dg(out.device());
+// lora_tred_group: up to 4 such products of the same M and R (non-transposed; one adapted module's
+// dB_i) in one launch, each assigning or accumulating.
+static bool lora_tred_impl(const std::vector<Tensor>& as, const std::vector<Tensor>& hs, const std::vector<Tensor>& outs,
+                           double alpha, const std::vector<bool>& accumulate, bool transpose) {
+  const int n = (int)as.size();
+  if (n < 1 || n > grt::kLoraTredMax || (int)hs.size() != n || (int)outs.size() != n || (int)accumulate.size() != n ||
+      (transpose && n != 1))
+    return false;
+  const int64_t M = as[0].size(0);
+  const int R = (int)hs[0].size(1);
   grt::LoraTredParams p{};
-  p.ks = grt::lora_tred_splits(M, N, R, device_cus(out.get_device()));
-  Tensor ws = at::empty({(int64_t)p.ks * N * R}, out.options().dtype(at::kFloat));
-  p.a = a.data_ptr(); p.lda = a.stride(0); p.h = h.data_ptr(); p.ldh = h.stride(0); p.ws = ws.data_ptr<float>();
-  p.M = M; p.N = N; p.R = R; p.out = out.data_ptr(); p.ldo = out.stride(0);
-  p.transpose = transpose ? 1 : 0; p.accumulate = accumulate ? 1 : 0; p.alpha = (float)alpha;
-  grt::lora_tred(p, cur_stream(out));
+  int nbt = 0;
+  for (int t = 0; t < n; ++t) {
+    const Tensor &a = as[t], &h = hs[t], &out = outs[t];
+    if (!rowmajor_bf16(a) || !rowmajor_bf16(h) || !rowmajor_bf16(out)) return false;
+    const int N = (int)a.size(1);
+    if (a.size(0) != M || h.size(0) != M || h.size(1) != R || !grt::lora_tred_supported(M, N, R)) return false;
+    if (transpose ? (out.size(0) != R || out.size(1) != N) : (out.size(0) != N || out.size(1) != R)) return false;
+    if (out.stride(0) % 4 != 0 || out.get_device() != outs[0].get_device()) return false;
+    p.a[t] = a.data_ptr(); p.lda[t] = a.stride(0); p.h[t] = h.data_ptr(); p.ldh[t] = h.stride(0);
+    p.out[t] = out.data_ptr(); p.ldo[t] = out.stride(0); p.N[t] = N; p.bo[t] = nbt;
+    p.accumulate[t] = accumulate[t] ? 1 : 0;
+    nbt += N / 128;
+  }
+  for (int t = n; t < grt::kLoraTredMax; ++t) {  // unused slots: never selected (bo past every block)
+    p.a[t] = p.a[0]; p.lda[t] = p.lda[0]; p.h[t] = p.h[0]; p.ldh[t] = p.ldh[0];
+    p.out[t] = p.out[0]; p.ldo[t] = p.ldo[0]; p.N[t] = p.N[0]; p.bo[t] = INT_MAX; p.accumulate[t] = 0;
+  }
+  const Tensor& o0 = outs[0];
+  c10::OptionalDeviceGuard dg(o0.device());
+  p.nprod = n; p.nbt = nbt; p.M = M; p.R = R;
+  p.ks = grt::lora_tred_splits(M, nbt * 128, R, device_cus(o0.get_device()));
+  Tensor ws = at::empty({(int64_t)p.ks * nbt * 128 * R}, o0.options().dtype(at::kFloat));
+  p.ws = ws.data_ptr<float>();
+  p.transpose = transpose ? 1 : 0; p.alpha = (float)alpha;
+  grt::lora_tred(p, cur_stream(o0));
   return true;
+}
+
+bool lora_tred(const Tensor& a, const Tensor& h, const Tensor& out, double alpha, bool accumulate, bool transpose) {
+  return lora_tred_impl({a}, {h}, {out}, alpha, {accumulate}, transpose);
+}
+
+bool lora_tred_group(const std::vector<Tensor>& as, const std::vector<Tensor>& hs, const std::vector<Tensor>& outs,
+                     double alpha, const std::vector<bool>& accumulate) {
+  return lora_tred_impl(as, hs, outs, alpha, accumulate, false);
 }
 
 // B_i [n_i, r] -> the adapter tail of W' [out, ldw] (columns col0 + j r ..) and of W'^T [.., ldt]
@@ -1086,8 +1143,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lora_refresh", &lora_refresh, py::arg("bs"), py::arg("offs"), py::arg("w"), py::arg("wt"), py::arg("col0"),
         py::arg("wt_row0") = -1);
   m.def("lora_g", &lora_g, py::arg("a"), py::arg("bt"), py::arg("c"), py::arg("alpha"), py::arg("accumulate"));
+  m.def("lora_g_group", &lora_g_group, py::arg("a"), py::arg("bt"), py::arg("c"), py::arg("alpha"),
+        py::arg("accumulate"));
   m.def("lora_tred", &lora_tred, py::arg("a"), py::arg("h"), py::arg("out"), py::arg("alpha"), py::arg("accumulate"),
         py::arg("transpose"));
+  m.def("lora_tred_group", &lora_tred_group, py::arg("a"), py::arg("h"), py::arg("out"), py::arg("alpha"),
+        py::arg("accumulate"));
   m.def("dropout_bwd_seeded", &dropout_bwd_seeded);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);

@@ -131,21 +131,32 @@ bool lora_dx_supported(int64_t M, int K, int R, uint64_t offset);
 void lora_dx(const LoraDxParams& p, hipStream_t s);
 
 // ---------------- LoRA gradient GEMMs (lora_grad.hip) ----------------
-// C[M][64] (+)= alpha * A[M][K] B[K][64], from B^T [64][K] (row stride ldbt)
+// C[M][64] (+)= alpha * A[M][K] B[K][64], from B^T [64][K] (row stride ldbt). Up to 4 products
+// of the same M (the targets of one adapted module: grid y = product) in one launch; product t
+// uses a[t], bt[t], c[t] with reduction length K[t].
+constexpr int kLoraGMax = 4;
 struct LoraGParams {
-  const void* a; int64_t lda; const void* bt; int64_t ldbt; void* c; int64_t ldc;
-  int64_t M; int K; float alpha; int accumulate;
-  int ks = 1; float* ws = nullptr;  // k splits (lora_g_splits) through the fp32 workspace [ks][M][64]
+  const void* a[kLoraGMax]; int64_t lda[kLoraGMax]; const void* bt[kLoraGMax]; int64_t ldbt[kLoraGMax];
+  void* c[kLoraGMax]; int64_t ldc[kLoraGMax]; int K[kLoraGMax];
+  int nprod = 1;
+  int64_t M; float alpha; int accumulate;
+  int ks = 1; float* ws = nullptr;  // k splits (lora_g_splits) through the fp32 workspace [nprod][ks][M][64]
 };
 bool lora_g_supported(int64_t M, int K, int r);
-int lora_g_splits(int64_t M, int K, int cus);
+int lora_g_splits(int64_t M, int K, int cus, int nprod = 1);
 void lora_g(const LoraGParams& p, hipStream_t s);
 // out (+)= alpha * A^T H, A [M][N], H [M][R]: out [N][R] (row stride ldo), or [R][N] when transpose;
 // ks token splits through the fp32 workspace ws [ks][N * R] (lora_tred_splits)
+// Up to 4 products of the same M and R in one launch (the dB_i of one adapted module's targets):
+// product t owns the 128-column blocks [bo[t], bo[t] + N[t] / 128) of the launch; its partials
+// sit at column offset 128 bo[t] of each split's [sum N][R] plane.
+constexpr int kLoraTredMax = 4;
 struct LoraTredParams {
-  const void* a; int64_t lda; const void* h; int64_t ldh; float* ws;
-  int64_t M; int N; int R; int ks; int64_t mchunk;
-  void* out; int64_t ldo; int transpose; int accumulate; float alpha;
+  const void* a[kLoraTredMax]; int64_t lda[kLoraTredMax]; const void* h[kLoraTredMax]; int64_t ldh[kLoraTredMax];
+  void* out[kLoraTredMax]; int64_t ldo[kLoraTredMax]; int N[kLoraTredMax]; int bo[kLoraTredMax];
+  int accumulate[kLoraTredMax];
+  int nprod = 1; int nbt;  // products, total column blocks
+  float* ws; int64_t M; int R; int ks; int64_t mchunk; int transpose; float alpha;
 };
 bool lora_tred_supported(int64_t M, int N, int R);
 int lora_tred_splits(int64_t M, int N, int R, int cus);

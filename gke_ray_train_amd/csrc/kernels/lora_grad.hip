@@ -81,19 +81,29 @@ __device__ __forceinline__ void wait_pending(int pending) {
 // private images with register staging — B^T re-read per wave — ran at ~half the HBM rate; 128-row
 // workgroups needed a 4-way k-split and a finalize launch per product: profiles/r3_lora_grad_gemms.md.)
 // With fewer than 256 row blocks the k-tiles are split over ks workgroups (fp32 partials, lora_g_fin).
+// product t's entry of a parameter array: selects on the wave-uniform index (a dynamically indexed
+// by-value kernel argument would be copied to scratch)
+template <class T>
+__device__ __forceinline__ T pick(const T (&v)[kLoraGMax], int t) {
+  return t == 0 ? v[0] : t == 1 ? v[1] : t == 2 ? v[2] : v[3];
+}
+
 __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
   __shared__ __attribute__((aligned(16))) char smem[G_NS * G_SLOT];
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4, l16 = lane & 15;
+  const int pt = blockIdx.y;  // product
   const int nrb = (int)((P.M + 31) / 32);
   const int rb = blockIdx.x % nrb, ksi = blockIdx.x / nrb;
   const int64_t m0 = (int64_t)rb * 32;
-  const int nkt_all = P.K / 128;
+  const int K = pick(P.K, pt);
+  const int64_t lda = pick(P.lda, pt), ldbt = pick(P.ldbt, pt), ldc = pick(P.ldc, pt);
+  const int nkt_all = K / 128;
   const int kt0 = ksi * nkt_all / P.ks;
   const int nt = (ksi + 1) * nkt_all / P.ks - kt0;
-  const bf16* A = static_cast<const bf16*>(P.a);
-  const bf16* BT = static_cast<const bf16*>(P.bt);
+  const bf16* A = static_cast<const bf16*>(pick(P.a, pt));
+  const bf16* BT = static_cast<const bf16*>(pick(P.bt, pt));
   // DMA sources: wave w fills A rows 8w..8w+7 (2 pieces of 4 rows) and B^T rows 16w..16w+15
   // (4 pieces); piece row 4p + g4, the XOR swizzle on the per-lane source chunk
   const bf16* asrc[2];
@@ -101,13 +111,13 @@ __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
   for (int q = 0; q < 2; ++q) {
     const int r = 8 * w + 4 * q + g4;
     const int64_t m = min(m0 + r, P.M - 1);
-    asrc[q] = A + m * P.lda + (int64_t)kt0 * 128 + 8 * (l16 ^ swz16(r));
+    asrc[q] = A + m * lda + (int64_t)kt0 * 128 + 8 * (l16 ^ swz16(r));
   }
   const bf16* bsrc[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int r = 16 * w + 4 * q + g4;
-    bsrc[q] = BT + (int64_t)r * P.ldbt + (int64_t)kt0 * 128 + 8 * (l16 ^ swz16(r));
+    bsrc[q] = BT + (int64_t)r * ldbt + (int64_t)kt0 * 128 + 8 * (l16 ^ swz16(r));
   }
   const uint32_t smem0 = lds_addr(smem);
   auto dma_tile = [&](int t, int slot) {
@@ -165,12 +175,12 @@ __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
     sum[4] += b[0]; sum[5] += b[1]; sum[6] += b[2]; sum[7] += b[3];
   }
   if (P.ks > 1) {  // fp32 partial of this k range; lora_g_fin sums them
-    float* ws = P.ws + ((int64_t)ksi * P.M + m) * 64 + c8;
+    float* ws = P.ws + (((int64_t)pt * P.ks + ksi) * P.M + m) * 64 + c8;
     *reinterpret_cast<f32x4*>(ws) = f32x4{sum[0], sum[1], sum[2], sum[3]};
     *reinterpret_cast<f32x4*>(ws + 4) = f32x4{sum[4], sum[5], sum[6], sum[7]};
     return;
   }
-  bf16* C = static_cast<bf16*>(P.c) + m * P.ldc + c8;
+  bf16* C = static_cast<bf16*>(pick(P.c, pt)) + m * ldc + c8;
   bf16x8 o;
   const bf16x8 old = P.accumulate ? *reinterpret_cast<const bf16x8*>(C) : bf16x8{};
 #pragma unroll
@@ -178,15 +188,18 @@ __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
   *reinterpret_cast<bf16x8*>(C) = o;
 }
 
-// C[m][0..63] (+)= alpha * sum_k ws[k][m][..]
+// C[m][0..63] (+)= alpha * sum_k ws[k][m][..] (grid y = product)
 __global__ __launch_bounds__(256) void lora_g_fin_kernel(const LoraGParams P) {
+  const int pt = blockIdx.y;
   const int64_t n4 = P.M * 16, plane = P.M * 64;
-  bf16* C = static_cast<bf16*>(P.c);
+  bf16* C = static_cast<bf16*>(pick(P.c, pt));
+  const int64_t ldc = pick(P.ldc, pt);
+  const float* ws = P.ws + (int64_t)pt * P.ks * plane;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
     const int64_t m = e >> 4, c = (e & 15) * 4;
-    f32x4 s = *reinterpret_cast<const f32x4*>(P.ws + 4 * e);
-    for (int k = 1; k < P.ks; ++k) s += *reinterpret_cast<const f32x4*>(P.ws + k * plane + 4 * e);
-    bf16x4* dst = reinterpret_cast<bf16x4*>(C + m * P.ldc + c);
+    f32x4 s = *reinterpret_cast<const f32x4*>(ws + 4 * e);
+    for (int k = 1; k < P.ks; ++k) s += *reinterpret_cast<const f32x4*>(ws + k * plane + 4 * e);
+    bf16x4* dst = reinterpret_cast<bf16x4*>(C + m * ldc + c);
     bf16x4 o;
     const bf16x4 old = P.accumulate ? *dst : bf16x4{};
 #pragma unroll
@@ -217,13 +230,16 @@ __global__ __launch_bounds__(256) void lora_tred_kernel(const LoraTredParams P) 
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g4 = lane >> 4, l16 = lane & 15;
-  const int nblk = P.N / 128;
-  const int nb = blockIdx.x % nblk, ks = blockIdx.x / nblk;
+  const int gb = blockIdx.x % P.nbt, ks = blockIdx.x / P.nbt;  // column block of the launch, split
+  const int pt = (gb >= P.bo[1]) + (gb >= P.bo[2]) + (gb >= P.bo[3]);  // product (bo past nprod: INT_MAX)
+  const int nb = gb - pick(P.bo, pt);
+  const int N = pick(P.N, pt);
+  const int64_t lda = pick(P.lda, pt), ldh = pick(P.ldh, pt);
   const int64_t mbeg = (int64_t)ks * P.mchunk;
   const int64_t mend = min(P.M, mbeg + P.mchunk);
   const int nt = mend > mbeg ? (int)((mend - mbeg) / 32) : 0;
-  const bf16* A = static_cast<const bf16*>(P.a) + (int64_t)nb * 128;
-  const bf16* H = static_cast<const bf16*>(P.h);
+  const bf16* A = static_cast<const bf16*>(pick(P.a, pt)) + (int64_t)nb * 128;
+  const bf16* H = static_cast<const bf16*>(pick(P.h, pt));
 
   // LDS-DMA of tile t: wave w fills image rows 8w .. 8w+7 (two 1-KiB pieces of 4 rows) of the A
   // image and of every H image; the XOR swizzle is applied to the per-lane SOURCE chunk. H images
@@ -234,14 +250,14 @@ __global__ __launch_bounds__(256) void lora_tred_kernel(const LoraTredParams P) 
   auto dma_tile = [&](int t, int slot) {
     const int64_t r0 = mbeg + 32 * t + row0, r1 = mbeg + 32 * t + row1;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + (uint32_t)(slot * SLOT + 8 * w * 256));
-    dma16(A + r0 * P.lda + 8 * ch0, dst);
-    dma16(A + r1 * P.lda + 8 * ch1, dst + 1024);
+    dma16(A + r0 * lda + 8 * ch0, dst);
+    dma16(A + r1 * lda + 8 * ch1, dst + 1024);
 #pragma unroll
     for (int hi = 0; hi < NHI; ++hi) {
       const int valid = (R - 128 * hi) >= 128 ? 16 : (R - 128 * hi) / 8;  // chunks of this image inside R
       const int c0 = 128 * hi + 8 * (ch0 % valid), c1 = 128 * hi + 8 * (ch1 % valid);
-      dma16(H + r0 * P.ldh + c0, dst + (1 + hi) * TR_IMG);
-      dma16(H + r1 * P.ldh + c1, dst + (1 + hi) * TR_IMG + 1024);
+      dma16(H + r0 * ldh + c0, dst + (1 + hi) * TR_IMG);
+      dma16(H + r1 * ldh + c1, dst + (1 + hi) * TR_IMG + 1024);
     }
   };
 
@@ -282,7 +298,7 @@ __global__ __launch_bounds__(256) void lora_tred_kernel(const LoraTredParams P) 
 #pragma unroll
     for (int r = 0; r < 16; ++r) tile[(32 * w + acc_row32(r, hh)) * TS + 32 * j + l32] = acc[j][r];
   __syncthreads();
-  float* ws = P.ws + (int64_t)ks * P.N * R;
+  float* ws = P.ws + ((int64_t)ks * P.nbt + pick(P.bo, pt)) * 128 * R;  // this product's plane of the split
   if (!P.transpose) {  // ws[n][j]: thread -> 4 consecutive j of one n
     for (int e = tid; e < 128 * R / 4; e += 256) {
       const int n = e / (R / 4), j4 = (e % (R / 4)) * 4;
@@ -294,23 +310,29 @@ __global__ __launch_bounds__(256) void lora_tred_kernel(const LoraTredParams P) 
       f32x4 v;
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = tile[(n4 + q) * TS + j];
-      *reinterpret_cast<f32x4*>(ws + (int64_t)j * P.N + nb * 128 + n4) = v;
+      *reinterpret_cast<f32x4*>(ws + (int64_t)j * N + nb * 128 + n4) = v;
     }
   }
 }
 
-// out[row][col] (+)= alpha * sum_ks ws[ks][row][col], rows x cols = N x R (or R x N transposed)
+// out_t[row][col] (+)= alpha * sum_ks ws[ks][plane of t][row][col], rows x cols = N_t x R (or R x N_t
+// transposed); grid y = product
 __global__ __launch_bounds__(256) void lora_tred_fin_kernel(const LoraTredParams P) {
-  const int64_t rows = P.transpose ? P.R : P.N, cols = P.transpose ? P.N : P.R;
-  const int64_t n4 = rows * cols / 4, plane = (int64_t)P.N * P.R;
-  bf16* out = static_cast<bf16*>(P.out);
+  const int pt = blockIdx.y;
+  const int N = pick(P.N, pt);
+  const int64_t rows = P.transpose ? P.R : N, cols = P.transpose ? N : P.R;
+  const int64_t n4 = rows * cols / 4, plane = (int64_t)P.nbt * 128 * P.R;
+  const float* ws = P.ws + (int64_t)pick(P.bo, pt) * 128 * P.R;
+  bf16* out = static_cast<bf16*>(pick(P.out, pt));
+  const int64_t ldo = pick(P.ldo, pt);
+  const bool acc = pick(P.accumulate, pt) != 0;
   for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)gridDim.x * 256) {
     const int64_t row = (4 * e) / cols, col = (4 * e) % cols;
-    f32x4 s = *reinterpret_cast<const f32x4*>(P.ws + 4 * e);
-    for (int k = 1; k < P.ks; ++k) s += *reinterpret_cast<const f32x4*>(P.ws + k * plane + 4 * e);
-    bf16x4* dst = reinterpret_cast<bf16x4*>(out + row * P.ldo + col);
+    f32x4 s = *reinterpret_cast<const f32x4*>(ws + 4 * e);
+    for (int k = 1; k < P.ks; ++k) s += *reinterpret_cast<const f32x4*>(ws + k * plane + 4 * e);
+    bf16x4* dst = reinterpret_cast<bf16x4*>(out + row * ldo + col);
     bf16x4 o;
-    if (P.accumulate) {
+    if (acc) {
       const bf16x4 old = *dst;
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = static_cast<bf16>(static_cast<float>(old[q]) + P.alpha * s[q]);
@@ -326,9 +348,10 @@ __global__ __launch_bounds__(256) void lora_tred_fin_kernel(const LoraTredParams
 
 bool lora_g_supported(int64_t M, int K, int r) { return M > 0 && K > 0 && K % 128 == 0 && r == 64; }
 
-// k splits: only when the 32-row blocks leave a quarter of the CUs idle (one 96 KiB workgroup per CU); at most 8
-int lora_g_splits(int64_t M, int K, int cus) {
-  const int64_t nrb = (M + 31) / 32;
+// k splits: only when the 32-row blocks (of all products) leave a quarter of the CUs idle (one 96 KiB
+// workgroup per CU); at most 8
+int lora_g_splits(int64_t M, int K, int cus, int nprod) {
+  const int64_t nrb = (M + 31) / 32 * nprod;
   if (4 * nrb >= 3 * (int64_t)cus) return 1;  // >= 3/4 of the CUs busy: no partials, no finalize launch
   int ks = (int)((cus + nrb - 1) / nrb);
   if (ks > 8) ks = 8;
@@ -337,12 +360,12 @@ int lora_g_splits(int64_t M, int K, int cus) {
 }
 
 void lora_g(const LoraGParams& p, hipStream_t s) {
-  const dim3 grid((unsigned)(((p.M + 31) / 32) * p.ks)), block(256);
+  const dim3 grid((unsigned)(((p.M + 31) / 32) * p.ks), (unsigned)p.nprod), block(256);
   hipLaunchKernelGGL(lora_g_kernel, grid, block, 0, s, p);
   if (p.ks > 1) {
     int64_t fb = (p.M * 16 + 255) / 256;
     if (fb > 1024) fb = 1024;
-    hipLaunchKernelGGL(lora_g_fin_kernel, dim3((unsigned)fb), block, 0, s, p);
+    hipLaunchKernelGGL(lora_g_fin_kernel, dim3((unsigned)fb, (unsigned)p.nprod), block, 0, s, p);
   }
 }
 
@@ -367,16 +390,18 @@ void lora_tred(const LoraTredParams& p0, hipStream_t s) {
   LoraTredParams p = p0;
   const int64_t tiles = p.M / 32;
   p.mchunk = 32 * ((tiles + p.ks - 1) / p.ks);
-  const dim3 grid((unsigned)((p.N / 128) * p.ks)), block(256);
+  const dim3 grid((unsigned)(p.nbt * p.ks)), block(256);
   switch (p.R) {
     case 64: hipLaunchKernelGGL(lora_tred_kernel<2>, grid, block, 0, s, p); break;
     case 128: hipLaunchKernelGGL(lora_tred_kernel<4>, grid, block, 0, s, p); break;
     default: hipLaunchKernelGGL(lora_tred_kernel<6>, grid, block, 0, s, p); break;
   }
-  const int64_t n4 = (int64_t)p.N * p.R / 4;
+  int nmax = 0;
+  for (int t = 0; t < p.nprod; ++t) nmax = p.N[t] > nmax ? p.N[t] : nmax;
+  const int64_t n4 = (int64_t)nmax * p.R / 4;
   int64_t fb = (n4 + 255) / 256;
   if (fb > 1024) fb = 1024;
-  hipLaunchKernelGGL(lora_tred_fin_kernel, dim3((unsigned)fb), block, 0, s, p);
+  hipLaunchKernelGGL(lora_tred_fin_kernel, dim3((unsigned)fb, (unsigned)p.nprod), block, 0, s, p);
 }
 
 }  // namespace grt

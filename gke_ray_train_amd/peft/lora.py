@@ -320,14 +320,38 @@ class _LoraKcatFn(torch.autograd.Function):
         g = torch.empty(M, r * k, device=dy2.device, dtype=dy2.dtype)  # dL/dh (unscaled h) = s dY_i B_i
         dBs: List[Optional[torch.Tensor]] = [None] * k
         bt = getattr(mod, "_bt", None) if _LORA_GRAD_KERNELS and _bf16_cuda(dy2, hc) else None
+        # g_i = s dY_i B_i of every target in one launch (B_i^T: rows j r .. of the B^T buffer
+        # lora_refresh filled in this step's forward)
+        g_done = bt is not None and C.lora_g_group(
+            [dy2[:, mod._spec[i][0]:mod._spec[i][0] + mod._spec[i][1]] for i in order],
+            [bt[j * r:(j + 1) * r, mod._spec[i][0]:mod._spec[i][0] + mod._spec[i][1]] for j, i in enumerate(order)],
+            [g[:, j * r:(j + 1) * r] for j in range(len(order))], s, False)
+        # dB_i = dY_i^T h'_i of every target in one launch, into the gradient slots (or new tensors)
+        db_done = False
+        if _LORA_GRAD_KERNELS and _bf16_cuda(dy2, hc) and len(order) > 1:
+            slots = [_slot_of(Bs[i]) for i in order]
+            outs = [sl.view if sl is not None else torch.empty(mod._spec[i][1], r, device=dy2.device, dtype=dy2.dtype)
+                    for sl, i in zip(slots, order)]
+            db_done = C.lora_tred_group(
+                [dy2[:, mod._spec[i][0]:mod._spec[i][0] + mod._spec[i][1]] for i in order],
+                [hc[:, j * r:(j + 1) * r] for j in range(len(order))], outs, 1.0,
+                [sl is not None and not sl.fresh for sl in slots])
+            if db_done:
+                for sl, o, i in zip(slots, outs, order):
+                    if sl is not None:
+                        sl.fresh, sl.direct = False, True
+                        sl.notify(Bs[i])
+                    else:
+                        dBs[i] = o
         for j, i in enumerate(order):
             off, n, _ = mod._spec[i]
             dyi = dy2[:, off:off + n]
             hj = hc[:, j * r:(j + 1) * r]                    # h' = s h: dB_i = dY_i^T h'_i
             gj = g[:, j * r:(j + 1) * r]
-            # B_i^T: rows j r .. of the B^T buffer lora_refresh filled in this step's forward
-            if not (bt is not None and C.lora_g(dyi, bt[j * r:(j + 1) * r, off:off + n], gj, s, False)):
+            if not (g_done or (bt is not None and C.lora_g(dyi, bt[j * r:(j + 1) * r, off:off + n], gj, s, False))):
                 gj.addmm_(dyi, Bs[i], beta=0.0, alpha=s)
+            if db_done:
+                continue
             sl = _slot_of(Bs[i])
             if sl is not None:
                 sl.write(lambda v: _tred_into(C, dyi, hj, v, 1.0, False, False) or v.addmm_(dyi.t(), hj, beta=0.0),

@@ -44,6 +44,49 @@ def test_lora_g(M, K, accumulate):
     assert torch.equal(gbuf[:, :64], before[:, :64]) and torch.equal(gbuf[:, 128:], before[:, 128:])
 
 
+@pytest.mark.parametrize("M", [200, 6016, 8192])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_lora_g_group(M, accumulate):
+    """One launch for the targets of a fused module (q / k / v column blocks of one dY, their B^T
+    rows, their g column blocks); equals the per-target products, incl. the k-split path (small M)."""
+    torch.manual_seed(3)
+    C = _C()
+    ns = [(0, 1024), (1024, 256), (1280, 256)]  # (offset, width) of q / k / v in the fused dY
+    dy = torch.randn(M, 1536, device=DEV, dtype=torch.bfloat16)
+    btbuf = torch.randn(192, 1536, device=DEV, dtype=torch.bfloat16) * 0.05
+    g = torch.randn(M, 192, device=DEV, dtype=torch.bfloat16)
+    before = g.clone()
+    a = [dy[:, o:o + n] for o, n in ns]
+    bt = [btbuf[64 * j:64 * (j + 1), o:o + n] for j, (o, n) in enumerate(ns)]
+    c = [g[:, 64 * j:64 * (j + 1)] for j in range(3)]
+    assert C.lora_g_group(a, bt, c, 0.5, accumulate)
+    for j in range(3):
+        ref = 0.5 * (a[j].float() @ bt[j].float().t()) + (before[:, 64 * j:64 * (j + 1)].float() if accumulate else 0)
+        _check(c[j], ref, f"lora_g_group M{M} product {j}")
+    assert not C.lora_g_group(a + a[:2], bt + bt[:2], c + c[:2], 0.5, False)  # more than 4 products
+
+
+@pytest.mark.parametrize("M", [384, 6016])
+def test_lora_tred_group(M):
+    """dB_i = dY_i^T h'_i of a fused module's targets in one launch: column blocks of one dY against
+    their own h' column blocks, each product assigning or accumulating into its own output."""
+    torch.manual_seed(4)
+    C = _C()
+    ns = [(0, 1024), (1024, 256), (1280, 256)]
+    dy = torch.randn(M, 1536, device=DEV, dtype=torch.bfloat16)
+    hc = torch.randn(M, 192, device=DEV, dtype=torch.bfloat16)
+    outs = [torch.randn(n, 64, device=DEV, dtype=torch.bfloat16) for _, n in ns]
+    before = [o.clone() for o in outs]
+    acc = [False, True, False]
+    a = [dy[:, o:o + n] for o, n in ns]
+    h = [hc[:, 64 * j:64 * (j + 1)] for j in range(3)]
+    assert C.lora_tred_group(a, h, outs, 1.0, acc)
+    for j in range(3):
+        ref = a[j].float().t() @ h[j].float() + (before[j].float() if acc[j] else 0)
+        _check(outs[j], ref, f"lora_tred_group M{M} product {j}")
+    assert not C.lora_tred_group(a, [hc[:, :128]] + h[1:], outs, 1.0, acc)  # R differs
+
+
 @pytest.mark.parametrize("M,N,R", [(384, 256, 64), (8192, 4096, 64), (2048, 1024, 128), (1024, 11008, 64),
                                    (4096, 4096, 192)])
 @pytest.mark.parametrize("transpose", [False, True])
