@@ -307,7 +307,8 @@ class LlamaForCausalLM(nn.Module):
             if attention_mask is not None:
                 shifted[:, :-1].masked_fill_(attention_mask[:, 1:] == 0, -100)
             if varlen is not None:  # a sequence's last token does not predict the next sequence's first
-                shifted[0, varlen.cu[1:].long() - 1] = -100
+                # index_fill_ with a device index: no host scalar upload (a blocking copy per step)
+                shifted[0].index_fill_(0, varlen.cu[1:].long() - 1, -100)
             out["loss"] = self.lm_head(x, labels=shifted.view(-1), row_weights=rw)
         if (labels is None and shifted_labels is None) or return_logits:
             out["logits"] = self.lm_head(x).view(B, S, -1)

@@ -82,6 +82,34 @@ def clip_grad_norm_(params_or_grads: Iterable, max_norm: float, prescale: float 
     return st
 
 
+# Hyper-parameter uploads (lr, betas, bias corrections, ...) go through a small ring of pinned host
+# buffers: a pageable torch.tensor(...) -> device copy is a blocking hipMemcpy that waits for the
+# stream, i.e. a host-device sync inside every optimizer step. A ring slot is reused only after the
+# event of its previous copy completed (normally long before).
+_PINNED_HYPER: dict = {}
+
+
+def upload_hyper(hb: torch.Tensor, values) -> None:
+    """hb (10 fp32 on the device) <- values, asynchronously on the current stream."""
+    if hb.device.type != "cuda":
+        hb.copy_(torch.tensor(values, dtype=torch.float32))
+        return
+    ring = _PINNED_HYPER.get(hb.data_ptr())
+    if ring is None:
+        ring = _PINNED_HYPER[hb.data_ptr()] = [[torch.empty(hb.numel(), dtype=torch.float32, pin_memory=True), None]
+                                               for _ in range(4)] + [0]
+    i = ring[-1]
+    ring[-1] = (i + 1) % 4
+    buf, ev = ring[i]
+    if ev is not None:
+        ev.synchronize()
+    buf.numpy()[:] = values
+    hb.copy_(buf, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    ring[i][1] = ev
+
+
 # Bumped by every framework optimizer step. The fused kernels write parameters through raw device
 # pointers, which does not advance a tensor's autograd version counter, so caches derived from
 # trainable parameters (peft/lora.py's K-concatenated W' tail) key on this as well as on _version.
@@ -152,9 +180,8 @@ class FusedAdamW(torch.optim.Optimizer):
                 st["step"] += 1
                 step = float(st["step"])
                 hb = self._hyper_buf(p.device, (gi,))
-                hb.copy_(torch.tensor([group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** step,
-                                       1.0 - b2 ** step, 1.0, self._sr(), step], dtype=torch.float32),
-                         non_blocking=True)
+                upload_hyper(hb, [group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** step,
+                                  1.0 - b2 ** step, 1.0, self._sr(), step])
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                 out.append((p, g, st["exp_avg"], st["exp_avg_sq"], st.get("master"), hb))
         return out
@@ -181,8 +208,7 @@ class FusedAdamW(torch.optim.Optimizer):
                 master = st.get("master")
                 if p.is_cuda:
                     hb = self._hyper_buf(p.device, (gi,))
-                    hb.copy_(torch.tensor([lr, b1, b2, eps, wd, bc1, bc2, 1.0, self._sr(), step],
-                                          dtype=torch.float32), non_blocking=True)
+                    upload_hyper(hb, [lr, b1, b2, eps, wd, bc1, bc2, 1.0, self._sr(), step])
                     g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
                     _native.kernels().adamw(p.data, g, st["exp_avg"], st["exp_avg_sq"], master, hb,
                                             None if grad_scale is None else grad_scale.buf)
@@ -232,8 +258,7 @@ class OffloadedAdamW(FusedAdamW):
                 st["step"] += 1
                 step = float(st["step"])
                 hb = self._hyper_buf(p.device, (gi,))
-                hb.copy_(torch.tensor([lr, b1, b2, eps, wd, 1.0 - b1 ** step, 1.0 - b2 ** step, 1.0, self._sr(), step]),
-                         non_blocking=True)
+                upload_hyper(hb, [lr, b1, b2, eps, wd, 1.0 - b1 ** step, 1.0 - b2 ** step, 1.0, self._sr(), step])
                 self._stream_update(p, st, hb, grad_scale)
 
     NSLOT = 3

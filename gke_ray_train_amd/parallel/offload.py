@@ -30,7 +30,7 @@ from typing import Dict, List, Optional
 import torch
 
 from .. import _native
-from ..ops.optim import GradClipState, OffloadedAdamW, bump_param_generation
+from ..ops.optim import GradClipState, OffloadedAdamW, bump_param_generation, upload_hyper
 
 
 class OverlappedOffloadAdamW(OffloadedAdamW):
@@ -98,12 +98,18 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
                 st["step"] += 1
                 step = float(st["step"])
                 hb = self._hyper_buf(p.device, (gi,))
-                hb.copy_(torch.tensor([group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** step,
-                                       1.0 - b2 ** step, 1.0, self._sr(), step]), non_blocking=True)
+                upload_hyper(hb, [group["lr"], b1, b2, group["eps"], group["weight_decay"], 1.0 - b1 ** step,
+                                  1.0 - b2 ** step, 1.0, self._sr(), step])
                 work.append((p, st, hb))
         entry = torch.cuda.Event()
         entry.record(comp)  # gradients, clip coefficient and hyper-parameters of this step
         gs = None if grad_scale is None else grad_scale.buf
+        if gs is not None:
+            # the clip state is read by every unit's update on the update stream, which runs under
+            # the next forward: a caller that drops it right after step() (a fresh GradClipState per
+            # step) must not let the allocator hand its memory to that forward before the updates ran
+            # (the flaky loss mismatch of tests/test_parallel_gpu.py's overlapped-offload test)
+            gs.record_stream(upd)
         (sp, sst, shb), (rp, rst, rhb) = work[0], work[1]
         for s in (up, upd, down):
             s.wait_event(entry)

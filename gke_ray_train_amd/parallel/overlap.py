@@ -151,6 +151,8 @@ class OverlappedOptimizer:
         start.record(cur)
         C = _native.kernels()
         gs = None if grad_scale is None else grad_scale.buf
+        if gs is not None:  # read by the chunks on the side stream: not reusable before they ran
+            gs.record_stream(self._stream)
         from ..ops.linear import register_transposed
         with torch.cuda.stream(self._stream):
             self._stream.wait_event(start)
