@@ -94,10 +94,15 @@ def upload_hyper(hb: torch.Tensor, values) -> None:
     if hb.device.type != "cuda":
         hb.copy_(torch.tensor(values, dtype=torch.float32))
         return
-    ring = _PINNED_HYPER.get(hb.data_ptr())
+    values = [float(v) for v in values]
+    key = (hb.data_ptr(), hb.device.index)
+    ring = _PINNED_HYPER.get(key)
     if ring is None:
-        ring = _PINNED_HYPER[hb.data_ptr()] = [[torch.empty(hb.numel(), dtype=torch.float32, pin_memory=True), None]
-                                               for _ in range(4)] + [0]
+        ring = _PINNED_HYPER[key] = [[torch.empty(hb.numel(), dtype=torch.float32, pin_memory=True), None]
+                                     for _ in range(4)] + [0]
+    if getattr(hb, "_grt_hyper", None) == values:  # this buffer already holds them (one upload per step)
+        return
+    hb._grt_hyper = values
     i = ring[-1]
     ring[-1] = (i + 1) % 4
     buf, ev = ring[i]

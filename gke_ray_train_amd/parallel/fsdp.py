@@ -145,7 +145,8 @@ class FullyShardedDataParallel(nn.Module):
         if self.dtype == torch.float32 and first.device.type != "meta":
             self.dtype = first.dtype
         # ---------------------------------------------------------------- shard stores
-        self._replaced = {}
+        self._replaced = {}      # id(original parameter) -> its materialised replacement
+        self._replaced_keep = []  # the originals, alive until construction ends: no id() is reused
         tot = sum(u.shard_numel for u in self.units)
         self.shard_store = torch.zeros(tot, dtype=self.dtype, device=self.device)
         self.grad_store = torch.zeros(tot, dtype=self.dtype, device=self.device)
@@ -164,9 +165,11 @@ class FullyShardedDataParallel(nn.Module):
                                     requires_grad=p.requires_grad)
                 setattr(m, n, newp)
                 self._replaced[id(p)] = newp
+                self._replaced_keep.append(p)
             if own and param_init_fn is not None:
                 param_init_fn(m)
         self.replicated = [(n, self._replaced.get(id(p), p)) for n, p in self.replicated]
+        self._replaced_keep = []
         rn = sum(p.numel() for _, p in self.replicated)
         self.rep_flat = torch.zeros(max(rn, 1), dtype=self.dtype, device=self.device)
         self.rep_grad = torch.zeros(max(rn, 1), dtype=self.dtype, device=self.device)
@@ -230,6 +233,7 @@ class FullyShardedDataParallel(nn.Module):
                                         requires_grad=p.requires_grad)
                     setattr(m, n, newp)
                     repl[id(p)] = newp
+                    self._replaced_keep.append(p)
                 if init_fn is not None:
                     init_fn(m)
             u.params = [repl.get(id(p), p) for p in u.params]
