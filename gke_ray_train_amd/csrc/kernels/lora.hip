@@ -20,6 +20,8 @@
 // or store; MFMA fragments are read from padded LDS images (a first version loaded the fragments
 // straight from global memory — 32 rows x 32 B per instruction, address-unit bound, 2-4x slower:
 // profiles/r2_perf_experiments.md).
+#include <stdlib.h>
+
 #include "grt_common.h"
 #include "grt_kernels.h"
 
@@ -67,7 +69,7 @@ constexpr int lora_down_lds_bytes() {  // x images + A images; the final reducti
 // TB: 32-token tiles per workgroup. The kernel is bound by the A chunk loads from L2 (one [R][KC]
 // chunk per workgroup per chunk: R / 32 times the x bytes at TB = 1; profiles/r2_perf_experiments.md),
 // so TB = 2 halves them per x byte: wave w takes token tile w % TB and k-slice w / TB of each chunk.
-template <int RB, int KC, int TB>  // R = 32 * RB
+template <int RB, int KC, int TB, int AD = 1>  // R = 32 * RB
 __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) {
   constexpr int R = 32 * RB;
   constexpr int XS = KC + 8;         // LDS row (bf16): +16 B so b128 fragment reads of 32 rows spread over banks
@@ -120,9 +122,15 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
 #pragma unroll
         for (int v = 0; v < NV; ++v) ring[i][u][v] = *reinterpret_cast<const bf16x8*>(src[u] + i * KC + 8 * v);
     }
-  bf16x8 areg[NA];
+  // A chunks AD ahead in registers (GRT_LORA_DOWN_AD selects 1 or 2 at launch: template AD)
+  bf16x8 areg[AD][NA];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * (256 / TPA) * P.K);
+  for (int d = 0; d < AD; ++d)
+    if (d < nch) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j)
+        areg[d][j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * (256 / TPA) * P.K + d * KC);
+    }
   f32x16 acc[RB];
 #pragma unroll
   for (int i = 0; i < RB; ++i) acc[i] = f32x16{};
@@ -146,12 +154,14 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
         // c - 2, which every wave finished before the barrier of chunk c - 1
         bf16* xt = xs + (i & 1) * XIMG;
         bf16* at = as + (i & 1) * AIMG;
+        constexpr int ad = AD;  // register set of chunk c: (c mod AD), c0 a multiple of LD_PF (a multiple of AD)
+        bf16x8(&ar_c)[NA] = areg[i % ad];
 #pragma unroll
-        for (int j = 0; j < NA; ++j) *reinterpret_cast<bf16x8*>(at + (ar + (256 / TPA) * j) * XS + ac) = areg[j];
-        if (c + 1 < nch) {
+        for (int j = 0; j < NA; ++j) *reinterpret_cast<bf16x8*>(at + (ar + (256 / TPA) * j) * XS + ac) = ar_c[j];
+        if (c + ad < nch) {
 #pragma unroll
           for (int j = 0; j < NA; ++j)
-            areg[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * (256 / TPA) * P.K + (c + 1) * KC);
+            ar_c[j] = *reinterpret_cast<const bf16x8*>(asrc + (int64_t)j * (256 / TPA) * P.K + (c + ad) * KC);
         }
 #pragma unroll
         for (int u = 0; u < TB; ++u)
@@ -206,6 +216,161 @@ __global__ __launch_bounds__(256) void lora_down_kernel(const LoraDownParams P) 
             f32x4{acc[rb][4 * q], acc[rb][4 * q + 1], acc[rb][4 * q + 2], acc[rb][4 * q + 3]};
   } else if (tok < P.M) {
     bf16* hrow = static_cast<bf16*>(P.h) + tok * (P.ldh > 0 ? P.ldh : (int64_t)R);
+    const float hs = P.hscale;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bf16x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(acc[rb][4 * q + j] * hs);
+        *reinterpret_cast<bf16x4*>(hrow + rb * 32 + 8 * q + 4 * h) = v;
+      }
+  }
+}
+
+// ---- lora_down, LDS-DMA form (default for R = 64 / 128 / 192). The register-staged kernel above
+// moves every x and A chunk through VGPRs into LDS (ds_write_b128: ~79 B/clk per CU, the A chunk is
+// R / 32 times the x chunk per 32 tokens); here both arrive by LDS-DMA (global_load_lds_dwordx4,
+// 1 KiB per wave-instruction, XOR-swizzled 128-byte rows: conflict-free b128 fragment reads) into a
+// 4-slot ring with a counted vmcnt across raw s_barriers (lora_grad.hip's pipeline). 64 tokens x
+// 64 columns per chunk; wave w takes token tile w & 1 and k-steps 2 (w >> 1), +1 of each chunk.
+// The dropout mask is applied to the x fragment in registers and x_d (XD) is stored from it.
+constexpr int LDD_NS = 4;                      // ring slots
+constexpr int LDD_KC = 64;                     // columns per chunk (128-byte rows)
+__device__ __forceinline__ int swz128(int r) { return (r >> 1) & 7; }
+__device__ __forceinline__ void dma16_lds(const void* gptr, uint32_t lds_byte_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(gptr), "s"(lds_byte_addr) : "memory", "m0");
+}
+
+template <int RB, bool XD>  // R = 32 RB
+__global__ __launch_bounds__(256) void lora_down_dma_kernel(const LoraDownParams P) {
+  constexpr int R = 32 * RB;
+  constexpr int XIMG = 64 * 128, AIMG = R * 128, SLOT = XIMG + AIMG;
+  constexpr int D = 2 + RB;        // DMA instructions per wave and chunk (2 x pieces + RB A pieces)
+  constexpr int S = XD ? 2 : 0;    // x_d stores per wave and chunk
+  __shared__ __attribute__((aligned(16))) char smem[LDD_NS * SLOT > 2 * RB * 16 * 64 * 4 ? LDD_NS * SLOT
+                                                                                     : 2 * RB * 16 * 64 * 4];
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tt = w & 1, ksl = w >> 1;
+  const int ntb = (int)((P.M + 63) / 64);
+  const int tb = blockIdx.x % ntb, ksi = blockIdx.x / ntb;
+  const int nch_all = P.K / LDD_KC;
+  const int c_lo = ksi * nch_all / P.ksplit;
+  const int nch = (ksi + 1) * nch_all / P.ksplit - c_lo;
+  const int64_t t0 = (int64_t)tb * 64;
+  const bf16* X = static_cast<const bf16*>(P.x);
+  const bf16* A = static_cast<const bf16*>(P.a);
+  // DMA sources: lane l of a piece covers row (piece row 0) + (l >> 3), LDS position l & 7, source
+  // chunk (l & 7) ^ swz(row). x: wave w fills rows 16 w .. 16 w + 15 (2 pieces); A: rows 8 RB w ..
+  const int pr = lane >> 3, pp = lane & 7;
+  const bf16* xsrc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int r = 16 * w + 8 * q + pr;
+    const int64_t tok = min(t0 + r, P.M - 1);
+    xsrc[q] = X + tok * (int64_t)P.ldx + (int64_t)c_lo * LDD_KC + 8 * (pp ^ swz128(r));
+  }
+  const bf16* asrc[RB];
+#pragma unroll
+  for (int q = 0; q < RB; ++q) {
+    const int r = 8 * RB * w + 8 * q + pr;
+    asrc[q] = A + (int64_t)r * P.K + (int64_t)c_lo * LDD_KC + 8 * (pp ^ swz128(r));
+  }
+  const uint32_t smem0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)(smem);
+  auto dma_chunk = [&](int c, int slot) __attribute__((always_inline)) {
+    const uint32_t base = smem0 + (uint32_t)(slot * SLOT);
+    const uint32_t dx = __builtin_amdgcn_readfirstlane(base + (uint32_t)(16 * w * 128));
+    const uint32_t da = __builtin_amdgcn_readfirstlane(base + (uint32_t)(XIMG + 8 * RB * w * 128));
+#pragma unroll
+    for (int q = 0; q < 2; ++q) dma16_lds(xsrc[q] + c * LDD_KC, dx + q * 1024);
+#pragma unroll
+    for (int q = 0; q < RB; ++q) dma16_lds(asrc[q] + c * LDD_KC, da + q * 1024);
+  };
+  // vmcnt: ops younger than chunk t's DMA are nd later chunks' DMAs and ns x_d store groups
+  auto wait_chunk = [&](int nd, int ns) __attribute__((always_inline)) {
+    switch (nd * 3 + ns) {
+      case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(S) : "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * S) : "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(D) : "memory"); break;
+      case 4: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(D + S) : "memory"); break;
+      case 5: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(D + 2 * S) : "memory"); break;
+      case 6: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * D) : "memory"); break;
+      case 7: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * D + S) : "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * D + 2 * S) : "memory"); break;
+    }
+  };
+  const bool drop = P.p > 0.f;
+  const uint32_t thr = drop_thr(P.p);
+  const float sc = drop ? 1.f / (1.f - P.p) : 1.f;
+  const uint64_t key = hash_u64(P.seed);
+  const int64_t mytok = t0 + 32 * tt + l32;
+  const bool tok_ok = mytok < P.M;
+  // a lane past the last token reads row M-1 (clamped DMA source) and stores exactly what that row's
+  // own lane stores (same mask index): every wave issues the same number of x_d stores, which the
+  // counted vmcnt relies on
+  const int64_t tokc = tok_ok ? mytok : P.M - 1;
+  bf16* xdrow = XD ? static_cast<bf16*>(P.xd) + tokc * (int64_t)P.K + (int64_t)c_lo * LDD_KC : nullptr;
+  const uint64_t eidx0 = P.offset + (uint64_t)tokc * (uint64_t)P.K + (uint64_t)c_lo * LDD_KC;
+
+  f32x16 acc[RB];
+#pragma unroll
+  for (int i = 0; i < RB; ++i) acc[i] = f32x16{};
+  const int pre = min(nch, LDD_NS - 1);
+  for (int c = 0; c < pre; ++c) dma_chunk(c, c);
+  for (int t = 0; t < nch; ++t) {
+    const int slot = t % LDD_NS;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");      // this wave's reads of slot t-1 are done
+    wait_chunk(min(2, nch - 1 - t), min(t, 2));             // chunk t landed (this wave's pieces)
+    __builtin_amdgcn_s_barrier();                            // ... every wave's; slot t-1 free
+    const char* xi = smem + slot * SLOT;
+    const char* ai = xi + XIMG;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int ch = 2 * (2 * ksl + s2) + h;  // 16-byte chunk of this lane's 8 k (k = 16 kstep + 8 h)
+      const int xr = 32 * tt + l32;
+      bf16x8 xf = *reinterpret_cast<const bf16x8*>(xi + xr * 128 + 16 * (ch ^ swz128(xr)));
+      if (drop) drop8(xf, key, eidx0 + (uint64_t)t * LDD_KC + 8 * ch, thr, sc);
+      if (XD) *reinterpret_cast<bf16x8*>(xdrow + t * LDD_KC + 8 * ch) = xf;
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) {
+        const int ar = rb * 32 + l32;
+        const bf16x8 af = *reinterpret_cast<const bf16x8*>(ai + ar * 128 + 16 * (ch ^ swz128(ar)));
+        acc[rb] = mfma32x32x16(af, xf, acc[rb]);
+      }
+    }
+    if (t + LDD_NS - 1 < nch) dma_chunk(t + LDD_NS - 1, (t + LDD_NS - 1) % LDD_NS);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // ring consumed: the space takes the k-slice reduction
+  float* red = reinterpret_cast<float*>(smem);  // [2 token tiles][RB * 16 * 64]
+  if (ksl > 0) {
+    float* dst = red + tt * RB * 1024;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[(rb * 16 + r) * 64 + lane] = acc[rb][r];
+  }
+  __syncthreads();
+  if (ksl > 0) return;
+  const float* src_red = red + tt * RB * 1024;
+#pragma unroll
+  for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[rb][r] += src_red[(rb * 16 + r) * 64 + lane];
+  if (tok_ok && P.ksplit > 1) {
+    float* prow = P.hpart + ((int64_t)ksi * P.M + mytok) * R;
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        *reinterpret_cast<f32x4*>(prow + rb * 32 + 8 * q + 4 * h) =
+            f32x4{acc[rb][4 * q], acc[rb][4 * q + 1], acc[rb][4 * q + 2], acc[rb][4 * q + 3]};
+  } else if (tok_ok) {
+    bf16* hrow = static_cast<bf16*>(P.h) + mytok * (P.ldh > 0 ? P.ldh : (int64_t)R);
     const float hs = P.hscale;
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb)
@@ -405,7 +570,32 @@ int lora_down_tb(int R) {
   return R >= 96 ? 2 : 1;
 }
 
+// the LDS-DMA kernel takes R = 128 / 192 (the fused gate/up and q/k/v adapters of the SFT job:
+// 57 -> 44 us and 67 -> 53 us at 6144 tokens, tools/lora_kernel_bench.py); at R = 64 the
+// register-staged kernel is as fast or faster (o 34 vs 34 us, down 100 vs 116 us), so it keeps
+// R = 64 unless GRT_LORA_DOWN_DMA=2. GRT_LORA_DOWN_DMA=0: the register-staged kernel everywhere.
+static bool lora_down_dma(int R) {
+  static const int env = [] { const char* e = getenv("GRT_LORA_DOWN_DMA"); return e ? atoi(e) : 1; }();
+  return env != 0 && (R == 128 || R == 192 || (env == 2 && R == 64));
+}
+
 int lora_down_splits(int64_t M, int K, int R, int cus) {
+  if (lora_down_dma(R)) {
+    // 64-token workgroups (R = 64: two 64 KiB workgroups per CU). Splits are chosen by whole rounds
+    // of workgroups: a launch of 1.1 rounds runs as long as 2 (the last workgroups stream a whole
+    // split alone), so the cost is rounds x (chunks per split + the fp32 partial a split writes, ~2
+    // chunks' worth of bytes), minimised over ks = 1 .. 16 with at least 4 chunks (the ring) per split.
+    const int64_t ntb = (M + 63) / 64, slots = (int64_t)cus * (R == 64 ? 2 : 1);
+    const int nch = K / LDD_KC;
+    int best = 1;
+    int64_t best_cost = -1;
+    for (int ks = 1; ks <= 16 && nch / ks >= 4; ++ks) {
+      const int64_t rounds = (ntb * ks + slots - 1) / slots;
+      const int64_t cost = rounds * ((nch + ks - 1) / ks + (ks > 1 ? 2 : 0));
+      if (best_cost < 0 || cost < best_cost) { best_cost = cost; best = ks; }
+    }
+    return best;
+  }
   // at least ~3 workgroups per CU at one token tile per workgroup (a single 4-wave workgroup per CU
   // leaves every per-chunk latency exposed); with two tiles per workgroup the A loads are halved
   // and one split per workgroup slot (~1-2 per CU) keeps the fp32 partials small
@@ -419,19 +609,35 @@ int lora_down_splits(int64_t M, int K, int R, int cus) {
 }
 
 void lora_down(const LoraDownParams& p, hipStream_t s) {
+  if (lora_down_dma(p.R)) {
+    const dim3 grid((unsigned)(((p.M + 63) / 64) * p.ksplit)), block(256);
+    const bool xd = p.xd != nullptr;
+#define GRT_LDD(RB)                                                                                  \
+  if (xd) hipLaunchKernelGGL((lora_down_dma_kernel<RB, true>), grid, block, 0, s, p);                \
+  else hipLaunchKernelGGL((lora_down_dma_kernel<RB, false>), grid, block, 0, s, p);
+    if (p.R == 64) { GRT_LDD(2) } else if (p.R == 128) { GRT_LDD(4) } else { GRT_LDD(6) }
+#undef GRT_LDD
+  } else {
   const int tbw = lora_down_tb(p.R);
   const dim3 grid((unsigned)(((p.M + 32 * tbw - 1) / (32 * tbw)) * p.ksplit)), block(256);
   // GRT_LORA_DOWN_KC=64: half the LDS per workgroup (two workgroups per CU up to R = 192); measured
   // neutral on the Llama-2-7B LoRA step (profiles/r2_perf_experiments.md), so 128 by default
   static const int kc_env = [] { const char* e = getenv("GRT_LORA_DOWN_KC"); return e ? atoi(e) : 0; }();
   const bool kc64 = kc_env == 64;
+  // GRT_LORA_DOWN_AD=2: A chunks two ahead in registers (R = 64 / 128 / 192 at 128-column chunks)
+  static const int ad_env = [] { const char* e = getenv("GRT_LORA_DOWN_AD"); return e ? atoi(e) : 1; }();
+  const bool ad2 = ad_env == 2 && !kc64;
 #define GRT_LD(N)                                                                               \
   case N:                                                                                       \
     if (tbw == 1) {                                                                             \
       if (kc64) hipLaunchKernelGGL((lora_down_kernel<N, 64, 1>), grid, block, 0, s, p);         \
+      else if (ad2 && (N == 2 || N == 4 || N == 6))                                             \
+        hipLaunchKernelGGL((lora_down_kernel<N, 128, 1, (N == 2 || N == 4 || N == 6) ? 2 : 1>), grid, block, 0, s, p); \
       else hipLaunchKernelGGL((lora_down_kernel<N, 128, 1>), grid, block, 0, s, p);             \
     } else { /* R > 192: 64-column chunks (the 128-column images exceed the LDS) */            \
       if (kc64) hipLaunchKernelGGL((lora_down_kernel<N, 64, 2>), grid, block, 0, s, p);         \
+      else if (ad2 && (N == 2 || N == 4 || N == 6))                                             \
+        hipLaunchKernelGGL((lora_down_kernel<N, (N >= 7 ? 64 : 128), 2, (N == 2 || N == 4 || N == 6) ? 2 : 1>), grid, block, 0, s, p); \
       else hipLaunchKernelGGL((lora_down_kernel<N, (N >= 7 ? 64 : 128), 2>), grid, block, 0, s, p); \
     }                                                                                           \
     break;
@@ -440,6 +646,7 @@ void lora_down(const LoraDownParams& p, hipStream_t s) {
     default: GRT_LD(8)
   }
 #undef GRT_LD
+  }
   if (p.ksplit > 1) {
     const int64_t n4 = p.M * (int64_t)p.R / 4;
     int64_t g = (n4 + 255) / 256;

@@ -24,6 +24,8 @@
 //             range go to a workspace in the OUTPUT layout (staged through LDS so both layouts store
 //             whole rows); lora_tred_fin sums them, scales, converts and assigns / accumulates.
 // v_mfma_f32_32x32x16_bf16 throughout (cdna_hip_programming.md §3 layouts).
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "grt_common.h"
@@ -63,7 +65,6 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // ---------------------------------------------------------------------------------------------
 // lora_g
 // ---------------------------------------------------------------------------------------------
-constexpr int G_NS = 4;                     // ring slots
 constexpr int G_SLOT = 8192 + 16384;        // A image (32 rows) + B^T image (64 rows)
 
 template <int D>  // D DMA instructions per tile: wait until at most `pending` tiles are in flight
@@ -88,6 +89,8 @@ __device__ __forceinline__ T pick(const T (&v)[kLoraGMax], int t) {
   return t == 0 ? v[0] : t == 1 ? v[1] : t == 2 ? v[2] : v[3];
 }
 
+// G_NS ring slots: 4 (96 KiB, one workgroup per CU) or 3 (72 KiB, two per CU)
+template <int G_NS>
 __global__ __launch_bounds__(256) void lora_g_kernel(const LoraGParams P) {
   __shared__ __attribute__((aligned(16))) char smem[G_NS * G_SLOT];
   const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, l32 = lane & 31;
@@ -348,9 +351,20 @@ __global__ __launch_bounds__(256) void lora_tred_fin_kernel(const LoraTredParams
 
 bool lora_g_supported(int64_t M, int K, int r) { return M > 0 && K > 0 && K % 128 == 0 && r == 64; }
 
-// k splits: only when the 32-row blocks (of all products) leave a quarter of the CUs idle (one 96 KiB
-// workgroup per CU); at most 8
+// ring depth (GRT_LORA_G_NS: 4 -> one 96 KiB workgroup per CU (default), 3 -> two 72 KiB workgroups
+// per CU: 1-2 % slower at the SFT shapes, tools/lora_kernel_bench.py)
+static int lora_g_ns() {
+  static const int ns = [] {
+    const char* e = getenv("GRT_LORA_G_NS");
+    return e && atoi(e) == 3 ? 3 : 4;
+  }();
+  return ns;
+}
+
+// k splits: only when the 32-row blocks (of all products) leave a quarter of the workgroup slots idle;
+// at most 8
 int lora_g_splits(int64_t M, int K, int cus, int nprod) {
+  cus *= lora_g_ns() == 3 ? 2 : 1;  // workgroup slots
   const int64_t nrb = (M + 31) / 32 * nprod;
   if (4 * nrb >= 3 * (int64_t)cus) return 1;  // >= 3/4 of the CUs busy: no partials, no finalize launch
   int ks = (int)((cus + nrb - 1) / nrb);
@@ -361,7 +375,8 @@ int lora_g_splits(int64_t M, int K, int cus, int nprod) {
 
 void lora_g(const LoraGParams& p, hipStream_t s) {
   const dim3 grid((unsigned)(((p.M + 31) / 32) * p.ks), (unsigned)p.nprod), block(256);
-  hipLaunchKernelGGL(lora_g_kernel, grid, block, 0, s, p);
+  if (lora_g_ns() == 3) hipLaunchKernelGGL(lora_g_kernel<3>, grid, block, 0, s, p);
+  else hipLaunchKernelGGL(lora_g_kernel<4>, grid, block, 0, s, p);
   if (p.ks > 1) {
     int64_t fb = (p.M * 16 + 255) / 256;
     if (fb > 1024) fb = 1024;
@@ -377,7 +392,13 @@ bool lora_tred_supported(int64_t M, int N, int R) {
 // at N = 4096, R = 64 made the partials a quarter of the operand's bytes), at most 16, each split a
 // whole number of 32-token tiles
 int lora_tred_splits(int64_t M, int N, int R, int cus) {
-  (void)R;
+  // workgroups per CU the splits aim at (GRT_LORA_TRED_WPC, default 1; R = 64 fits two 64 KiB
+  // workgroups per CU, 5-9 % slower at the SFT shapes: tools/lora_kernel_bench.py)
+  static const int wpc = [] {
+    const char* e = getenv("GRT_LORA_TRED_WPC");
+    return e && atoi(e) > 1 ? 2 : 1;
+  }();
+  if (R == 64) cus *= wpc;
   const int nblk = N / 128;
   int ks = (int)(((int64_t)cus + nblk - 1) / nblk);
   const int64_t tiles = M / 32;

@@ -685,7 +685,8 @@ def test_lora_fp32_adapters_take_the_gemm_path():
 
 @pytest.mark.parametrize("M,K,R,p,offset,strided", [
     (256, 256, 32, 0.0, 0, False), (200, 512, 64, 0.1, 0, False), (77, 1024, 192, 0.1, 8, True),
-    (1024, 4096, 128, 0.1, 0, False), (33, 128, 256, 0.5, 4, False)])
+    (1024, 4096, 128, 0.1, 0, False), (33, 128, 256, 0.5, 4, False), (6144, 14336, 64, 0.1, 0, True),
+    (300, 4096, 192, 0.0, 0, True), (130, 256, 64, 0.1, 4, False)])
 def test_lora_down_kernel(M, K, R, p, offset, strided):
     """lora.hip lora_down: h = drop(x) A^T (mask = the host hash, ops/_ref.py) and the x_d side output."""
     from gke_ray_train_amd.ops import _ref
