@@ -23,6 +23,7 @@ The plan mirrors what the engines actually allocate:
 """
 from __future__ import annotations
 
+import math
 import os
 from dataclasses import asdict, dataclass, field
 from typing import Dict, List, Optional
@@ -174,17 +175,29 @@ def plan_memory(cfg, world: int, parallel: str = "ddp", offload: bool = False, p
         kcat = (r % 64 == 0 and h % 128 == 0 and f % 128 == 0 and os.environ.get("GRT_LORA_KCAT", "1") != "0") \
             if lora_kcat is None else lora_kcat
         tails = L * sum(o * R for o, R in mods)
+        cached = True
         if peft == "qlora":  # NF4 codes (0.5 B) + fp32 absmax per 64
             hbm["frozen_nf4_codes"] = lin * (0.5 + 4.0 / 64)
+            # peft/quant.py set_dequant_cache: the resident bf16 W / W^T exist only when the cache is
+            # on ("auto": 4 B per base parameter within 15 % of the device's HBM — 8B yes, 70B no).
+            # Without it the K-concatenated path is off too and each projection is dequantised per use
+            mode = os.environ.get("GRT_NF4_CACHE", "auto")
+            cap = plan.hbm_capacity if math.isfinite(plan.hbm_capacity) else float(MI355X_HBM_BYTES)
+            cached = (4.0 * lin <= 0.15 * cap) if mode == "auto" else mode not in ("0", "off", "false")
+            kcat = kcat and cached
         hbm["frozen_unadapted"] = (P - lin) * B  # embeddings, LM head, norms
-        if kcat:
+        if not cached:
+            # transient per-use dequantisation: the largest projection's W (forward) and W^T (backward)
+            hbm["nf4_dequant_scratch"] = 2 * h * max(2 * f, h + 2 * kvd) * B
+        elif kcat:
             # K-concatenated W' = [W | B blocks] (bf16; for LoRA the base weight is a view of it, for
             # QLoRA it replaces the dequant cache) + the B^T buffer of the adapter-gradient kernel
             hbm["frozen_kcat_weight"] = (lin + tails) * B
             hbm["lora_bt"] = tails * B if r == 64 else 0.0
         else:
             hbm["frozen_base"] = lin * B  # bf16 weight, or the resident NF4 dequant cache
-        hbm["frozen_base_transposed"] = lin * B  # cached W^T of the TN dX GEMMs (both peft kinds)
+        if cached:
+            hbm["frozen_base_transposed"] = lin * B  # cached W^T of the TN dX GEMMs (both peft kinds)
         hbm["adapters"] = t * B
         hbm["adapter_grads"] = t * B
         hbm["adam_moments_fp32"] = 8.0 * t

@@ -64,6 +64,24 @@ def test_7b_headline_config_fits_and_zero_shrinks_optimizer():
     assert nokcat.hbm_per_rank["frozen_base"] > 11 * GiB and "frozen_kcat_weight" not in nokcat.hbm_per_rank
 
 
+def test_qlora_70b_plan_follows_the_nf4_dequant_cache_rule(monkeypatch):
+    """peft/quant.py set_dequant_cache "auto": the resident bf16 W / W^T (and with them the K-concat
+    W') exist only when 4 B per base parameter fits in 15 % of HBM — on for 8B, off for 70B, where
+    the plan holds the NF4 codes plus one projection's per-use dequantisation instead."""
+    monkeypatch.delenv("GRT_NF4_CACHE", raising=False)
+    big = plan_memory(get_config("llama3-70b"), 1, "ddp", peft="qlora", micro_batch=2, seq=1024, hbm_capacity=HBM)
+    hb = big.hbm_per_rank
+    for k in ("frozen_kcat_weight", "frozen_base_transposed", "frozen_base", "lora_bt"):
+        assert k not in hb
+    assert hb["frozen_nf4_codes"] < 40 * GiB and hb["nf4_dequant_scratch"] < 2 * GiB
+    assert big.fits and big.hbm_total < 120 * GiB
+    small = plan_memory(get_config("llama3.1-8b"), 1, "ddp", peft="qlora", micro_batch=2, seq=1024, hbm_capacity=HBM)
+    assert "frozen_kcat_weight" in small.hbm_per_rank and "nf4_dequant_scratch" not in small.hbm_per_rank
+    monkeypatch.setenv("GRT_NF4_CACHE", "0")  # forced off for 8B too
+    off = plan_memory(get_config("llama3.1-8b"), 1, "ddp", peft="qlora", micro_batch=2, seq=1024, hbm_capacity=HBM)
+    assert "frozen_kcat_weight" not in off.hbm_per_rank and off.hbm_total < small.hbm_total - 20 * GiB
+
+
 def test_bench_plan_only_cli():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--plan-only", "--model", "llama2-7b",
                         "--device", "cpu"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
