@@ -140,6 +140,40 @@ def input_grad(dy2: torch.Tensor, w: torch.Tensor, wt_ev=None) -> torch.Tensor:
 _NATIVE_EMBEDDING = os.environ.get("GRT_NATIVE_EMBEDDING", "0") == "1"
 
 
+# Where the two transposes of the TN weight gradient run (opt-in placements). GRT_WGRAD_XT_FWD=1:
+# the inputs X of a projection are transposed in the FORWARD, right after the kernel that produced
+# them (norm, SwiGLU, attention) while they may still sit in the 256 MB Infinity Cache, and X^T is
+# saved for the backward instead of X; GRT_WGRAD_DYT_FIRST=1: dY^T at the top of the backward,
+# right after its producer. Measured on the headline step (3 interleaved rounds, scripts/gpu_r4_xt.sh,
+# profiles/r4_batch1.md): 298.4-298.7 / 298.3-298.9 ms vs 298.7-298.9 ms with the transposes inside
+# ``wgrad`` — no cache benefit, +2 GiB peak (the attention output is saved twice), so both stay off.
+_WGRAD_XT_FWD = os.environ.get("GRT_WGRAD_XT_FWD", "0") == "1"
+_WGRAD_DYT_FIRST = os.environ.get("GRT_WGRAD_DYT_FIRST", "0") == "1"
+
+
+def _tn_wgrad_ok(t2: torch.Tensor) -> bool:
+    """``t2`` ([M, C] token-major) can be an operand of the transposed (TN) weight-gradient path."""
+    return (_WGRAD_NATIVE and _WGRAD_TN and t2.is_cuda and t2.dtype == torch.bfloat16 and t2.dim() == 2
+            and t2.shape[0] % 64 == 0 and t2.shape[1] % 64 == 0 and t2.is_contiguous())
+
+
+def transposed(t2: torch.Tensor) -> torch.Tensor:
+    """[M, C] -> contiguous [C, M] through the HIP transpose kernel (HBM / cache-bound)."""
+    from .. import _native
+    tt = torch.empty(t2.shape[1], t2.shape[0], device=t2.device, dtype=t2.dtype)
+    _native.kernels().transpose_into(t2, tt)
+    return tt
+
+
+def wgrad_tn(dyt: torch.Tensor, xt: torch.Tensor, out: torch.Tensor, accumulate: bool) -> torch.Tensor:
+    """dW = dY^T X from the already transposed operands ([N, M], [K, M]): the TN library GEMM."""
+    if accumulate:
+        out.addmm_(dyt, xt.t())
+    else:
+        torch.mm(dyt, xt.t(), out=out)
+    return out
+
+
 def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor = None, accumulate: bool = False) -> torch.Tensor:
     """dW = dy2^T @ x2 ([M,N]^T [M,K] -> [N,K]), written into / accumulated onto ``out``.
 
@@ -184,7 +218,9 @@ def wgrad(dy2: torch.Tensor, x2: torch.Tensor, out: torch.Tensor = None, accumul
 class _DirectGradLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
-        ctx.save_for_backward(x, w)
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.x_t = _WGRAD_XT_FWD and ctx.needs_input_grad[1] and w.shape[0] % 64 == 0 and _tn_wgrad_ok(x2)
+        ctx.save_for_backward(transposed(x2) if ctx.x_t else x, w)
         ctx.has_b = b is not None
         ctx.wt_ev = transpose_for_backward(w) if ctx.needs_input_grad[0] else None
         return F.linear(x, w, b)
@@ -192,20 +228,33 @@ class _DirectGradLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dyt = None
+        if ctx.x_t:  # X^T saved by the forward: dY^T now, while dY is fresh from its producer
+            if not dy2.is_contiguous():
+                dy2 = dy2.contiguous()
+            dyt = transposed(dy2) if _WGRAD_DYT_FIRST else None
         dx = None
         if ctx.needs_input_grad[0]:
             dx = input_grad(dy, w, ctx.wt_ev)
             ctx.wt_ev = None
-        x2 = x.reshape(-1, x.shape[-1])
-        dy2 = dy.reshape(-1, dy.shape[-1])
         dw = db = None
+        if ctx.x_t:
+            xt = x
+            if dyt is None:
+                dyt = transposed(dy2)
+            fn = lambda v, acc: wgrad_tn(dyt, xt, v, acc)  # noqa: E731
+        else:
+            x2 = x.reshape(-1, x.shape[-1])
+            fn = lambda v, acc: wgrad(dy2, x2, v, acc)  # noqa: E731
         if ctx.needs_input_grad[1]:
             slot = getattr(w, "_grt_slot", None)
             if slot is not None:
-                slot.write(lambda v: wgrad(dy2, x2, v, False), lambda v: wgrad(dy2, x2, v, True))
+                slot.write(lambda v: fn(v, False), lambda v: fn(v, True))
                 slot.notify(w)
             else:
-                dw = wgrad(dy2, x2)
+                dw = torch.empty_like(w)
+                fn(dw, False)
         if ctx.has_b:
             b_needs = ctx.needs_input_grad[2]
             if b_needs:

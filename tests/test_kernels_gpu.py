@@ -553,6 +553,36 @@ def test_wgrad_helper_fallback_and_native():
     assert (wgrad(dy, x).float() - ref).abs().max().item() < 0.05 * ref.abs().max().item()
 
 
+def test_direct_grad_linear_transpose_placements_agree(monkeypatch):
+    """X^T taken in the forward (saved instead of X) and dY^T at the top of the backward give the
+    same dX / dW bits as the transposes inside wgrad, into a gradient slot over two accumulating
+    micro-steps, and match the fp32 math."""
+    from gke_ray_train_amd.ops import linear as L
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = torch.randn(2, 192, 512, device=DEV, generator=g).bfloat16()
+    w = (torch.randn(384, 512, device=DEV, generator=g) * 0.05).bfloat16()
+    dys = [torch.randn(2, 192, 384, device=DEV, generator=g).bfloat16() for _ in range(2)]
+    res = {}
+    for xt_fwd, dyt_first in ((False, False), (True, False), (True, True)):
+        monkeypatch.setattr(L, "_WGRAD_XT_FWD", xt_fwd)
+        monkeypatch.setattr(L, "_WGRAD_DYT_FIRST", dyt_first)
+        wp = torch.nn.Parameter(w.clone())
+        wp._grt_slot = L.GradSlot(torch.empty_like(w), lambda p: None)
+        dxs = []
+        for dy in dys:
+            xi = x.clone().requires_grad_()
+            y = L.linear(xi, wp)
+            y.backward(dy)
+            dxs.append(xi.grad)
+        res[(xt_fwd, dyt_first)] = (dxs, wp._grt_slot.view.clone())
+    base = res[(False, False)]
+    for k, (dxs, dw) in res.items():
+        assert all(torch.equal(a, b) for a, b in zip(dxs, base[0])), k
+        assert torch.equal(dw, base[1]), k
+    ref = sum(dy.reshape(-1, 384).float().t() @ x.reshape(-1, 512).float() for dy in dys)
+    assert (base[1].float() - ref).abs().max().item() < 0.02 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_embedding_fwd_bwd(dtype):
     """Gather forward and the one-pass segmented backward (zero-fill of unhit rows, duplicates,
