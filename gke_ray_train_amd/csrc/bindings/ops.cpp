@@ -836,6 +836,22 @@ Tensor nf4_dequantize(const Tensor& q, const Tensor& absmax, int64_t n, int64_t 
   return w;
 }
 
+// dequantise into out ([rows, cols] bf16 view, unit column stride, any row stride: the W head of a
+// K-concatenated [W | B] buffer); false when the shape is not handled
+bool nf4_dequantize_into(const Tensor& q, const Tensor& absmax, Tensor out, int64_t blocksize) {
+  check_contig(q, "q");
+  check_contig(absmax, "absmax");
+  TORCH_CHECK(out.dim() == 2 && out.scalar_type() == at::kBFloat16 && out.stride(1) == 1 && out.is_cuda(),
+              "nf4_dequantize_into: out must be a 2-D bf16 view with unit column stride");
+  const int64_t rows = out.size(0), cols = out.size(1);
+  TORCH_CHECK(q.numel() * 2 == rows * cols && absmax.numel() * blocksize == rows * cols, "nf4 shapes");
+  TORCH_CHECK(rows <= INT32_MAX && cols <= INT32_MAX, "nf4_dequantize_into: dims");
+  if (out.stride(0) % 8 != 0 || reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 != 0) return false;  // 16-byte stores
+  c10::OptionalDeviceGuard g(q.device());
+  return grt::nf4_dequantize_2d(q.data_ptr<uint8_t>(), absmax.data_ptr<float>(), out.data_ptr(), (int)rows,
+                                (int)cols, out.stride(0), (int)blocksize, cur_stream(q));
+}
+
 Tensor nf4_dequantize_t(const Tensor& q, const Tensor& absmax, int64_t rows, int64_t cols, int64_t blocksize) {
   check_contig(q, "q");
   check_contig(absmax, "absmax");
@@ -1174,6 +1190,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);
+  m.def("nf4_dequantize_into", &nf4_dequantize_into);
   m.def("transpose_into", &transpose_into);
   m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("attn_decode", &attn_decode);

@@ -226,6 +226,10 @@ void nf4_quantize(DType dt, const void* w, uint8_t* q, float* absmax, int64_t n,
 void nf4_dequantize(DType dt, const uint8_t* q, const float* absmax, void* w, int64_t n,
                     int blocksize, hipStream_t s);
 // W^T [cols][rows] (bf16) from the NF4 codes of W [rows][cols]; cols % 64 == 0, blocksize 64
+// bf16 W [rows][cols] into a row-strided destination (row stride ldo elements); false = shape not
+// handled (blocksize != 64, cols % 16 != 0)
+bool nf4_dequantize_2d(const uint8_t* q, const float* absmax, void* w, int rows, int cols, int64_t ldo,
+                       int blocksize, hipStream_t s);
 void nf4_dequantize_t(const uint8_t* q, const float* absmax, void* wt, int rows, int cols, int blocksize,
                       hipStream_t s);
 

@@ -180,15 +180,18 @@ def plan_memory(cfg, world: int, parallel: str = "ddp", offload: bool = False, p
             hbm["frozen_nf4_codes"] = lin * (0.5 + 4.0 / 64)
             # peft/quant.py set_dequant_cache: the resident bf16 W / W^T exist only when the cache is
             # on ("auto": 4 B per base parameter within 15 % of the device's HBM — 8B yes, 70B no).
-            # Without it the K-concatenated path is off too and each projection is dequantised per use
+            # Without it each projection is dequantised per use: into a transient K-concatenated W'
+            # (peft/lora.py _kcat_weight_streamed) in the forward, as W^T in the backward
             mode = os.environ.get("GRT_NF4_CACHE", "auto")
             cap = plan.hbm_capacity if math.isfinite(plan.hbm_capacity) else float(MI355X_HBM_BYTES)
             cached = (4.0 * lin <= 0.15 * cap) if mode == "auto" else mode not in ("0", "off", "false")
-            kcat = kcat and cached
+            kcat = kcat and (cached or os.environ.get("GRT_NF4_STREAM_KCAT", "1") != "0")
         hbm["frozen_unadapted"] = (P - lin) * B  # embeddings, LM head, norms
         if not cached:
-            # transient per-use dequantisation: the largest projection's W (forward) and W^T (backward)
+            # transient per-use dequantisation: the largest projection's W' (forward) and W^T (backward)
             hbm["nf4_dequant_scratch"] = 2 * h * max(2 * f, h + 2 * kvd) * B
+            if kcat and r == 64:
+                hbm["lora_bt"] = tails * B
         elif kcat:
             # K-concatenated W' = [W | B blocks] (bf16; for LoRA the base weight is a view of it, for
             # QLoRA it replaces the dequant cache) + the B^T buffer of the adapter-gradient kernel

@@ -118,6 +118,11 @@ def _adapter_then_base_dx(ctx, C, base, dy2, g, acat):
 # folded into the GEMMs' alpha. GRT_LORA_DIRECT_GRAD=0 -> autograd accumulation.
 _LORA_DIRECT_GRAD = os.environ.get("GRT_LORA_DIRECT_GRAD", "1") != "0"
 _LORA_KCAT = os.environ.get("GRT_LORA_KCAT", "1") != "0"
+# NF4 base WITHOUT the resident dequant cache (QLoRA's 4-bit memory: 70B on one GPU, or
+# GRT_NF4_CACHE=0): the K-concatenated forward still applies, on a transient W' that each forward
+# dequantises straight into its head (nf4_dequantize_into) — one bf16 write per base weight and
+# use, no resident bf16 copy. GRT_NF4_STREAM_KCAT=0: the unconcatenated per-use path.
+_NF4_STREAM_KCAT = os.environ.get("GRT_NF4_STREAM_KCAT", "1") != "0"
 # The adapter-gradient GEMMs g_i = s dY_i B_i, dB_i = dY_i^T h'_i and dA = g^T x_d on the
 # framework's one-pass kernels (csrc/kernels/lora_grad.hip: each reads its [tokens, features]
 # operand once) instead of hipBLASLt's skinny tiles (2-4 reads per product). GRT_LORA_GRAD_KERNELS=0:
@@ -447,7 +452,8 @@ class LoraLinear(nn.Module):
                 and all(n % 64 == 0 and off % 8 == 0 for _, off, n in self.targets)):
             return 0
         if isinstance(b, NF4Linear):
-            ok = getattr(b, "_cache_on", False) and b.qweight.is_cuda and b.compute_dtype == torch.bfloat16
+            ok = (getattr(b, "_cache_on", False) or _NF4_STREAM_KCAT) and b.qweight.is_cuda \
+                and b.compute_dtype == torch.bfloat16 and b.blocksize == 64
         else:
             w = getattr(b, "weight", None)
             ok = w is not None and w.is_cuda and w.dtype == torch.bfloat16 and not w.requires_grad \
@@ -461,6 +467,8 @@ class LoraLinear(nn.Module):
         column order ``order`` refreshed (every forward: B changes with each optimizer step)."""
         K, r = self.in_features, self.r
         R = r * len(self.targets)
+        if isinstance(self.base, NF4Linear) and not getattr(self.base, "_cache_on", False):
+            return self._kcat_weight_streamed(order, Bs)
         if self._wk is None:
             w = self.base.dequantize() if isinstance(self.base, NF4Linear) else self.base.weight.detach()
             wk = torch.zeros(self.out_features, K + R, device=w.device, dtype=w.dtype)
@@ -502,6 +510,33 @@ class LoraLinear(nn.Module):
         return self._wk
 
     @torch.no_grad()
+    def _kcat_weight_streamed(self, order, Bs):
+        """W' for an NF4 base without the dequant cache: a fresh [out, in + R] buffer per forward, W
+        dequantised into its head, the B blocks (and the B^T buffer of the adapter-gradient kernel)
+        into the tail. Nothing bf16 of the base outlives the forward's GEMM."""
+        K, r = self.in_features, self.r
+        R = r * len(self.targets)
+        q = self.base.qweight
+        wk = torch.empty(self.out_features, K + R, device=q.device, dtype=torch.bfloat16)
+        self.base.dequantize_into(wk[:, :K])
+        wk[:, K:].zero_()
+        bl = [Bs[i].detach() for i in order]
+        offs = [self._spec[i][0] for i in order]
+        if all(b.is_contiguous() for b in bl):
+            if _LORA_GRAD_KERNELS and r == 64:
+                if self._bt is None or self._wk_order != list(order):
+                    self._bt = torch.zeros(R, self.out_features, device=q.device, dtype=torch.bfloat16)
+                    self._wk_order = list(order)
+                _native.kernels().lora_refresh(bl, offs, wk, self._bt, K, 0)
+            else:
+                _native.kernels().lora_refresh(bl, offs, wk, None, K)
+        else:
+            self._bt = None
+            for j, (b, off) in enumerate(zip(bl, offs)):
+                wk[off:off + b.shape[0], K + j * r:K + (j + 1) * r].copy_(b)
+        return wk
+
+    @torch.no_grad()
     def prepare_frozen_weights(self):
         """Materialise the frozen base's derived layouts now, while the model is prepared, instead of
         inside the first training step: the K-concatenated W' (or, without it, the NF4 dequant cache
@@ -512,10 +547,11 @@ class LoraLinear(nn.Module):
         if w is None or not w.is_cuda:
             return
         names = [t[0] for t in self.targets]
-        if self.kcat_pad:
+        streamed = isinstance(b, NF4Linear) and not getattr(b, "_cache_on", False)
+        if self.kcat_pad and not streamed:
             pk = _packed([self.lora_A[n] for n in names])
             self._kcat_weight(list(range(len(names))) if pk is None else pk[0], [self.lora_B[n] for n in names])
-        elif isinstance(b, NF4Linear):
+        elif isinstance(b, NF4Linear) and not streamed:
             b.dequantize()
         if isinstance(b, NF4Linear):
             b.prepare_input_grad()

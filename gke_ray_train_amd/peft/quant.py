@@ -112,6 +112,15 @@ class NF4Linear(nn.Module):
                                                       self.in_features, self.blocksize)
         return None
 
+    def dequantize_into(self, out: torch.Tensor) -> torch.Tensor:
+        """bf16 W written into ``out`` ([out_features, in_features] view with unit column stride, any
+        row stride: the W head of the K-concatenated [W | B] buffer of peft/lora.py), returned."""
+        if out.is_cuda and self.compute_dtype == torch.bfloat16 and out.dtype == torch.bfloat16:
+            from .. import _native
+            if _native.kernels().nf4_dequantize_into(self.qweight, self._absmax().contiguous(), out, self.blocksize):
+                return out
+        return out.copy_(self._dequant())
+
     def _cache_key(self):
         return (self.qweight.data_ptr(), self.qweight._version)
 

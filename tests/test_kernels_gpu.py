@@ -770,6 +770,25 @@ def test_transpose_and_nf4_dequant_t():
     assert torch.equal(C.nf4_dequantize_t(q, absmax, 384, 640, 64), deq.t())
 
 
+@pytest.mark.parametrize("rows,cols", [(384, 640), (4096, 1024), (200, 256), (64, 4224)])
+def test_nf4_dequant_v2_exact(rows, cols):
+    """v2 dequantisation (byte-indexed LDS table): flat, into a row-strided [W | tail] buffer, and
+    transposed, all bit-equal to the fp32 math (level x absmax, one rounding to bf16)."""
+    from gke_ray_train_amd import ops
+    from gke_ray_train_amd.ops import _ref
+    C = _C()
+    g = torch.Generator(device=DEV).manual_seed(rows + cols)
+    w = torch.randn(rows, cols, device=DEV, generator=g).bfloat16()
+    q, absmax = ops.nf4_quantize(w.reshape(-1), 64)
+    ref = _ref.nf4_dequantize(q.cpu(), absmax.cpu(), w.numel(), 64, torch.bfloat16).view(rows, cols)
+    flat = ops.nf4_dequantize(q, absmax, w.numel(), 64, torch.bfloat16).view(rows, cols)
+    assert torch.equal(flat.cpu(), ref)
+    buf = torch.full((rows, cols + 192), float("nan"), device=DEV, dtype=torch.bfloat16)
+    assert C.nf4_dequantize_into(q, absmax, buf[:, :cols], 64)
+    assert torch.equal(buf[:, :cols].cpu(), ref) and bool(torch.isnan(buf[:, cols:]).all())
+    assert torch.equal(C.nf4_dequantize_t(q, absmax, rows, cols, 64).cpu(), ref.t())
+
+
 def test_transposed_dgrad_linear_matches_nn():
     """Trainable DDP weight: forward writes W^T on a side stream, backward runs the TN GEMM;
     gradients equal the NN path (GRT_TRANSPOSED_DGRAD=0) to bf16 rounding."""
@@ -882,13 +901,16 @@ def test_decode_attention(B, Sk, hq, hkv, pad):
     _close(o, ref, 1e-2, 1e-2, "decode attention")
 
 
-@pytest.mark.parametrize("nf4", [False, True])
+@pytest.mark.parametrize("nf4", [False, True, "stream"])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("engine", ["none", "ddp"])
 def test_kcat_lora_matches_reference(nf4, p, engine):
     """K-concatenated LoRA (peft/lora.py _LoraKcatFn): the input is the head of a [M, in + R] row
     buffer, h' lands in its tail, y = [x | h'] W'^T and [dX | g] = dY W' are single GEMMs. Same
-    y / dX / dA / dB as the fp32 formula (masks regenerated from the seed the op drew)."""
+    y / dX / dA / dB as the fp32 formula (masks regenerated from the seed the op drew).
+    nf4="stream": NF4 base without the dequant cache, W' rebuilt per forward (_kcat_weight_streamed)."""
+    stream = nf4 == "stream"
+    nf4 = bool(nf4)
     from gke_ray_train_amd.ops import _ref
     from gke_ray_train_amd.ops.linear import Linear
     from gke_ray_train_amd.peft.lora import LoraConfig, LoraLinear
@@ -898,7 +920,7 @@ def test_kcat_lora_matches_reference(nf4, p, engine):
     lin.slices = [("q_proj", 256), ("k_proj", 256), ("v_proj", 256)]
     base = NF4Linear.from_linear(lin, BitsAndBytesConfig()) if nf4 else lin
     if nf4:
-        base.set_dequant_cache(True)
+        base.set_dequant_cache(not stream)
     for q in base.parameters():
         q.requires_grad_(False)
     cfg = LoraConfig(r=64, lora_alpha=32, lora_dropout=p)
@@ -943,6 +965,8 @@ def test_kcat_lora_matches_reference(nf4, p, engine):
     (yr * dy.float()).sum().backward()
     _close(y, yr, 3e-2, 3e-2, "kcat y")
     _close(x.grad, x2.grad, 3e-2, 3e-2, "kcat dx")
+    if stream:
+        assert mod._wk is None and getattr(base, "_w_cache", None) is None  # nothing bf16 stays resident
     for n in names:
         for got, ref, what in ((mod.lora_A[n].grad, A[n].grad, "dA"), (mod.lora_B[n].grad, B[n].grad, "dB")):
             rel = (got.float() - ref).norm() / ref.norm().clamp_min(1e-6)

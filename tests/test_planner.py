@@ -65,14 +65,15 @@ def test_7b_headline_config_fits_and_zero_shrinks_optimizer():
 
 
 def test_qlora_70b_plan_follows_the_nf4_dequant_cache_rule(monkeypatch):
-    """peft/quant.py set_dequant_cache "auto": the resident bf16 W / W^T (and with them the K-concat
+    """peft/quant.py set_dequant_cache "auto": the resident bf16 W / W^T (and the resident K-concat
     W') exist only when 4 B per base parameter fits in 15 % of HBM — on for 8B, off for 70B, where
-    the plan holds the NF4 codes plus one projection's per-use dequantisation instead."""
+    the plan holds the NF4 codes plus one projection's per-use dequantisation (a transient W') instead."""
     monkeypatch.delenv("GRT_NF4_CACHE", raising=False)
     big = plan_memory(get_config("llama3-70b"), 1, "ddp", peft="qlora", micro_batch=2, seq=1024, hbm_capacity=HBM)
     hb = big.hbm_per_rank
-    for k in ("frozen_kcat_weight", "frozen_base_transposed", "frozen_base", "lora_bt"):
+    for k in ("frozen_kcat_weight", "frozen_base_transposed", "frozen_base"):
         assert k not in hb
+    assert hb["lora_bt"] < 2 * GiB  # the streamed W' path keeps only the adapters' B^T resident
     assert hb["frozen_nf4_codes"] < 40 * GiB and hb["nf4_dequant_scratch"] < 2 * GiB
     assert big.fits and big.hbm_total < 120 * GiB
     small = plan_memory(get_config("llama3.1-8b"), 1, "ddp", peft="qlora", micro_batch=2, seq=1024, hbm_capacity=HBM)
