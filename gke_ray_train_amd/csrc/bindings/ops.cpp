@@ -95,6 +95,25 @@ std::vector<Tensor> rmsnorm_bwd(const Tensor& dy, const Tensor& h, const Tensor&
   return {dx, dw};
 }
 
+// dX only (frozen norm weight: LoRA / QLoRA): no weight-gradient slab, no column-sum launch
+Tensor rmsnorm_bwd_dx(const Tensor& dy, const Tensor& h, const Tensor& w, const Tensor& rstd,
+                      const optional<Tensor>& dres) {
+  check_contig(dy, "dy");
+  check_contig(h, "h");
+  c10::OptionalDeviceGuard g(dy.device());
+  const int64_t d = h.size(-1), rows = h.numel() / d;
+  TORCH_CHECK(dy.sizes() == h.sizes() && dy.scalar_type() == h.scalar_type(), "dy/h mismatch");
+  TORCH_CHECK(w.numel() == d && w.scalar_type() == h.scalar_type() && rstd.numel() == rows, "w / rstd shapes");
+  if (dres.has_value()) {
+    check_contig(*dres, "dres");
+    TORCH_CHECK(dres->sizes() == h.sizes() && dres->scalar_type() == h.scalar_type(), "dres mismatch");
+  }
+  auto dx = at::empty_like(h);
+  grt::rmsnorm_bwd(dtype_of(h), dy.data_ptr(), h.data_ptr(), w.data_ptr(), rstd.data_ptr<float>(),
+                   ptr_or_null(dres), dx.data_ptr(), nullptr, nullptr, rows, (int)d, cur_stream(h), nullptr, 0);
+  return dx;
+}
+
 std::vector<Tensor> layernorm_fwd(const Tensor& x, const optional<Tensor>& residual, const Tensor& w,
                                   const optional<Tensor>& b, double eps) {
   check_contig(x, "x");
@@ -1191,6 +1210,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);
   m.def("nf4_dequantize_into", &nf4_dequantize_into);
+  m.def("rmsnorm_bwd_dx", &rmsnorm_bwd_dx);
   m.def("transpose_into", &transpose_into);
   m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("attn_decode", &attn_decode);

@@ -193,6 +193,7 @@ __global__ __launch_bounds__(kNT) void norm_bwd_kernel(const T* __restrict__ dy,
       }
     }
   }
+  if (ws == nullptr) return;  // frozen weight (LoRA / QLoRA): no dw / db slab, no column sums
   float* wsb = ws + (int64_t)blockIdx.x * 2 * d;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
@@ -304,6 +305,7 @@ void launch_bwd(const void* dy, const void* h, const void* w, const float* mean,
   else GRT_NB(8);
 #undef GRT_NB
 #undef GRT_NB2
+  if (ws == nullptr) return;
   const int ncols = RMS ? d : 2 * d;
   const dim3 cg((ncols + 63) / 64);
   if (dw_t != nullptr && RMS) {  // weight gradient in T, straight into its gradient slot

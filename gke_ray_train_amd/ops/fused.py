@@ -41,6 +41,8 @@ class _RMSNorm(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, rstd = ctx.saved_tensors
+        if not ctx.needs_input_grad[1]:  # frozen weight (LoRA / QLoRA): dX only
+            return _native.kernels().rmsnorm_bwd_dx(dy.contiguous(), x, w, rstd, None), None, None, None
         dx, dw = _norm_bwd_into_slot(w, lambda out, acc: _native.kernels().rmsnorm_bwd(
             dy.contiguous(), x, w, rstd, None, out, acc))
         return dx, dw, None, None
@@ -78,6 +80,9 @@ class _AddRMSNorm(torch.autograd.Function):
         h, w, rstd = ctx.saved_tensors
         dy = torch.zeros_like(h) if dy is None else dy.contiguous()
         dres = None if dh is None else dh.contiguous()
+        if not ctx.needs_input_grad[2]:  # frozen weight (LoRA / QLoRA): dX only
+            dx = _native.kernels().rmsnorm_bwd_dx(dy, h, w, rstd, dres)
+            return dx, dx, None, None, None
         dx, dw = _norm_bwd_into_slot(w, lambda out, acc: _native.kernels().rmsnorm_bwd(dy, h, w, rstd, dres, out, acc))
         return dx, dx, dw, None, None
 

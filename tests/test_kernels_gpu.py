@@ -56,6 +56,31 @@ def test_rmsnorm(dtype, d):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("fused_add", [False, True])
+def test_rmsnorm_frozen_weight_dx_only(dtype, fused_add):
+    """Frozen norm weight (LoRA / QLoRA): the dX-only backward gives the same dX bits as the full
+    backward and no weight gradient."""
+    from gke_ray_train_amd import ops
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(300, 4096, device=DEV, dtype=dtype, generator=g)
+    r = torch.randn(300, 4096, device=DEV, dtype=dtype, generator=g)
+    dy = torch.randn(300, 4096, device=DEV, dtype=dtype, generator=g)
+    grads = {}
+    for trainable in (True, False):
+        w = (1 + 0.1 * torch.randn(4096, device=DEV, dtype=dtype, generator=torch.Generator(device=DEV).manual_seed(4)))
+        w.requires_grad_(trainable)
+        xi = x.clone().requires_grad_()
+        if fused_add:
+            y, h = ops.add_rms_norm(xi, r, w, 1e-5)
+            (y.float() * dy.float()).sum().add(h.float().sum()).backward()
+        else:
+            (ops.rms_norm(xi, w, 1e-5).float() * dy.float()).sum().backward()
+        grads[trainable] = (xi.grad, w.grad)
+    assert torch.equal(grads[True][0], grads[False][0])
+    assert grads[False][1] is None and grads[True][1] is not None
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_layernorm(dtype):
     from gke_ray_train_amd import ops
     torch.manual_seed(1)
