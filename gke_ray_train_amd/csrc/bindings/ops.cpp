@@ -1206,6 +1206,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_get_schedule", &grt::attn_get_schedule);
   m.def("attn_set_dkdv_form", &grt::attn_set_dkdv_form, "dK / dV kernel: 1 = 4-wave, 2 = wave-pair (default)");
   m.def("attn_get_dkdv_form", &grt::attn_get_dkdv_form);
+  m.def("attn_set_dma_fast", &grt::attn_set_dma_fast, "1 = hoisted LDS-DMA addressing (default), 0 = clamped per tile");
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);

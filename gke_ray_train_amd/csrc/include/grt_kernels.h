@@ -185,11 +185,16 @@ struct AttnParams {
   // workgroup schedule of one bf16 kernel, set by the launchers from the attn_set_schedule() mask
   // (1 = forward, 2 = dQ, 4 = dK / dV): 0 = one block per workgroup, heaviest first; 1 = causal pairs
   int sched;
+  // set by the launchers (attn_set_dma_fast, GRT_ATTN_DMA_FAST, default 1): tiles that lie inside the
+  // sequence take their LDS-DMA source addresses as a uniform tile base + per-lane offsets fixed for
+  // the sweep (one 64-bit add per DMA) instead of the clamped per-lane row arithmetic
+  int dma_fast;
 };
 void attn_set_schedule(int s);
 int attn_get_schedule();
 void attn_set_dkdv_form(int f);  // 1 = 4-wave dK / dV kernel, 2 = wave-pair kernel (default)
 int attn_get_dkdv_form();
+void attn_set_dma_fast(int on);  // 1 = hoisted DMA addressing (default), 0 = per-tile clamped addressing
 void attn_fwd(const AttnParams& p, hipStream_t s);
 struct AttnBwdParams {
   AttnParams f;

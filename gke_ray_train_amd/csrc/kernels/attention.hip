@@ -232,9 +232,24 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   // wave w fills image rows 8w .. 8w+7 of K and V: two 1-KiB pieces of 4 rows per image
   const int row0 = 8 * w + g, row1 = row0 + 4;
   const int ch0 = l16 ^ img_swz(row0), ch1 = l16 ^ img_swz(row1);
+  // per-lane source offsets of the two rows, fixed for the whole sweep: a tile inside the sequence
+  // then costs one 64-bit add per DMA (the tile base is uniform, SALU); only the tile that crosses
+  // the end takes the clamped per-lane row arithmetic (64-bit multiplies: quarter-rate VALU)
+  // (32-bit: a row of a 32-row tile times the row stride; one VGPR each)
+  const uint32_t ko0 = (uint32_t)(row0 * p.k_ss + ch0 * 8), ko1 = (uint32_t)(row1 * p.k_ss + ch1 * 8);
+  const uint32_t vo0 = (uint32_t)(row0 * p.v_ss + ch0 * 8), vo1 = (uint32_t)(row1 * p.v_ss + ch1 * 8);
   auto dma_tile = [&](int t, uint32_t slot_off) {
-    const int64_t k0r = min(t * F3N + row0, Sk - 1), k1r = min(t * F3N + row1, Sk - 1);  // past Sk: masked
     const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(8 * w * 256));
+    if (p.dma_fast && (t + 1) * F3N <= Sk) {
+      const bf16* kt = K + (int64_t)(t * F3N) * p.k_ss;
+      const bf16* vt = Vg + (int64_t)(t * F3N) * p.v_ss;
+      lds_dma16(kt + ko0, dst);
+      lds_dma16(vt + vo0, dst + F3IMG);
+      lds_dma16(kt + ko1, dst + 1024);
+      lds_dma16(vt + vo1, dst + F3IMG + 1024);
+      return;
+    }
+    const int64_t k0r = min(t * F3N + row0, Sk - 1), k1r = min(t * F3N + row1, Sk - 1);  // past Sk: masked
     lds_dma16(K + k0r * p.k_ss + ch0 * 8, dst);
     lds_dma16(Vg + k0r * p.v_ss + ch0 * 8, dst + F3IMG);
     lds_dma16(K + k1r * p.k_ss + ch1 * 8, dst + 1024);
@@ -546,15 +561,26 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   const int ch0 = l16 ^ img_swz(row0), ch1 = l16 ^ img_swz(row1);
   const int sl = l16 & 7;
   const int64_t st_lane = (l16 < 8 ? (int64_t)p.B * p.Hq * Sqp : 0) + 4 * sl;  // lse2 | delta
+  const uint32_t qo0 = (uint32_t)(row0 * p.q_ss + ch0 * 8), qo1 = (uint32_t)(row1 * p.q_ss + ch1 * 8);
+  const uint32_t oo0 = (uint32_t)(row0 * P.do_ss + ch0 * 8), oo1 = (uint32_t)(row1 * P.do_ss + ch1 * 8);
   auto dma_tile = [&](int hq, int qt, uint32_t slot_off) {
     const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + tok0 * p.q_ss + (int64_t)hq * p.q_hs;
     const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + tok0 * P.do_ss + (int64_t)hq * P.do_hs;
-    const int64_t q0r = min(qt + row0, Sq - 1), q1r = min(qt + row1, Sq - 1);  // past Sq: lse2 = +inf
     const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(8 * w * 256));
-    lds_dma16(Q + q0r * p.q_ss + ch0 * 8, dst);
-    lds_dma16(dO + q0r * P.do_ss + ch0 * 8, dst + K2IMG);
-    lds_dma16(Q + q1r * p.q_ss + ch1 * 8, dst + 1024);
-    lds_dma16(dO + q1r * P.do_ss + ch1 * 8, dst + K2IMG + 1024);
+    if (p.dma_fast && qt + K2M <= Sq) {  // tile inside the sequence: uniform base + fixed per-lane offsets
+      const bf16* qb = Q + (int64_t)qt * p.q_ss;
+      const bf16* ob = dO + (int64_t)qt * P.do_ss;
+      lds_dma16(qb + qo0, dst);
+      lds_dma16(ob + oo0, dst + K2IMG);
+      lds_dma16(qb + qo1, dst + 1024);
+      lds_dma16(ob + oo1, dst + K2IMG + 1024);
+    } else {
+      const int64_t q0r = min(qt + row0, Sq - 1), q1r = min(qt + row1, Sq - 1);  // past Sq: lse2 = +inf
+      lds_dma16(Q + q0r * p.q_ss + ch0 * 8, dst);
+      lds_dma16(dO + q0r * P.do_ss + ch0 * 8, dst + K2IMG);
+      lds_dma16(Q + q1r * p.q_ss + ch1 * 8, dst + 1024);
+      lds_dma16(dO + q1r * P.do_ss + ch1 * 8, dst + K2IMG + 1024);
+    }
     const int64_t ri = ((int64_t)b * p.Hq + hq) * Sqp + qt;
     lds_dma16(P.delta + st_lane + ri,
               __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(2 * K2IMG + w * 1024)));
@@ -824,13 +850,19 @@ __global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdPa
   const uint32_t smem0 = lds_u32(smem);
   const int row = 4 * w + g, ch = l16 ^ img_swz(row);
   const int64_t st_lane = ((l16 & 15) < 8 ? (int64_t)p.B * p.Hq * Sqp : 0) + 4 * (l16 & 7);  // lse2 | delta
+  const uint32_t qo = (uint32_t)(row * p.q_ss + ch * 8), oo = (uint32_t)(row * P.do_ss + ch * 8);
   auto dma_tile = [&](int hq, int qt, uint32_t slot_off) __attribute__((always_inline)) {
     const bf16* Q = (const bf16*)p.q + (int64_t)b * p.q_bs + tok0 * p.q_ss + (int64_t)hq * p.q_hs;
     const bf16* dO = (const bf16*)P.dout + (int64_t)b * P.do_bs + tok0 * P.do_ss + (int64_t)hq * P.do_hs;
-    const int64_t qr = min(qt + row, Sq - 1);  // past Sq: lse2 = +inf, p = 0
     const uint32_t dst = __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(4 * w * 256));
-    lds_dma16(Q + qr * p.q_ss + ch * 8, dst);
-    lds_dma16(dO + qr * P.do_ss + ch * 8, dst + K3IMG);
+    if (p.dma_fast && qt + K3M <= Sq) {  // tile inside the sequence: uniform base + fixed per-lane offsets
+      lds_dma16(Q + (int64_t)qt * p.q_ss + qo, dst);
+      lds_dma16(dO + (int64_t)qt * P.do_ss + oo, dst + K3IMG);
+    } else {
+      const int64_t qr = min(qt + row, Sq - 1);  // past Sq: lse2 = +inf, p = 0
+      lds_dma16(Q + qr * p.q_ss + ch * 8, dst);
+      lds_dma16(dO + qr * P.do_ss + ch * 8, dst + K3IMG);
+    }
     const int64_t ri = ((int64_t)b * p.Hq + hq) * Sqp + qt;
     lds_dma16(P.delta + st_lane + ri, __builtin_amdgcn_readfirstlane(smem0 + slot_off + (uint32_t)(2 * K3IMG + w * 1024)));
   };
@@ -1232,6 +1264,14 @@ int dkdv_form() {
   }
   return g_dkdv;
 }
+int g_dma_fast = -1;
+int dma_fast_now() {
+  if (g_dma_fast < 0) {
+    const char* e = getenv("GRT_ATTN_DMA_FAST");
+    g_dma_fast = e && atoi(e) == 0 ? 0 : 1;
+  }
+  return g_dma_fast;
+}
 int sched_now() {
   if (g_sched < 0) {
     const char* e = getenv("GRT_ATTN_SCHED");
@@ -1260,6 +1300,7 @@ static int pair_if_fills(int want, int nblk, int groups, int per_cu) {
 void attn_set_schedule(int s) { g_sched = s; }
 void attn_set_dkdv_form(int f) { g_dkdv = f == 1 ? 1 : 2; }
 int attn_get_dkdv_form() { return dkdv_form(); }
+void attn_set_dma_fast(int on) { g_dma_fast = on ? 1 : 0; }
 int attn_get_schedule() { return sched_now(); }
 
 // Padding-free packing (cu_seqlens): the grid is sized for the longest sequence, so a shorter one's
@@ -1269,6 +1310,7 @@ static int sched_for(const AttnParams& p, int bit) { return p.cu_seqlens ? 0 : (
 
 void attn_fwd(const AttnParams& p0, hipStream_t s) {
   AttnParams p = p0;
+  p.dma_fast = dma_fast_now();
   const int nqb = (p.Sq + F3M - 1) / F3M;
   p.sched = pair_if_fills(sched_for(p, 0), nqb, p.B * p.Hq, 2);
   const dim3 grid(q_grid(p.sched, nqb, p.B * p.Hq));
@@ -1284,6 +1326,7 @@ int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
 
 void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   AttnBwdParams p = p0;
+  p.f.dma_fast = dma_fast_now();
   const int64_t rows = (int64_t)p.f.B * p.f.Hq * sq_pad(p.f.Sq);
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
   const int nkb = (p.f.Sk + K2N - 1) / K2N;
