@@ -264,14 +264,28 @@ __global__ __launch_bounds__(kNT) void adamw_t_kernel(bf16* __restrict__ p, cons
   const int64_t tr = blockIdx.x / ntc, tc = blockIdx.x % ntc;
   // 4 threads per 256-byte row; per k the 4 threads take 4 adjacent 16-byte chunks (coalesced)
   const int tid = threadIdx.x, row = tid >> 2;
+  // every load of the thread's 4 chunks is issued before the first update (the compiler otherwise
+  // serialises load -> update -> store per chunk: one chunk's 96 bytes in flight per thread)
+  bf16x8 pva[4], gva[4];
+  f32x4 mva[4][2], vva[4][2];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t o = (tr * 64 + row) * cols + tc * 128 + ((tid & 3) + 4 * k) * 8;
+    pva[k] = *reinterpret_cast<const bf16x8*>(p + o);
+    gva[k] = *reinterpret_cast<const bf16x8*>(g + o);
+    mva[k][0] = *reinterpret_cast<const f32x4*>(m + o);
+    mva[k][1] = *reinterpret_cast<const f32x4*>(m + o + 4);
+    vva[k][0] = *reinterpret_cast<const f32x4*>(v + o);
+    vva[k][1] = *reinterpret_cast<const f32x4*>(v + o + 4);
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int ch = (tid & 3) + 4 * k;
     const int64_t o = (tr * 64 + row) * cols + tc * 128 + ch * 8;
-    const bf16x8 pv = *reinterpret_cast<const bf16x8*>(p + o);
-    const bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + o);
-    f32x4 mv[2] = {*reinterpret_cast<const f32x4*>(m + o), *reinterpret_cast<const f32x4*>(m + o + 4)};
-    f32x4 vv[2] = {*reinterpret_cast<const f32x4*>(v + o), *reinterpret_cast<const f32x4*>(v + o + 4)};
+    const bf16x8 pv = pva[k];
+    const bf16x8 gv = gva[k];
+    f32x4 mv[2] = {mva[k][0], mva[k][1]};
+    f32x4 vv[2] = {vva[k][0], vva[k][1]};
     bf16x8 out;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
@@ -358,7 +372,18 @@ void launch_adamw(dim3 grid, hipStream_t s, P* p, const G* g, float* m, float* v
 
 void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
                 int64_t n, const float* hyper, const float* gsp, hipStream_t s, int max_blocks, int64_t ioff) {
-  unsigned nb = grid_for(n / 8 + 1);
+  // workgroup cap of the grid-strided update (GRT_ADAMW_GRID_CAP, default 256 CUs x 64): fewer
+  // serial load -> update -> store iterations per thread. Isolated, Llama-2-7B shapes: 2048 ->
+  // 16384 workgroups is qkv 222 -> 207 us, gate_up 396 -> 373, down 200 -> 183 (65536: no further
+  // gain; scripts/gpu_adamw_ab.sh, profiles/r4_batch1.md)
+  static const int64_t cap = [] {
+    const char* e = std::getenv("GRT_ADAMW_GRID_CAP");
+    const int64_t c = e ? std::atoll(e) : 256 * 64;
+    return c > 0 ? c : (int64_t)256 * 64;
+  }();
+  int64_t nb64 = (n / 8 + 1 + kNT - 1) / kNT;
+  if (nb64 > cap) nb64 = cap;
+  unsigned nb = (unsigned)(nb64 < 1 ? 1 : nb64);
   if (max_blocks > 0 && nb > (unsigned)max_blocks) nb = (unsigned)max_blocks;
   const dim3 grid(nb);
   const uint64_t io = (uint64_t)ioff;
