@@ -1272,6 +1272,13 @@ int dma_fast_now() {
   }
   return g_dma_fast;
 }
+// the fast addressing keeps per-lane row offsets in 32 bits (24-bit multiplies): every row stride
+// of the streamed operands must be below 2^24 elements
+int dma_fast_for(const AttnParams& p, int64_t do_ss) {
+  const int64_t lim = (int64_t)1 << 24;
+  return dma_fast_now() && p.q_ss < lim && p.k_ss < lim && p.v_ss < lim && do_ss < lim && p.q_ss >= 0 &&
+         p.k_ss >= 0 && p.v_ss >= 0 && do_ss >= 0;
+}
 int sched_now() {
   if (g_sched < 0) {
     const char* e = getenv("GRT_ATTN_SCHED");
@@ -1310,7 +1317,7 @@ static int sched_for(const AttnParams& p, int bit) { return p.cu_seqlens ? 0 : (
 
 void attn_fwd(const AttnParams& p0, hipStream_t s) {
   AttnParams p = p0;
-  p.dma_fast = dma_fast_now();
+  p.dma_fast = dma_fast_for(p, 0);
   const int nqb = (p.Sq + F3M - 1) / F3M;
   p.sched = pair_if_fills(sched_for(p, 0), nqb, p.B * p.Hq, 2);
   const dim3 grid(q_grid(p.sched, nqb, p.B * p.Hq));
@@ -1326,7 +1333,7 @@ int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
 
 void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   AttnBwdParams p = p0;
-  p.f.dma_fast = dma_fast_now();
+  p.f.dma_fast = dma_fast_for(p.f, p.do_ss);
   const int64_t rows = (int64_t)p.f.B * p.f.Hq * sq_pad(p.f.Sq);
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
   const int nkb = (p.f.Sk + K2N - 1) / K2N;
