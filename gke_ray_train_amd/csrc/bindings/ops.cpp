@@ -175,6 +175,39 @@ Tensor swiglu_bwd(const Tensor& gu, const Tensor& dout) {
   grt::swiglu_bwd(dtype_of(gu), gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), rows, (int)f, cur_stream(gu));
   return dgu;
 }
+// (out, out^T) or None when the shape is not handled
+std::vector<Tensor> swiglu_fwd_t(const Tensor& gu, int64_t pad) {
+  check_contig(gu, "gu");
+  c10::OptionalDeviceGuard g(gu.device());
+  const int64_t two_f = gu.size(-1), rows = gu.numel() / two_f, f = two_f / 2;
+  TORCH_CHECK(gu.scalar_type() == at::kBFloat16 && gu.is_cuda(), "swiglu_fwd_t: bf16 on the device");
+  TORCH_CHECK(pad >= 0 && pad % 8 == 0 && (pad == 0 || gu.dim() == 2), "swiglu_fwd_t: pad % 8 == 0 on [rows, 2f]");
+  if (rows % 64 != 0 || f % 128 != 0 || reinterpret_cast<uintptr_t>(gu.data_ptr()) % 16 != 0) return {};
+  auto sizes = gu.sizes().vec();
+  sizes.back() = f;
+  auto out = pad == 0 ? at::empty(sizes, gu.options()) : at::empty({rows, f + pad}, gu.options()).narrow(1, 0, f);
+  auto outT = at::empty({f, rows}, gu.options());
+  if (!grt::swiglu_fwd_t(gu.data_ptr(), out.data_ptr(), outT.data_ptr(), rows, (int)f, cur_stream(gu), f + pad))
+    return {};
+  return {out, outT};
+}
+// (dgu, dgu^T) or None when the shape is not handled
+std::vector<Tensor> swiglu_bwd_t(const Tensor& gu, const Tensor& dout) {
+  check_contig(gu, "gu");
+  check_contig(dout, "dout");
+  c10::OptionalDeviceGuard g(gu.device());
+  const int64_t two_f = gu.size(-1), rows = gu.numel() / two_f, f = two_f / 2;
+  TORCH_CHECK(dout.numel() == rows * f && dout.scalar_type() == gu.scalar_type(), "dout shape mismatch");
+  TORCH_CHECK(gu.scalar_type() == at::kBFloat16 && gu.is_cuda(), "swiglu_bwd_t: bf16 on the device");
+  if (rows % 64 != 0 || f % 128 != 0 || reinterpret_cast<uintptr_t>(gu.data_ptr()) % 16 != 0 ||
+      reinterpret_cast<uintptr_t>(dout.data_ptr()) % 16 != 0)
+    return {};
+  auto dgu = at::empty_like(gu);
+  auto dguT = at::empty({two_f, rows}, gu.options());
+  if (!grt::swiglu_bwd_t(gu.data_ptr(), dout.data_ptr(), dgu.data_ptr(), dguT.data_ptr(), rows, (int)f, cur_stream(gu)))
+    return {};
+  return {dgu, dguT};
+}
 Tensor gelu_fwd(const Tensor& x) {
   check_contig(x, "x");
   c10::OptionalDeviceGuard g(x.device());
@@ -1212,6 +1245,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nf4_dequantize_t", &nf4_dequantize_t);
   m.def("nf4_dequantize_into", &nf4_dequantize_into);
   m.def("rmsnorm_bwd_dx", &rmsnorm_bwd_dx);
+  m.def("swiglu_fwd_t", &swiglu_fwd_t);
+  m.def("swiglu_bwd_t", &swiglu_bwd_t);
   m.def("transpose_into", &transpose_into);
   m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("attn_decode", &attn_decode);

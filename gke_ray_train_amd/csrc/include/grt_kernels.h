@@ -33,6 +33,10 @@ void layernorm_bwd(DType dt, const void* dy, const void* h, const void* w, const
 
 // ---------------- elementwise (elementwise.hip) ----------------
 void swiglu_fwd(DType dt, const void* gu, void* out, int64_t rows, int f, hipStream_t s, int64_t ldo = 0);
+// bf16 SwiGLU that also writes the transposed result for the TN weight gradient (out^T [f, rows],
+// dgu^T [2f, rows]); false = shape not handled (rows % 64, f % 128)
+bool swiglu_fwd_t(const void* gu, void* out, void* outT, int64_t rows, int f, hipStream_t s, int64_t ldo = 0);
+bool swiglu_bwd_t(const void* gu, const void* dout, void* dgu, void* dguT, int64_t rows, int f, hipStream_t s);
 void swiglu_bwd(DType dt, const void* gu, const void* dout, void* dgu, int64_t rows, int f,
                 hipStream_t s);
 // GELU (erf form) with optional fused dropout mask (uint8, 1 = keep, scale applied).

@@ -8,6 +8,8 @@
 // grid capped at 256 CUs x 8 workgroups and grid-strided (Guideline 11). RoPE reads the fused
 // QKV projection output in place (row stride `ld`) and writes attention-ready q/k, so there is
 // no transpose or split copy anywhere in the attention block.
+#include <limits.h>
+
 #include "grt_common.h"
 #include "grt_kernels.h"
 
@@ -67,6 +69,110 @@ __global__ __launch_bounds__(kNT) void swiglu_bwd_kernel(const T* __restrict__ g
     store16(dgu + r * 2 * f + c, dg);
     store16(dgu + r * 2 * f + f + c, du);
   }
+}
+
+// ---------------- SwiGLU with the transposed copy for the weight gradient ---------------------
+// The TN weight gradient of the down projection needs h^T (h = silu(gate) * up, [M, F]) and that of
+// the gate/up projection needs dgu^T ([2F, M]). A separate transpose kernel re-reads what these
+// kernels just wrote; here the producing kernel writes both layouts: one workgroup = 64 token rows x
+// 128 columns, the row-major result stored directly and staged in an XOR-swizzled bf16 LDS image
+// (16 chunks of 16 bytes per row) that gfx950's ds_read_b64_tr_b16 reads back transposed, stored as
+// 16-byte row segments of the transposed output (the scheme of transpose.hip).
+typedef __attribute__((address_space(3))) bf16x4 ew_lds_bf16x4_t;
+__device__ __forceinline__ int ew_tswz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int ew_toff(int row, int ch) { return row * 256 + 16 * (ch ^ ew_tswz(row)); }
+
+// image [64 rows][128 cols] -> dst rows c0 + (0..127) (row stride ldt), columns r0 .. r0 + 63
+__device__ __forceinline__ void ew_store_transposed(const char* img, bf16* __restrict__ dst, int64_t ldt, int64_t r0) {
+  const int t = threadIdx.x, l16 = t & 15, grp = t >> 4;
+#pragma unroll
+  for (int pp = 0; pp < 2; ++pp) {
+    const int pr = grp + 16 * pp;
+    const int cb = 16 * (pr >> 2), rb = 16 * (pr & 3);
+    bf16x4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rr = rb + 4 * k + (l16 >> 2), col = cb + 4 * (l16 & 3);
+      q[k] = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((ew_lds_bf16x4_t*)(img + ew_toff(rr, col >> 3) + 8 * ((col >> 2) & 1)));
+    }
+    bf16* d = dst + (int64_t)(cb + l16) * ldt + r0 + rb;
+    *reinterpret_cast<bf16x8*>(d) = __builtin_shufflevector(q[0], q[1], 0, 1, 2, 3, 4, 5, 6, 7);
+    *reinterpret_cast<bf16x8*>(d + 8) = __builtin_shufflevector(q[2], q[3], 0, 1, 2, 3, 4, 5, 6, 7);
+  }
+}
+
+// out [rows, f] (row stride ldo) and outT [f, rows]; rows % 64 == 0, f % 128 == 0
+__global__ __launch_bounds__(256) void swiglu_fwd_t_kernel(const bf16* __restrict__ gu, bf16* __restrict__ out,
+                                                           bf16* __restrict__ outT, int64_t rows, int f, int64_t ldo) {
+  __shared__ __attribute__((aligned(16))) char img[64 * 256];
+  const int ncb = f / 128;
+  const int64_t r0 = (int64_t)(blockIdx.x / ncb) * 64;
+  const int c0 = (blockIdx.x % ncb) * 128;
+  const int t = threadIdx.x, row = t >> 2;
+  const bf16* src = gu + (r0 + row) * 2 * f + c0;
+  bf16x8 gv[4], uv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // every load in flight before the math
+    const int ch = (t & 3) + 4 * k;
+    gv[k] = *reinterpret_cast<const bf16x8*>(src + ch * 8);
+    uv[k] = *reinterpret_cast<const bf16x8*>(src + f + ch * 8);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ch = (t & 3) + 4 * k;
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float g = static_cast<float>(gv[k][j]), u = static_cast<float>(uv[k][j]);
+      o[j] = static_cast<bf16>(g * sigmoidf_(g) * u);
+    }
+    *reinterpret_cast<bf16x8*>(out + (r0 + row) * ldo + c0 + ch * 8) = o;
+    *reinterpret_cast<bf16x8*>(img + ew_toff(row, ch)) = o;
+  }
+  __syncthreads();
+  ew_store_transposed(img, outT + (int64_t)c0 * rows, rows, r0);
+}
+
+// dgu [rows, 2f] and dguT [2f, rows]; rows % 64 == 0, f % 128 == 0
+__global__ __launch_bounds__(256) void swiglu_bwd_t_kernel(const bf16* __restrict__ gu, const bf16* __restrict__ dout,
+                                                           bf16* __restrict__ dgu, bf16* __restrict__ dguT,
+                                                           int64_t rows, int f) {
+  __shared__ __attribute__((aligned(16))) char img[2][64 * 256];
+  const int ncb = f / 128;
+  const int64_t r0 = (int64_t)(blockIdx.x / ncb) * 64;
+  const int c0 = (blockIdx.x % ncb) * 128;
+  const int t = threadIdx.x, row = t >> 2;
+  const bf16* src = gu + (r0 + row) * 2 * f + c0;
+  const bf16* dsrc = dout + (r0 + row) * f + c0;
+  bf16x8 gv[4], uv[4], dv[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ch = (t & 3) + 4 * k;
+    gv[k] = *reinterpret_cast<const bf16x8*>(src + ch * 8);
+    uv[k] = *reinterpret_cast<const bf16x8*>(src + f + ch * 8);
+    dv[k] = *reinterpret_cast<const bf16x8*>(dsrc + ch * 8);
+  }
+  bf16* drow = dgu + (r0 + row) * 2 * f + c0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ch = (t & 3) + 4 * k;
+    bf16x8 dg, du;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // same arithmetic as swiglu_bwd_kernel
+      const float g = static_cast<float>(gv[k][j]), u = static_cast<float>(uv[k][j]), d = static_cast<float>(dv[k][j]);
+      const float sg = sigmoidf_(g);
+      const float silu = g * sg;
+      du[j] = static_cast<bf16>(d * silu);
+      dg[j] = static_cast<bf16>(d * u * sg * (1.f + g * (1.f - sg)));
+    }
+    *reinterpret_cast<bf16x8*>(drow + ch * 8) = dg;
+    *reinterpret_cast<bf16x8*>(drow + f + ch * 8) = du;
+    *reinterpret_cast<bf16x8*>(img[0] + ew_toff(row, ch)) = dg;
+    *reinterpret_cast<bf16x8*>(img[1] + ew_toff(row, ch)) = du;
+  }
+  __syncthreads();
+  ew_store_transposed(img[0], dguT + (int64_t)c0 * rows, rows, r0);
+  ew_store_transposed(img[1], dguT + (int64_t)(f + c0) * rows, rows, r0);
 }
 
 // ------------------------------- GELU (erf) ---------------------------------
@@ -343,6 +449,19 @@ void swiglu_bwd(DType dt, const void* gu, const void* dout, void* dgu, int64_t r
 #define K(T, ...) hipLaunchKernelGGL(swiglu_bwd_kernel<T>, dim3(grid_for(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)gu, (const T*)dout, (T*)dgu, rows, f)
   GRT_DISPATCH(dt, K, 0);
 #undef K
+}
+bool swiglu_fwd_t(const void* gu, void* out, void* outT, int64_t rows, int f, hipStream_t s, int64_t ldo) {
+  if (ldo <= 0) ldo = f;
+  if (rows % 64 != 0 || f % 128 != 0 || ldo % 8 != 0 || rows / 64 * (f / 128) >= INT32_MAX) return false;
+  hipLaunchKernelGGL(swiglu_fwd_t_kernel, dim3((unsigned)(rows / 64 * (f / 128))), dim3(256), 0, s,
+                     (const bf16*)gu, (bf16*)out, (bf16*)outT, rows, f, ldo);
+  return true;
+}
+bool swiglu_bwd_t(const void* gu, const void* dout, void* dgu, void* dguT, int64_t rows, int f, hipStream_t s) {
+  if (rows % 64 != 0 || f % 128 != 0 || rows / 64 * (f / 128) >= INT32_MAX) return false;
+  hipLaunchKernelGGL(swiglu_bwd_t_kernel, dim3((unsigned)(rows / 64 * (f / 128))), dim3(256), 0, s,
+                     (const bf16*)gu, (const bf16*)dout, (bf16*)dgu, (bf16*)dguT, rows, f);
+  return true;
 }
 void gelu_fwd(DType dt, const void* x, void* y, int64_t n, hipStream_t s) {
 #define K(T, ...) hipLaunchKernelGGL(gelu_fwd_kernel<T>, dim3(grid_for(n / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)x, (T*)y, n / Vec16<T>::N)

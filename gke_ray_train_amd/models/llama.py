@@ -160,6 +160,13 @@ class LlamaAttention(nn.Module):
         return self.o_proj(o)
 
 
+def _direct_wgrad(lin) -> bool:
+    """``lin``'s weight gradient runs on the direct TN path of ops/linear.py in this forward."""
+    w = getattr(lin, "weight", None)
+    return (isinstance(w, torch.Tensor) and w.requires_grad and w.is_cuda and torch.is_grad_enabled()
+            and getattr(w, "_grt_slot", None) is not None)
+
+
 class LlamaMLP(nn.Module):
     def __init__(self, cfg: LlamaConfig, device=None, dtype=None):
         super().__init__()
@@ -168,7 +175,10 @@ class LlamaMLP(nn.Module):
         self.down_proj = Linear(f, cfg.hidden_size, bias=False, device=device, dtype=dtype)
 
     def forward(self, x):
-        return self.down_proj(ops.swiglu(self.gate_up_proj(x), pad=_tail_pad(self.down_proj)))
+        # trainable projections on the direct-gradient path take their weight-gradient operand
+        # transposed from the SwiGLU kernels (h^T for down, dgu^T for gate / up)
+        return self.down_proj(ops.swiglu(self.gate_up_proj(x), pad=_tail_pad(self.down_proj),
+                                         fwd_t=_direct_wgrad(self.down_proj), bwd_t=_direct_wgrad(self.gate_up_proj)))
 
 
 class RMSNorm(nn.Module):

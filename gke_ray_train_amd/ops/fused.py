@@ -131,25 +131,52 @@ def layer_norm(x, w, b=None, eps=1e-5, residual=None):
 
 
 # ----------------------------------------------------------------------------- activations
+# SwiGLU kernels that also write the transposed result for the TN weight gradients of the
+# neighbouring projections (h^T for down_proj, dgu^T for gate_up_proj; elementwise.hip
+# swiglu_*_t_kernel): the consumer (ops/linear.py _DirectGradLinear) takes the copy from the
+# tensor's ``_grt_T`` attribute instead of running its own transpose. GRT_SWIGLU_T=0: off.
+_SWIGLU_T = os.environ.get("GRT_SWIGLU_T", "1") != "0"
+
+
 class _SwiGLU(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, gu, pad=0):
+    def forward(ctx, gu, pad=0, fwd_t=False, bwd_t=False):
         gu = gu.contiguous()
         ctx.save_for_backward(gu)
-        return _native.kernels().swiglu_fwd(gu, pad)
+        ctx.bwd_t = bwd_t
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the h^T output
+        C = _native.kernels()
+        if fwd_t:
+            r = C.swiglu_fwd_t(gu, pad)
+            if r:
+                ctx.mark_non_differentiable(r[1])
+                return r[0], r[1]
+        return C.swiglu_fwd(gu, pad), None
 
     @staticmethod
-    def backward(ctx, dout):
+    def backward(ctx, dout, _dt=None):
         (gu,) = ctx.saved_tensors
-        return _native.kernels().swiglu_bwd(gu, dout.contiguous()), None
+        C = _native.kernels()
+        if ctx.bwd_t:
+            r = C.swiglu_bwd_t(gu, dout.contiguous())
+            if r:
+                r[0]._grt_T = r[1]
+                return r[0], None, None, None
+        return C.swiglu_bwd(gu, dout.contiguous()), None, None, None
 
 
-def swiglu(gu, pad: int = 0):
+def swiglu(gu, pad: int = 0, fwd_t: bool = False, bwd_t: bool = False):
     """silu(gu[..., :F]) * gu[..., F:] for the fused [gate | up] projection output; ``pad`` as in
-    ``rms_norm`` (the down projection's LoRA tail)."""
+    ``rms_norm`` (the down projection's LoRA tail). ``fwd_t`` / ``bwd_t``: also produce h^T / dgu^T
+    for a trainable down / gate_up projection's weight gradient (bf16, rows % 64, F % 128)."""
     if _gpu(gu):
         pad = pad if gu.dim() == 2 else 0
-        return _tail(_SwiGLU.apply(gu, pad), pad)
+        fwd_t = fwd_t and _SWIGLU_T and gu.dtype == torch.bfloat16
+        bwd_t = bwd_t and _SWIGLU_T and gu.dtype == torch.bfloat16
+        y, yt = _SwiGLU.apply(gu, pad, fwd_t, bwd_t)
+        if yt is not None:
+            y._grt_T = yt
+        return _tail(y, pad)
     return _ref.swiglu(gu)
 
 

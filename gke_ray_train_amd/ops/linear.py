@@ -165,6 +165,24 @@ def transposed(t2: torch.Tensor) -> torch.Tensor:
     return tt
 
 
+def provided_transposed(t2: torch.Tensor, t: torch.Tensor):
+    """The contiguous [C, M] transpose of ``t2`` ([M, C], a 2-D view of ``t``) that the kernel which
+    produced ``t`` wrote beside it (``t._grt_T``), or None. Taken once: the attribute is cleared, so
+    the copy lives only as long as its consumer keeps it."""
+    tt = getattr(t, "_grt_T", None)
+    if tt is None:
+        return None
+    try:
+        del t._grt_T
+    except AttributeError:
+        pass
+    if (tt.dim() == 2 and tt.shape[0] == t2.shape[1] and tt.shape[1] == t2.shape[0] and tt.is_contiguous()
+            and tt.dtype == t2.dtype == torch.bfloat16 and _WGRAD_NATIVE and _WGRAD_TN
+            and t2.shape[0] % 64 == 0 and t2.shape[1] % 64 == 0):
+        return tt
+    return None
+
+
 def wgrad_tn(dyt: torch.Tensor, xt: torch.Tensor, out: torch.Tensor, accumulate: bool) -> torch.Tensor:
     """dW = dY^T X from the already transposed operands ([N, M], [K, M]): the TN library GEMM."""
     if accumulate:
@@ -219,8 +237,12 @@ class _DirectGradLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1])
-        ctx.x_t = _WGRAD_XT_FWD and ctx.needs_input_grad[1] and w.shape[0] % 64 == 0 and _tn_wgrad_ok(x2)
-        ctx.save_for_backward(transposed(x2) if ctx.x_t else x, w)
+        # X^T written by the producing kernel (ops.fused.swiglu: the down projection's input)
+        xt = provided_transposed(x2, x) if ctx.needs_input_grad[1] else None
+        ctx.x_t = xt is not None and w.shape[0] % 64 == 0 and _tn_wgrad_ok(x2)
+        if not ctx.x_t and _WGRAD_XT_FWD and ctx.needs_input_grad[1] and w.shape[0] % 64 == 0 and _tn_wgrad_ok(x2):
+            ctx.x_t, xt = True, transposed(x2)
+        ctx.save_for_backward(xt if ctx.x_t else x, w)
         ctx.has_b = b is not None
         ctx.wt_ev = transpose_for_backward(w) if ctx.needs_input_grad[0] else None
         return F.linear(x, w, b)
@@ -229,8 +251,12 @@ class _DirectGradLinear(torch.autograd.Function):
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dyt = None
-        if ctx.x_t:  # X^T saved by the forward: dY^T now, while dY is fresh from its producer
+        # dY^T written by the producing kernel (ops.fused.swiglu backward: the gate / up gradient)
+        dyt = provided_transposed(dy2, dy) if ctx.needs_input_grad[1] else None
+        if dyt is not None and not ctx.x_t:  # X was saved untransposed: its transpose now
+            x = transposed(x.reshape(-1, x.shape[-1]))
+            ctx.x_t = True
+        if ctx.x_t and dyt is None:  # X^T saved by the forward: dY^T now, while dY is fresh from its producer
             if not dy2.is_contiguous():
                 dy2 = dy2.contiguous()
             dyt = transposed(dy2) if _WGRAD_DYT_FIRST else None

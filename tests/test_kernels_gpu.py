@@ -814,6 +814,59 @@ def test_nf4_dequant_v2_exact(rows, cols):
     assert torch.equal(C.nf4_dequantize_t(q, absmax, rows, cols, 64).cpu(), ref.t())
 
 
+def test_swiglu_transposing_kernels_exact():
+    """swiglu_fwd_t / swiglu_bwd_t: the row-major results are bit-equal to the plain kernels and the
+    second outputs are exactly their transposes; unhandled shapes return nothing."""
+    C = _C()
+    g = torch.Generator(device=DEV).manual_seed(9)
+    gu = torch.randn(256, 2 * 384, device=DEV, generator=g).bfloat16()
+    dout = torch.randn(256, 384, device=DEV, generator=g).bfloat16()
+    out = C.swiglu_fwd(gu, 0)
+    o, ot = C.swiglu_fwd_t(gu, 0)
+    assert torch.equal(o, out) and torch.equal(ot, out.t())
+    o64, ot64 = C.swiglu_fwd_t(gu, 64)  # the [rows, f + 64] LoRA-tail row buffer
+    assert o64.stride(0) == 384 + 64 and torch.equal(o64, out) and torch.equal(ot64, out.t())
+    dgu = C.swiglu_bwd(gu, dout)
+    d, dt = C.swiglu_bwd_t(gu, dout)
+    assert torch.equal(d, dgu) and torch.equal(dt, dgu.t())
+    assert not C.swiglu_fwd_t(gu[:100].contiguous(), 0) and not C.swiglu_bwd_t(gu[:100].contiguous(), dout[:100].contiguous())
+
+
+def test_swiglu_transposed_wgrad_path_matches(monkeypatch):
+    """Llama MLP under the DDP engine: with the transposing SwiGLU the down / gate_up weight
+    gradients take h^T / dgu^T from the SwiGLU kernels (two fewer transposes per layer) and every
+    gradient is bit-identical to the separate-transpose path."""
+    from gke_ray_train_amd.models import build_llama, get_config
+    from gke_ray_train_amd.ops import fused as Fu
+    from gke_ray_train_amd.ops import linear as L
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    cfg = get_config("llama-tiny-gqa", intermediate_size=1536)
+    ids = torch.randint(0, 512, (2, 256), device=DEV, generator=torch.Generator(device=DEV).manual_seed(1))
+    calls = {"n": 0}
+    real = L.wgrad_tn
+
+    def counting(*a):
+        calls["n"] += 1
+        return real(*a)
+    monkeypatch.setattr(L, "wgrad_tn", counting)
+    out, ncalls = [], []
+    for flag in (False, True):
+        monkeypatch.setattr(Fu, "_SWIGLU_T", flag)
+        calls["n"] = 0
+        m = build_llama(cfg, device=DEV, dtype=torch.bfloat16, seed=2)
+        ddp = DistributedDataParallel(m)
+        m(ids, labels=ids)["loss"].backward()
+        ddp.finish_gradient_sync()
+        torch.cuda.synchronize()
+        out.append({n: p.grad.clone() for n, p in m.named_parameters()})
+        ncalls.append(calls["n"])
+    for n in out[0]:
+        assert torch.equal(out[0][n], out[1][n]), n
+    # with the flag: the down (h^T from the forward kernel) and gate_up (dgu^T from the backward
+    # kernel) weight gradients of both layers ran on the provided copies
+    assert ncalls == [0, 2 * cfg.num_hidden_layers], ncalls
+
+
 def test_transposed_dgrad_linear_matches_nn():
     """Trainable DDP weight: forward writes W^T on a side stream, backward runs the TN GEMM;
     gradients equal the NN path (GRT_TRANSPOSED_DGRAD=0) to bf16 rounding."""
