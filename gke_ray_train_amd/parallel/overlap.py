@@ -110,6 +110,10 @@ class OverlappedOptimizer:
     def _make_stream(dev):
         """The update's side stream: confined to GRT_OPT_CUS CUs (``ops/streams.py``) so the
         forward GEMMs keep the rest of the chip; 0 = an ordinary stream on every CU."""
+        if os.environ.get("GRT_OVERLAP_OPT_SERIAL", "0") == "1":
+            # A/B switch: the same per-module (transposing) updates, run in order on the compute
+            # stream at step() instead of beside the next forward
+            return torch.cuda.current_stream(dev)
         n = int(os.environ.get("GRT_OPT_CUS", "0"))
         if n > 0:
             from ..ops.streams import cu_masked_stream
