@@ -213,28 +213,36 @@ __global__ __launch_bounds__(kNT) void norm_bwd_kernel(const T* __restrict__ dy,
 // accumulators so the slab loads (256 contiguous bytes per wave) stay in flight.
 // GO: output type of dw / db (float, or bf16 written straight into a gradient buffer; ACC adds
 // to what the buffer holds).
+// One workgroup = kColsumCols columns x (256 / kColsumCols) slab-row groups: 16 columns per
+// workgroup gives 256 workgroups at d = 4096 (64 columns left 3/4 of the CUs idle: 22 us per call
+// in the headline step for a 16 MB slab)
+constexpr int kColsumCols = 16;
+constexpr int kColsumGroups = kNT / kColsumCols;
 template <typename GO, bool ACC>
 __global__ __launch_bounds__(kNT) void colsum_kernel(const float* __restrict__ ws, int nb, int d, int ncols,
                                                      GO* __restrict__ dw, GO* __restrict__ db) {
-  __shared__ float red[4][64];
-  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int j = blockIdx.x * 64 + c;
+  __shared__ float red[kColsumGroups][kColsumCols];
+  const int c = threadIdx.x % kColsumCols, rg = threadIdx.x / kColsumCols;
+  const int j = blockIdx.x * kColsumCols + c;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   if (j < ncols) {
     const int64_t ld = 2 * (int64_t)d;
+    constexpr int G = kColsumGroups;
     int b = rg;
-    for (; b + 12 < nb; b += 16) {
+    for (; b + 3 * G < nb; b += 4 * G) {
       a0 += ws[(int64_t)b * ld + j];
-      a1 += ws[(int64_t)(b + 4) * ld + j];
-      a2 += ws[(int64_t)(b + 8) * ld + j];
-      a3 += ws[(int64_t)(b + 12) * ld + j];
+      a1 += ws[(int64_t)(b + G) * ld + j];
+      a2 += ws[(int64_t)(b + 2 * G) * ld + j];
+      a3 += ws[(int64_t)(b + 3 * G) * ld + j];
     }
-    for (; b < nb; b += 4) a0 += ws[(int64_t)b * ld + j];
+    for (; b < nb; b += G) a0 += ws[(int64_t)b * ld + j];
   }
   red[rg][c] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (rg == 0 && j < ncols) {
-    const float s = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < kColsumGroups; ++g) s += red[g][c];
     GO* out = j < d ? dw : db;
     const int jj = j < d ? j : j - d;
     if (out) out[jj] = from_f<GO>(ACC ? to_f(out[jj]) + s : s);
@@ -307,7 +315,7 @@ void launch_bwd(const void* dy, const void* h, const void* w, const float* mean,
 #undef GRT_NB2
   if (ws == nullptr) return;
   const int ncols = RMS ? d : 2 * d;
-  const dim3 cg((ncols + 63) / 64);
+  const dim3 cg((ncols + kColsumCols - 1) / kColsumCols);
   if (dw_t != nullptr && RMS) {  // weight gradient in T, straight into its gradient slot
     if (accumulate)
       hipLaunchKernelGGL((colsum_kernel<T, true>), cg, dim3(kNT), 0, s, ws, nb, d, ncols, (T*)dw_t, (T*)nullptr);

@@ -1,0 +1,15 @@
+#!/bin/bash
+# colsum grid change: norm tests + DDP/FSDP gradient tests, headline bench x2, smoke.
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/${1:-r4colsum}; rm -rf $OUT; mkdir -p $OUT
+fatal() { case $1 in 124|134|137|139) echo "fatal rc $1"; exit $1;; esac; }
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_parallel_gpu.py -q -k "norm or ddp or fsdp or transposed or direct" --timeout 120 \
+    --timeout-method thread -p no:cacheprovider > $OUT/test.log 2>&1; rc=$?
+grep -E "^FAILED|^ERROR" $OUT/test.log | head; tail -1 $OUT/test.log; fatal $rc; [ $rc -eq 0 ] || exit $rc
+for r in 1 2; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $OUT/b_$r.log 2>&1; rc=$?
+  echo "bench r$r $(tail -1 $OUT/b_$r.log | grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' | tr '\n' ' ')"; fatal $rc
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 3 --warmup 2 > $OUT/prof.log 2>&1; rc=$?
+grep -h "colsum" $OUT/prof/run_kernel_stats.csv | cut -c1-200; fatal $rc
+echo done
