@@ -281,6 +281,9 @@ struct GemmParams {
 };
 bool gemm_nt_supported(int64_t M, int64_t N, int64_t K);
 void gemm_nt(const GemmParams& p, hipStream_t stream);
+// 256x256x64-tile kernel (gemm_k64.hip): M, N % 256, K % 128, K >= 128, byte offsets below 2^31
+bool gemm_nt_k64_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t ldb);
+void gemm_nt_k64(const GemmParams& p, hipStream_t stream);
 // weight-gradient form on token-major operands: C[M][N] (+)= sum_k A[k][m] * B[k][n] (a = A [K][M],
 // b = B [K][N]); M % 256 == 0, N % 256 == 0, K % 64 == 0
 void gemm_tt2(const GemmParams& p, hipStream_t stream);

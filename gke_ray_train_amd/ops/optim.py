@@ -160,6 +160,39 @@ class FusedAdamW(torch.optim.Optimizer):
     def _sr(self) -> float:
         return 1.0 if self.stochastic_rounding and not self.master_weights else 0.0
 
+    _host_states = False  # OffloadedAdamW: moments live in pinned host memory
+
+    def _state_tensor(self, v: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+        """A loaded moment / master copy in the layout the fused kernels take: fp32, contiguous,
+        on the parameter's device (pinned host memory for the offloaded optimizers)."""
+        v = v.detach().to(torch.float32, copy=True)  # never alias the state dict's tensors
+        if self._host_states:
+            v = v.cpu().contiguous()
+            return v.pin_memory() if torch.cuda.is_available() else v
+        return v.to(p.device).contiguous()
+
+    def load_state_dict(self, state_dict):
+        """torch.optim.Optimizer.load_state_dict casts floating state to the parameter's dtype and
+        device — bf16 on the GPU for a bf16 model — which would drop the moments to bf16 (and put
+        an offloaded optimizer's host state in HBM). Restore them from the checkpoint's own tensors
+        in fp32 after the base class has mapped the parameters."""
+        super().load_state_dict(state_dict)
+        idmap = {}
+        for g, sg in zip(self.param_groups, state_dict["param_groups"]):
+            for p, pid in zip(g["params"], sg["params"]):
+                idmap[pid] = p
+        for pid, sst in state_dict["state"].items():
+            p = idmap.get(pid)
+            if p is None:
+                continue
+            st = self.state[p]
+            for k in ("exp_avg", "exp_avg_sq", "master"):
+                v = sst.get(k)
+                if isinstance(v, torch.Tensor):
+                    st[k] = self._state_tensor(v, p)
+            if isinstance(st.get("step"), torch.Tensor):
+                st["step"] = st["step"].detach().to("cpu", torch.float32, copy=True).reshape(())
+
     def _init_state(self, p):
         st = self.state[p]
         if len(st) == 0:

@@ -864,17 +864,20 @@ class SFTTrainer:
                 m = self._unwrapped()
                 is_adapter = hasattr(m, "adapter_state_dict") and hasattr(m, "lora_modules")
                 snap = self._snapshot if self.device.type == "cuda" and is_adapter else None
+                # ZeRO: rank 0 holds only its 1/world shard of the AdamW state, which must never sit
+                # under the HF full-state name optimizer.pt; every rank writes optimizer_rank<r>.pt
+                opt_sd = {} if sharded_opt else self.optimizer.state_dict()
                 if snap is not None:  # ONE pinned snapshot of optimizer state (+ adapters)
-                    host = snap.take({"o": self.optimizer.state_dict(),
-                                      "a": m.adapter_state_dict() if is_adapter else None})
+                    host = snap.take({"o": opt_sd, "a": m.adapter_state_dict() if is_adapter else None})
                 else:
-                    host = {"o": _to_host(self.optimizer.state_dict()),
-                            "a": _to_host(m.adapter_state_dict()) if is_adapter else None}
+                    host = {"o": _to_host(opt_sd), "a": _to_host(m.adapter_state_dict()) if is_adapter else None}
                 tm.append(time.time())
-                files = {"optimizer.pt": host["o"],
-                         "scheduler.pt": self.scheduler.state_dict(), "training_args.bin": a.to_dict()}
+                files = {"scheduler.pt": self.scheduler.state_dict(), "training_args.bin": a.to_dict()}
+                if not sharded_opt:
+                    files["optimizer.pt"] = host["o"]
                 st = dict(self.state, train_batch_size=a.per_device_train_batch_size, max_steps=a.max_steps,
-                          logging_steps=a.logging_steps, save_steps=a.save_steps, eval_steps=a.eval_steps)
+                          logging_steps=a.logging_steps, save_steps=a.save_steps, eval_steps=a.eval_steps,
+                          grt_optimizer_layout={"zero": sharded_opt, "world": self.world})
                 st = json.loads(json.dumps(st))  # frozen copy: the live state keeps changing
                 adapter = None
                 if is_adapter:
@@ -900,7 +903,7 @@ class SFTTrainer:
         try:
             os.makedirs(d, exist_ok=True)
             torch.save(_rng_snapshot(), os.path.join(d, f"rng_state_{self.rank}.pth"))
-            if sharded_opt:  # ZeRO: each rank holds 1/world of the AdamW state; rank 0's is also optimizer.pt
+            if sharded_opt:  # ZeRO: each rank holds 1/world of the AdamW state
                 torch.save(_to_host(self.optimizer.state_dict()), os.path.join(d, f"optimizer_rank{self.rank}.pt"))
         except Exception as e:
             err = err or e
@@ -963,15 +966,26 @@ class SFTTrainer:
             from ..models.hub import from_pretrained
             loaded = from_pretrained(d, device=self.device, torch_dtype=next(m.parameters()).dtype)
             m.load_state_dict(loaded.state_dict())
-        shard = os.path.join(d, f"optimizer_rank{self.rank}.pt")
-        if getattr(self.engine, "zero", False) and not os.path.exists(shard):
-            raise FileNotFoundError(f"{d}: sharded (ZeRO) optimizer state for rank {self.rank} is missing "
-                                    f"(checkpoint written at another world size?)")
-        opt_f = shard if getattr(self.engine, "zero", False) else os.path.join(d, "optimizer.pt")
-        self.optimizer.load_state_dict(torch.load(opt_f, map_location=self.device, weights_only=True))
-        self.scheduler.load_state_dict(torch.load(os.path.join(d, "scheduler.pt"), weights_only=True))
         with open(os.path.join(d, "trainer_state.json")) as f:
             st = json.load(f)
+        zero_now = bool(getattr(self.engine, "zero", False))
+        layout = st.pop("grt_optimizer_layout", None)
+        if layout is not None:  # the optimizer layout must match: a shard is 1/world of the flat state
+            if bool(layout.get("zero")) != zero_now or (zero_now and int(layout.get("world", -1)) != self.world):
+                raise ValueError(
+                    f"{d}: optimizer state was written {'ZeRO-sharded' if layout.get('zero') else 'unsharded'} "
+                    f"at world {layout.get('world')}; this run is {'ZeRO-sharded' if zero_now else 'unsharded'} "
+                    f"at world {self.world}. Resume with the same world size and GRT_SFT_ZERO setting.")
+        shard = os.path.join(d, f"optimizer_rank{self.rank}.pt")
+        if zero_now and not os.path.exists(shard):
+            raise FileNotFoundError(f"{d}: sharded (ZeRO) optimizer state for rank {self.rank} is missing "
+                                    f"(checkpoint written at another world size?)")
+        opt_f = shard if zero_now else os.path.join(d, "optimizer.pt")
+        if not os.path.exists(opt_f):
+            raise FileNotFoundError(f"{d}: {os.path.basename(opt_f)} is missing (checkpoint written with a ZeRO-sharded "
+                                    f"optimizer? its state is in optimizer_rank<r>.pt)")
+        self.optimizer.load_state_dict(torch.load(opt_f, map_location=self.device, weights_only=True))
+        self.scheduler.load_state_dict(torch.load(os.path.join(d, "scheduler.pt"), weights_only=True))
         self.state.update(st)
         rp = os.path.join(d, f"rng_state_{self.rank}.pth")
         if os.path.exists(rp):  # continue the RNG streams (dropout masks, sampler) where they stopped

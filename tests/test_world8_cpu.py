@@ -1,0 +1,252 @@
+"""8-rank rehearsal of the whole data plane on the CPU (gloo), the world size of one MI355X node.
+
+At world 8 the code paths differ from the 2-rank tests: ZeRO's bucket alignment is 64 x world
+(parallel/ddp.py), FSDP pads every unit's flat buffer to a multiple of world (parallel/fsdp.py),
+the ZeRO shard of a bucket can be empty on high ranks, and eight workers must fail fast together.
+GRT_GLOO_TENSOR_COLLECTIVES=1 makes gloo run the exact RCCL call pattern (reduce_scatter_tensor /
+all_gather_into_tensor into views). Reference: DDP over NCCL at 16 workers,
+ray-jobs/pytorch_llm_ray.py:230,346-350,362-376; ray-jobs/fine_tune_llama_ray.py:439-457.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORLD = 8
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ids(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, 512, (n, 32), generator=g)
+
+
+def _engines_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GRT_GLOO_TENSOR_COLLECTIVES="1",
+                      OMP_NUM_THREADS="1")
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    try:
+        from gke_ray_train_amd.models import build_llama
+        from gke_ray_train_amd.ops import FusedAdamW
+        from gke_ray_train_amd.parallel import DistributedDataParallel
+        from gke_ray_train_amd.parallel.fsdp import FullyShardedDataParallel
+        accum = 2
+        # (1) DDP gradients with accumulation, small buckets (many buckets, uneven last one)
+        m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=7)
+        ddp = DistributedDataParallel(m, bucket_cap_mb=0.05)
+        assert ddp.num_buckets() > 4
+        mine = _ids(world * accum, 0).view(world, accum, 1, 32)[rank]
+        for j in range(accum):
+            with ddp.no_sync(j < accum - 1):
+                (m(mine[j], labels=mine[j])["loss"] / accum).backward()
+        ddp.finish_gradient_sync()
+        out["ddp_grads"] = {n: (p.grad / world).numpy().copy() for n, p in m.named_parameters()}
+        del m, ddp
+        # (2) ZeRO (reduce-scatter + sharded AdamW + all-gather) vs replicated DDP: 3 optimizer steps
+        for zero in (False, True):
+            m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=3)
+            eng = DistributedDataParallel(m, bucket_cap_mb=0.1, shard_optimizer=zero)
+            assert eng.zero == zero
+            opt = FusedAdamW(eng.optimizer_param_groups(0.1), lr=3e-3)
+            if zero:
+                n_opt = sum(p.numel() for gp in opt.param_groups for p in gp["params"])
+                assert n_opt * world <= sum(g.flat.numel() for g in eng.groups) + 64 * world
+            for step in range(3):
+                ids = _ids(world * 2, 10 + step).view(world, 2, 32)[rank]
+                eng(ids, labels=ids)["loss"].backward()
+                eng.finish_gradient_sync()
+                st = eng.clip_grad_norm_(0.5)
+                opt.step(grad_scale=st)
+                eng.after_optimizer_step()
+                eng.zero_grad()
+            eng.wait_params()
+            out[f"params_zero{int(zero)}"] = {n: p.detach().numpy().copy() for n, p in m.named_parameters()}
+            del m, eng, opt
+        # (3) FSDP full-shard, activation checkpointing + accumulation
+        m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=5)
+        m.gradient_checkpointing_enable()
+        f = FullyShardedDataParallel(m)
+        mine = _ids(world * accum, 1).view(world, accum, 1, 32)[rank]
+        for j in range(accum):
+            with f.no_sync(j < accum - 1):
+                (f(mine[j], labels=mine[j])["loss"] / accum).backward()
+        f.finish_gradient_sync()
+        out["fsdp_grads"] = {k: (v / world).numpy().copy() for k, v in f.full_grad_dict().items()}
+        out["fsdp_norm"] = float(f.clip_grad_norm_(1.0).buf[0])
+        q.put((rank, out))
+    except BaseException as e:  # report instead of hanging the parent on q.get
+        q.put((rank, {"error": repr(e)}))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _reference_grads(seed_model, seed_ids, world, accum, ckpt=False):
+    from gke_ray_train_amd.models import build_llama
+    m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=seed_model)
+    if ckpt:
+        m.gradient_checkpointing_enable()
+    ids = _ids(world * accum, seed_ids).view(world * accum, 1, 32)
+    for j in range(world * accum):
+        (m(ids[j], labels=ids[j])["loss"] / (world * accum)).backward()
+    return {n: p.grad.clone() for n, p in m.named_parameters()}
+
+
+def test_ddp_zero_fsdp_equivalence_world8():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_engines_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(WORLD):
+            r, out = q.get(timeout=900)
+            assert "error" not in out, f"rank {r}: {out['error']}"
+            res[r] = out
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    # every rank ends with identical DDP gradients, ZeRO/DDP parameters and FSDP gradients
+    for r in range(1, WORLD):
+        for key in ("ddp_grads", "params_zero0", "params_zero1", "fsdp_grads"):
+            for n, v in res[0][key].items():
+                assert np.array_equal(v, res[r][key][n]), f"{key} {n}: rank {r} diverged from rank 0"
+    # DDP == one process on the global batch
+    ref = _reference_grads(7, 0, WORLD, 2)
+    for n, g in ref.items():
+        assert np.allclose(g.numpy(), res[0]["ddp_grads"][n], atol=1e-5, rtol=1e-4), n
+    # ZeRO == replicated DDP after 3 AdamW steps. The reduce-scatter sums the 8 contributions in a
+    # different order than the all-reduce; AdamW's m / sqrt(v) amplifies that on near-zero
+    # gradient elements (rare embedding rows), so the bound is 3 % of one lr step (lr 3e-3)
+    for n, v in res[0]["params_zero0"].items():
+        assert abs(v - res[0]["params_zero1"][n]).max() < 1e-4, n
+    # FSDP == one process (checkpointed forward), and its global norm
+    ref = _reference_grads(5, 1, WORLD, 2, ckpt=True)
+    for n, g in ref.items():
+        assert np.allclose(g.numpy(), res[0]["fsdp_grads"][n], atol=2e-5, rtol=1e-4), n
+    ref_norm = float(torch.sqrt(sum(g.pow(2).sum() for g in ref.values())))
+    assert abs(ref_norm - res[0]["fsdp_norm"]) < 1e-4 * max(1.0, ref_norm)
+
+
+def _fail_loop(config):
+    """Eight ranks train; rank 3 raises inside its backward while the other seven wait in the
+    gradient all-reduce of the same step."""
+    from gke_ray_train_amd import train
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    rank = train.get_context().get_world_rank()
+    m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=1)
+    ddp = DistributedDataParallel(m)
+    ids = _ids(2, rank)
+    for step in range(3):
+        loss = ddp(ids, labels=ids)["loss"]
+        if step == 1 and rank == 3:
+            def boom(_g):
+                raise RuntimeError("rank 3 exploded mid-backward")
+            loss.register_hook(boom)
+        loss.backward()
+        ddp.finish_gradient_sync()
+        ddp.zero_grad()
+        train.report({"step": step})
+
+
+def test_rank_failure_mid_backward_fails_fast_world8(tmp_path, monkeypatch):
+    from gke_ray_train_amd import runtime as rt
+    from gke_ray_train_amd.runtime.errors import TrainingFailedError
+    from gke_ray_train_amd.train import RunConfig, ScalingConfig, TorchTrainer
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    rt.init(num_cpus=WORLD, num_gpus=0, ignore_reinit_error=True)
+    try:
+        trainer = TorchTrainer(_fail_loop, scaling_config=ScalingConfig(num_workers=WORLD),
+                               run_config=RunConfig(storage_path=str(tmp_path)))
+        t0 = time.time()
+        with pytest.raises(TrainingFailedError) as ei:
+            trainer.fit()
+        dt = time.time() - t0
+    finally:
+        rt.shutdown()
+    assert "exploded" in str(ei.value.__cause__) or "exploded" in str(ei.value)
+    # the seven peers blocked in the all-reduce are torn down, not left to the 1800 s PG timeout
+    assert dt < 120, f"fit() took {dt:.0f} s to fail"
+
+
+def test_bench_gpus8_cpu_through_trainer(tmp_path):
+    """``python bench.py --gpus 8`` (the driver's N=8 line without torchrun): 8 TorchTrainer
+    workers, ZeRO by default at world 8, one JSON line with the whole-job value."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(WORLD), "--steps", "2", "--warmup", "1",
+           "--model", "llama-tiny-gqa", "--device", "cpu", "--seq", "64", "--batch", "2"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    env["GRT_GLOO_TENSOR_COLLECTIVES"] = "1"
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == WORLD and out["pg_world_size"] == WORLD and out["pg_backend"] == "gloo"
+    assert out["config"]["parallelism"] == f"dp{WORLD}+zero1"
+    assert out["config"]["global_batch"] == 2 * WORLD
+    assert abs(out["value"] - 2 * WORLD * 64 / (out["ms_per_step"] / 1e3)) / out["value"] < 0.02
+
+
+def test_sft_full_ft_world8_zero_checkpoint_layout(tmp_path, monkeypatch):
+    """SFTTrainer full fine-tune at world 8 runs the ZeRO branch: every rank writes its optimizer
+    shard, nothing is written under the HF full-state name, the layout is recorded, and a resume
+    at another world size is refused with a clear error."""
+    sys.path.insert(0, os.path.join(ROOT, "jobs"))
+    import fine_tune_llama_ray as job
+    from gke_ray_train_amd import runtime as rt
+    monkeypatch.setenv("GRT_STORAGE_PATH", str(tmp_path / "ray_results"))
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    over = {"MODEL_ID": "llama-tiny-gqa", "OUTPUT_DIR_BASE": str(tmp_path / "out"), "MAX_SEQ_LENGTH": 64,
+            "USE_QLORA": False, "INFERENCE": False, "NUM_TRAIN_SAMPLES": 64, "NUM_EVAL_SAMPLES": 8,
+            "LOGGING_STEPS": 1, "SAVE_STEPS_SFT": 2, "EVAL_STEPS_SFT": 100, "GRADIENT_ACCUMULATION_STEPS": 1,
+            "PER_DEVICE_TRAIN_BATCH_SIZE": 2, "NUM_TRAIN_EPOCHS": 1}
+    rt.init(num_cpus=WORLD, num_gpus=0, ignore_reinit_error=True)
+    try:
+        job.main(job.load_config(overrides=over), num_workers=WORLD, use_gpu=False)
+    finally:
+        rt.shutdown()
+    sft = tmp_path / "out" / "sft_model_output_sql_gretel"
+    ck = sorted((d for d in os.listdir(sft) if d.startswith("checkpoint-")), key=lambda d: int(d.split("-")[1]))
+    assert ck, os.listdir(sft)
+    d = sft / ck[0]
+    files = set(os.listdir(d))
+    assert {f"optimizer_rank{r}.pt" for r in range(WORLD)} <= files, files
+    assert "optimizer.pt" not in files
+    st = json.load(open(d / "trainer_state.json"))
+    assert st["grt_optimizer_layout"] == {"zero": True, "world": WORLD}
+    # shards are 1/world each (of the padded flat state)
+    sizes = [sum(v["exp_avg"].numel() for v in torch.load(d / f"optimizer_rank{r}.pt", weights_only=True)["state"].values())
+             for r in range(WORLD)]
+    assert len(set(sizes)) == 1 and sizes[0] > 0
+    # resume in one process (no ZeRO): refused up front, not an "adamw size mismatch" later
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32)
+    tr = SFTTrainer(m, SFTConfig(output_dir=str(tmp_path / "r"), per_device_train_batch_size=2, max_steps=4,
+                                 logging_steps=1, save_steps=100), train_dataset=[{"text": "hello world " * 5}] * 16)
+    with pytest.raises(ValueError, match="ZeRO-sharded"):
+        tr.train(resume_from_checkpoint=str(d))
