@@ -35,6 +35,7 @@
 #include "grt_common.h"
 #include "grt_kernels.h"
 
+#include <algorithm>
 #include <type_traits>
 #include <utility>
 
@@ -48,21 +49,52 @@ constexpr int BUFB = 2 * TEN;    // A + B of one K-tile
 constexpr int LDSB = 2 * BUFB;   // two K-tile buffers = 133,120 B
 constexpr int kGroupRows = 8;
 
-// MFMA with the accumulator pinned to AGPRs; the compiler does not model the asm, every
-// accumulator is next touched >= 56 MFMAs later, and the epilogue pads the final hazard.
-__device__ __forceinline__ void mfma16(f32x4& c, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+// The 8 x 8 accumulator blocks live in LITERAL AGPRs: block (i, j) = a[4 (8 i + j) .. +3]. One
+// statement at kernel entry declares all 256 AGPRs clobbered, which makes the kernel descriptor
+// allocate them; the compiler's own values need ~140 arch VGPRs, so it never allocates, copies or
+// spills into the AGPR file (checked: no v_accvgpr_* outside these statements in the .s;
+// cdna_hip_programming.md §5.7 item 4). The MFMA statements themselves list no clobbers: with them
+// hipcc pads an s_nop between every two consecutive statements. ZERO: the first K-tile of an output
+// tile starts from the inline constant 0.
+#define GRT_ACC_CLOBBERS "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47", "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63", "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79", "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95", "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", "a111", "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127", "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143", "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159", "a160", "a161", "a162", "a163", "a164", "a165", "a166", "a167", "a168", "a169", "a170", "a171", "a172", "a173", "a174", "a175", "a176", "a177", "a178", "a179", "a180", "a181", "a182", "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191", "a192", "a193", "a194", "a195", "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207", "a208", "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", "a222", "a223", "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", "a235", "a236", "a237", "a238", "a239", "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", "a248", "a249", "a250", "a251", "a252", "a253", "a254", "a255"
+template <int N, bool ZERO>
+__device__ __forceinline__ void mfma_acc(const bf16x8& a, const bf16x8& b) {
+  if constexpr (ZERO)
+    asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, 0" :: "v"(a), "v"(b), "i"(N), "i"(N + 3) : GRT_ACC_CLOBBERS);
+  else
+    asm volatile("v_mfma_f32_16x16x32_bf16 a[%c2:%c3], %0, %1, a[%c2:%c3]" :: "v"(a), "v"(b), "i"(N), "i"(N + 3) : GRT_ACC_CLOBBERS);
+}
+// MFMA + the LDS-DMA that rides behind it in ONE statement (the compiler pads an s_nop between an
+// MFMA and any following inline asm, as it cannot see what the asm reads; the DMA reads no MFMA
+// result). M0 = wave base + OFF is written first; the MFMA between the write and the DMA is the
+// M0 -> LDS-DMA wait state. SCC is declared clobbered (s_add), so the compiler never schedules the
+// statement between its own s_cmp / s_cselect or s_add / s_addc pairs.
+template <int N, bool ZERO, int OFF>
+__device__ __forceinline__ void mfma_acc_dma(const bf16x8& a, const bf16x8& b, uint32_t voff,
+                                             __amdgpu_buffer_rsrc_t rsrc, uint32_t soff, uint32_t mbase) {
+  if constexpr (ZERO)
+    asm volatile("s_add_u32 m0, %5, %6\n\tv_mfma_f32_16x16x32_bf16 a[%c7:%c8], %0, %1, 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds"
+                 :: "v"(a), "v"(b), "v"(voff), "s"(rsrc), "s"(soff), "s"(mbase), "i"(OFF), "i"(N), "i"(N + 3)
+                 : "memory", "m0", "scc");
+  else
+    asm volatile("s_add_u32 m0, %5, %6\n\tv_mfma_f32_16x16x32_bf16 a[%c7:%c8], %0, %1, a[%c7:%c8]\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds"
+                 :: "v"(a), "v"(b), "v"(voff), "s"(rsrc), "s"(soff), "s"(mbase), "i"(OFF), "i"(N), "i"(N + 3)
+                 : "memory", "m0", "scc");
+}
+// accumulator block at a[N .. N+3] -> VGPRs (after the MFMA -> VALU-read pad)
+template <int N>
+__device__ __forceinline__ f32x4 acc_read() {
+  float x0, x1, x2, x3;
+  asm volatile("v_accvgpr_read_b32 %0, a%c4\n\tv_accvgpr_read_b32 %1, a%c5\n\tv_accvgpr_read_b32 %2, a%c6\n\tv_accvgpr_read_b32 %3, a%c7"
+               : "=v"(x0), "=v"(x1), "=v"(x2), "=v"(x3) : "i"(N), "i"(N + 1), "i"(N + 2), "i"(N + 3));
+  return f32x4{x0, x1, x2, x3};
 }
 
-// LDS-DMA of 16 B per lane to M0 + 16 * lane; M0 = wave base + OFF. Inline asm so the compiler
-// neither counts it (its waitcnt pass would drain vmcnt) nor keeps M0 (declared clobbered: nothing
-// else in this kernel uses it). M0 is set by s_mov from an SGPR the compiler computed: an s_add in
-// the asm would clobber SCC behind the compiler's back (it schedules these statements between its
-// own s_cmp / s_cselect and s_add / s_addc pairs).
+// prologue DMA (no MFMA to hide the M0 -> LDS-DMA wait state behind: explicit s_nop)
 template <int OFF>
 __device__ __forceinline__ void dma(uint32_t voff, __amdgpu_buffer_rsrc_t rsrc, uint32_t soff, uint32_t mbase) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
-               :: "v"(voff), "s"(rsrc), "s"(mbase + OFF), "s"(soff) : "memory", "m0");
+  asm volatile("s_add_u32 m0, %2, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+               :: "v"(voff), "s"(rsrc), "s"(mbase), "s"(soff), "i"(OFF) : "memory", "m0", "scc");
 }
 
 __device__ __forceinline__ uint32_t lds_u32(const void* p) {
@@ -79,14 +111,18 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // ---- per-period schedule: what rides behind MFMA number I (0..127) --------------------------
-// seg 1: A kk1 reads; seg 2: B kk1 reads + A DMAs 0-4; seg 3: A DMAs 5-7, B DMAs 0-4;
-// seg 4: kk0 reads of the next tile (B0[0], A0[0], B0[1..7], A0[1..7]) + B DMAs 5-7
+// seg 1 (0-21): A kk1 reads -> lgkmcnt(0), barrier 1
+// seg 2 (22-47): B kk1 reads + A DMAs 0-3 -> lgkmcnt(0), barrier 2
+// seg 3 (48-79): A DMAs 4-7, B DMAs 0-3 -> vmcnt(12), barrier 3
+// seg 4 (80-127): kk0 reads of the next tile (B0[0], A0[0], B0[1..7], A0[1..7]) at 80..110, B DMAs 4-7
+// (the last read lands >= 17 MFMAs before the next period's first MFMA)
 constexpr int kReadA1[8] = {0, 2, 5, 8, 11, 13, 16, 18};
-constexpr int kReadB1[8] = {22, 25, 28, 31, 34, 37, 40, 43};
-constexpr int kDmaA[8] = {23, 29, 35, 41, 47, 53, 58, 63};
-constexpr int kDmaB[8] = {68, 73, 78, 83, 88, 98, 108, 118};
-constexpr int kRead0First = 93;  // 16 reads at 93, 95, ..., 123
-constexpr int kBar1 = 21, kBar2 = 51, kBar3 = 92;
+constexpr int kReadB1[8] = {22, 24, 27, 30, 33, 36, 39, 42};
+constexpr int kDmaA[8] = {23, 29, 35, 41, 49, 53, 57, 61};
+constexpr int kDmaB[8] = {65, 69, 73, 77, 85, 95, 105, 115};
+constexpr int kRead0First = 80;  // 16 reads at 80, 82, ..., 110
+constexpr int kBar1 = 21, kBar2 = 47, kBar3 = 79;
+constexpr int kDmaBeforeBar3 = 12;
 
 constexpr int find8(const int (&t)[8], int i) {
   for (int q = 0; q < 8; ++q)
@@ -94,28 +130,42 @@ constexpr int find8(const int (&t)[8], int i) {
   return -1;
 }
 
-template <int EPI, int DBG>
+// PERSIST: grid = min(#tiles, #CUs); workgroup b takes the tiles of rounds k = 0, 1, ... (tile
+// round_base + remap(b) of round k, round_base = k * G). The K pipeline runs straight across output
+// tiles: the last two periods of a tile DMA the first two K-tiles of the workgroup's next tile, and
+// the last period's kk0 reads are already that tile's first fragments, so between tiles only the
+// epilogue remains (no prologue, no pipeline drain). Without PERSIST the grid is one workgroup per
+// tile (A/B reference).
+template <int EPI, bool PERSIST>
 __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 1, wc = w & 1;
+  const int nM = p.M / 256, nN = p.N / 256, ntiles = nM * nN;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int T = p.K / KT;  // even, >= 2 (host check)
 
-  // ---- tile coordinates: bijective XCD remap, then grouped order
-  const int nM = p.M / 256, nN = p.N / 256, nwg = nM * nN;
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int per_group = kGroupRows * nN;
-  const int grp = wg / per_group, first = grp * kGroupRows;
-  const int gsize = min(nM - first, kGroupRows);
-  const int tm = first + (wg % per_group) % gsize, tn = (wg % per_group) / gsize;
-  GRT_DEVICE_CHECK(tm < nM && tn < nN);
-  const int m0 = tm * 256, n0 = tn * 256;
-  const int T = p.K / KT;
+  // this workgroup's tile of round k, or -1 when the round has no tile for it
+  auto tile_of = [&](int k, int& tm, int& tn) __attribute__((always_inline)) -> bool {
+    const int base = k * G;
+    if (base >= ntiles) return false;
+    const int nr = min(G, ntiles - base);
+    const int r = xcd_remap(b, G);
+    if (r >= nr) return false;
+    const int lin = base + r;
+    const int per_group = kGroupRows * nN;
+    const int grp = lin / per_group, first = grp * kGroupRows;
+    const int gsize = min(nM - first, kGroupRows);
+    // wave-uniform by construction; readfirstlane makes it provable (the descriptors built from
+    // it must sit in SGPRs)
+    tm = __builtin_amdgcn_readfirstlane(first + (lin % per_group) % gsize);
+    tn = __builtin_amdgcn_readfirstlane((lin % per_group) / gsize);
+    return true;
+  };
 
   // ---- DMA addressing: wave w, instruction q fills chunk 4q + w: lane l carries row
   // 128 (q >> 2) + 16 (l >> 3) + 4 (q & 3) + w, k-chunk l & 7
-  const char* abase = static_cast<const char*>(p.a) + ((int64_t)m0 * p.lda) * 2;
-  const char* bbase = static_cast<const char*>(p.b) + ((int64_t)n0 * p.ldb) * 2;
   const uint32_t avoff = (uint32_t)(((16 * (lane >> 3) + w) * p.lda + 8 * (lane & 7)) * 2);
   const uint32_t bvoff = (uint32_t)(((16 * (lane >> 3) + w) * p.ldb + 8 * (lane & 7)) * 2);
   const uint32_t lda2 = (uint32_t)p.lda * 2, ldb2 = (uint32_t)p.ldb * 2;
@@ -126,101 +176,68 @@ __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
     sob[q] = (uint32_t)(128 * (q >> 2) + 4 * (q & 3)) * ldb2;
   }
   const uint32_t mbase = __builtin_amdgcn_readfirstlane(lds_u32(smem) + w * CH);
-  auto rsrc = [](const char* base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), 0, 0x7fffffff, 0x00020000);
+  auto rsrc = [](const char* base, int num) __attribute__((always_inline)) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), 0, num, 0x00020000);
   };
+  // 32-bit offsets (host check: every operand below 2 GiB) keep the address math on the SALU, so
+  // the descriptors built from it are SGPR values (the asm "s" operands)
+  auto a_tile = [&](int tm) __attribute__((always_inline)) { return static_cast<const char*>(p.a) + (uint32_t)(tm * 256) * lda2; };
+  auto b_tile = [&](int tn) __attribute__((always_inline)) { return static_cast<const char*>(p.b) + (uint32_t)(tn * 256) * ldb2; };
 
   // ---- fragment addressing: lane l reads row (l & 15) of a 16-row block, k-chunk (l >> 4) (+4 kk)
   const int lf = (lane & 15) * CH + (lane >> 4) * 16;
   const char* fa[2] = {smem + 0 * BUFB + 16 * wr * CH + lf, smem + 1 * BUFB + 16 * wr * CH + lf};
   const char* fb[2] = {smem + 0 * BUFB + TEN + 16 * wc * CH + lf, smem + 1 * BUFB + TEN + 16 * wc * CH + lf};
-  auto frag = [](const char* base, int blk, int kk) -> bf16x8 {
+  auto frag = [](const char* base, int blk, int kk) __attribute__((always_inline)) -> bf16x8 {
     return *reinterpret_cast<const bf16x8*>(base + blk * 128 + kk * 64);
   };
 
-  // accumulators zeroed by the matrix pipe itself (MFMA with an inline-constant 0 accumulator and
-  // zero operands): no VALU-write -> MFMA-read hazard, and the compiler sees each one defined by an
-  // asm statement, so it neither re-materialises nor copies them
-  f32x4 acc[8][8];
-  {
-    const bf16x8 zf = {};
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %1, 0" : "=a"(acc[i][j]) : "v"(zf));
-  }
+  int tm, tn;
+  if (!tile_of(0, tm, tn)) return;  // whole workgroup: uniform
+  asm volatile("" ::: GRT_ACC_CLOBBERS);  // allocates the AGPR file (see mfma_acc)
   bf16x8 a0[8], a1[8], b0[8], b1[8];
 
-  // ---- prologue: tiles 0 and 1 in flight (32 DMAs), kk0 of tile 0 into registers
+  // ---- prologue (once per workgroup): K-tiles 0 and 1 of the first tile in flight, kk0 of K-tile 0
   {
-    const auto ra0 = rsrc(abase), rb0 = rsrc(bbase);
-    const auto ra1 = rsrc(abase + (T > 1 ? KT * 2 : 0)), rb1 = rsrc(bbase + (T > 1 ? KT * 2 : 0));
-    static_for<8>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-      dma<0 * BUFB + 0 + q * 4 * CH>(avoff, ra0, soa[q], mbase);
-    });
-    static_for<8>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-      dma<0 * BUFB + TEN + q * 4 * CH>(bvoff, rb0, sob[q], mbase);
-    });
-    static_for<8>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-      dma<1 * BUFB + 0 + q * 4 * CH>(avoff, ra1, soa[q], mbase);
-    });
-    static_for<8>([&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-      dma<1 * BUFB + TEN + q * 4 * CH>(bvoff, rb1, sob[q], mbase);
-    });
-    if constexpr (DBG & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    const auto ra = rsrc(a_tile(tm), 0x7fffffff), rb = rsrc(b_tile(tn), 0x7fffffff);
+    const auto ra1 = rsrc(a_tile(tm) + KT * 2, 0x7fffffff), rb1 = rsrc(b_tile(tn) + KT * 2, 0x7fffffff);
+    static_for<8>([&](auto Q) __attribute__((always_inline)) { dma<0 * BUFB + 0 + decltype(Q)::value * 4 * CH>(avoff, ra, soa[decltype(Q)::value], mbase); });
+    static_for<8>([&](auto Q) __attribute__((always_inline)) { dma<0 * BUFB + TEN + decltype(Q)::value * 4 * CH>(bvoff, rb, sob[decltype(Q)::value], mbase); });
+    static_for<8>([&](auto Q) __attribute__((always_inline)) { dma<1 * BUFB + 0 + decltype(Q)::value * 4 * CH>(avoff, ra1, soa[decltype(Q)::value], mbase); });
+    static_for<8>([&](auto Q) __attribute__((always_inline)) { dma<1 * BUFB + TEN + decltype(Q)::value * 4 * CH>(bvoff, rb1, sob[decltype(Q)::value], mbase); });
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { b0[j] = frag(fb[0], j, 0); a0[j] = frag(fa[0], j, 0); }
-    if constexpr (DBG & 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-    if constexpr (DBG & 64) {  // debug: wave 0's first A / B fragments and the tile-0 MFMA of block (0,0)
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      if (w == 0) {
-        reinterpret_cast<bf16x8*>(p.c)[lane] = a0[0];
-        reinterpret_cast<bf16x8*>(p.c)[64 + lane] = b0[0];
-        f32x4 z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[0], a0[0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        reinterpret_cast<f32x4*>(p.c)[128 + lane] = z;
-      }
-      return;
-    }
-    if constexpr (DBG & 4) {  // debug: dump buffer 0 (A and B images of tile 0) to C and stop
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      for (int x = tid; x < BUFB / 16; x += 256)
-        reinterpret_cast<uint4*>(p.c)[x] = reinterpret_cast<const uint4*>(smem)[x];
-      return;
-    }
   }
 
-  // ---- one K-tile period on buffer U (compile-time) for tile t
-  auto period = [&](int t, auto U_) {
+  // ---- one K-tile period on buffer U (compile-time); FIRST: K-tile 0 of an output tile (its kk0
+  // MFMAs start the accumulators at 0). ra / rb: the DMA source of this period (K-tile t+2 of this
+  // tile, or K-tile t+2-T of the next one, or nothing)
+  auto period = [&](auto U_, auto FIRST_, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb) __attribute__((always_inline)) {
     constexpr int U = decltype(U_)::value;
-    const int td = min(t + 2, T - 1);  // tile whose DMAs ride in this period
-    const auto ra = rsrc(abase + (int64_t)td * (KT * 2));
-    const auto rb = rsrc(bbase + (int64_t)td * (KT * 2));
-    static_for<128>([&](auto I_) {
+    constexpr bool ZERO = decltype(FIRST_)::value && (true);
+    static_for<128>([&](auto I_) __attribute__((always_inline)) {
       constexpr int I = decltype(I_)::value;
       constexpr int kk = I / 64, i = (I % 64) / 8, j = I % 8;
-      if constexpr (DBG & 2) {
-        if constexpr (kk == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j], a0[i], acc[i][j], 0, 0, 0);
-        else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0);
-      } else {
-        if constexpr (kk == 0) mfma16(acc[i][j], b0[j], a0[i]);
-        else mfma16(acc[i][j], b1[j], a1[i]);
-      }
       constexpr int ra1q = find8(kReadA1, I), rb1q = find8(kReadB1, I);
       constexpr int dAq = find8(kDmaA, I), dBq = find8(kDmaB, I);
+      constexpr uint32_t m0off = dAq >= 0 ? U * BUFB + 0 + dAq * 4 * CH : U * BUFB + TEN + (dBq >= 0 ? dBq : 0) * 4 * CH;
+      bf16x8& af = kk == 0 ? a0[i] : a1[i];
+      bf16x8& bfr = kk == 0 ? b0[j] : b1[j];
+      if constexpr (dAq >= 0 || dBq >= 0) {
+        constexpr int q = dAq >= 0 ? dAq : dBq;
+        const uint32_t vo = dAq >= 0 ? avoff : bvoff;
+        const uint32_t so = dAq >= 0 ? soa[q] : sob[q];
+        const auto rs = dAq >= 0 ? ra : rb;
+        mfma_acc_dma<4 * (8 * i + j), ZERO && kk == 0, m0off>(bfr, af, vo, rs, so, mbase);
+      } else {
+        mfma_acc<4 * (8 * i + j), ZERO && kk == 0>(bfr, af);
+      }
       if constexpr (ra1q >= 0) a1[ra1q] = frag(fa[U], ra1q, 1);
       if constexpr (rb1q >= 0) b1[rb1q] = frag(fb[U], rb1q, 1);
-      if constexpr (dAq >= 0) dma<U * BUFB + 0 + dAq * 4 * CH>(avoff, ra, soa[dAq], mbase);
-      if constexpr (dBq >= 0) dma<U * BUFB + TEN + dBq * 4 * CH>(bvoff, rb, sob[dBq], mbase);
       if constexpr (I >= kRead0First && I < kRead0First + 32 && (I - kRead0First) % 2 == 0) {
         constexpr int x = (I - kRead0First) / 2;  // 0: B0[0], 1: A0[0], 2..8: B0[1..7], 9..15: A0[1..7]
         if constexpr (x == 0) b0[0] = frag(fb[U ^ 1], 0, 0);
@@ -233,73 +250,93 @@ __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
       if constexpr (I == kBar3) {
+        static_assert(kDmaBeforeBar3 == 12, "vmcnt below");
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(13)\n\ts_barrier" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
       }
       __builtin_amdgcn_sched_barrier(0);
     });
   };
   using Z = std::integral_constant<int, 0>;
   using O = std::integral_constant<int, 1>;
-  if constexpr (DBG & 16) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_nop 15" ::: "memory");
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) mfma16(acc[i][j], b0[j], a0[i]);
-  } else {
-    if constexpr (DBG & 32) asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-    int t = 0;
-    do {  // T >= 2 (host check): no zero-trip path, so no phi copies of the accumulators at the exit
-      period(t, Z{});
-      period(t + 1, O{});
-      t += 2;
-    } while (t < T);
-  }
-  // the last MFMAs' results are read by VALU below: 3 x 8 wait states (8-pass XDL write -> VALU
-  // read), then an empty asm "redefines" every accumulator so no read is hoisted above the pad
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(acc[i][j]));
-  __builtin_amdgcn_sched_barrier(0);
-  if constexpr (DBG & 128) {  // debug: raw fp32 accumulators of block (0,0) and (7,7) of wave 0
-    asm volatile("s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (w == 0) {
-      reinterpret_cast<f32x4*>(p.c)[lane] = acc[0][0];
-      reinterpret_cast<f32x4*>(p.c)[64 + lane] = acc[7][7];
-    }
-    return;
-  }
+  using Fy = std::integral_constant<bool, true>;
+  using Fn = std::integral_constant<bool, false>;
 
-  // ---- epilogue: lane holds C[m][n .. n+3], m = m0 + 128 wr + 16 i + (lane & 15),
-  // n = n0 + 128 wc + 16 j + 4 (lane >> 4)
-  bf16* cbase = static_cast<bf16*>(p.c) + (int64_t)(m0 + 128 * wr + (lane & 15)) * p.ldc + n0 + 128 * wc + 4 * (lane >> 4);
-  auto store_row = [&](int i, bool accumulate) {
-    bf16* crow = cbase + (int64_t)16 * i * p.ldc;
-    bf16x4 old[8];
-    if (accumulate) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) old[j] = *reinterpret_cast<const bf16x4*>(crow + 16 * j);
+  const int r = lane & 15, g = lane >> 4;
+  const int cofs = ((g & 1) ? 16 : 0) + ((g & 2) ? 8 : 0);
+  for (int k = 0;; ++k) {
+    // next tile of this workgroup (DMA target of the last two periods)
+    int ntm = 0, ntn = 0;
+    const bool has_next = __builtin_amdgcn_readfirstlane((PERSIST && tile_of(k + 1, ntm, ntn)) ? 1 : 0) != 0;
+    const char* abase = a_tile(tm);
+    const char* bbase = b_tile(tn);
+    const char* anext = a_tile(has_next ? ntm : tm);
+    const char* bnext = b_tile(has_next ? ntn : tn);
+    auto src = [&](int t, const char* cur, const char* nxt) __attribute__((always_inline)) {
+      // K-tile t + 2 of this tile, else K-tile t + 2 - T of the next tile, else no records
+      // (selects, not branches: one descriptor either way)
+      const bool here = t + 2 < T;
+      const char* base = here ? cur + (uint32_t)(t + 2) * (KT * 2) : nxt + (uint32_t)(t + 2 - T) * (KT * 2);
+      return rsrc(base, (here || has_next) ? 0x7fffffff : 0);
+    };
+    period(Z{}, Fy{}, src(0, abase, anext), src(0, bbase, bnext));
+    period(O{}, Fn{}, src(1, abase, anext), src(1, bbase, bnext));
+    for (int t = 2; t < T; t += 2) {
+      period(Z{}, Fn{}, src(t, abase, anext), src(t, bbase, bnext));
+      period(O{}, Fn{}, src(t + 1, abase, anext), src(t + 1, bbase, bnext));
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      bf16x4 r;
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        r[e] = static_cast<bf16>(accumulate ? acc[i][j][e] + static_cast<float>(old[j][e]) : acc[i][j][e]);
-      *reinterpret_cast<bf16x4*>(crow + 16 * j) = r;
-    }
-  };
-  if (p.beta) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) store_row(i, true);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) store_row(i, false);
+    // ---- epilogue. The last MFMAs' results are read by VALU: 3 x 8 wait states (8-pass XDL
+    // write -> VALU read), then an empty asm redefines every accumulator so no read is hoisted
+    // above the pad. Lane (r, g) holds C[m][n .. n+3] of block (i, j), m = m0 + 128 wr + 16 i + r,
+    // n = n0 + 128 wc + 16 j + 4 g; for a block pair (j, j+1) one v_permlane16_swap per dword (odd
+    // 16-lane rows of the first operand <-> even rows of the second) leaves each lane 8 consecutive
+    // columns: g = 0 block j cols 0-7, g = 1 block j+1 cols 0-7, g = 2 block j cols 8-15, g = 3
+    // block j+1 cols 8-15 -> one 16-B store per lane and pair (T21). The stores join the vmcnt
+    // stream; the next tile's barrier-3 vmcnt(12) simply also covers them.
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    bf16* cbase = static_cast<bf16*>(p.c) + (int64_t)(tm * 256 + 128 * wr + r) * p.ldc + tn * 256 + 128 * wc + cofs;
+    auto pack2 = [](float a_, float b_) __attribute__((always_inline)) -> uint32_t {
+      const bf16x2 v = {static_cast<bf16>(a_), static_cast<bf16>(b_)};
+      return __builtin_bit_cast(uint32_t, v);
+    };
+    auto swap = [](f32x4& x, f32x4& y, auto E_) __attribute__((always_inline)) {
+      constexpr int e = decltype(E_)::value;
+      const auto v = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[e]), __float_as_uint(y[e]), false, false);
+      x[e] = __uint_as_float(v[0]);
+      y[e] = __uint_as_float(v[1]);
+    };
+    auto store_pair = [&](auto I_, auto JP_, bool accumulate) __attribute__((always_inline)) {
+      constexpr int i = decltype(I_)::value, jp = decltype(JP_)::value;
+      bf16* crow = cbase + (int64_t)16 * i * p.ldc + 32 * jp;
+      f32x4 x = acc_read<4 * (8 * i + 2 * jp)>(), y = acc_read<4 * (8 * i + 2 * jp + 1)>();
+      if (accumulate) {
+        static_for<4>([&](auto E_) __attribute__((always_inline)) { swap(x, y, E_); });
+        const bf16x8 old = *reinterpret_cast<const bf16x8*>(crow);
+        uint4 o;
+        o.x = pack2(x[0] + (float)old[0], x[1] + (float)old[1]);
+        o.y = pack2(x[2] + (float)old[2], x[3] + (float)old[3]);
+        o.z = pack2(y[0] + (float)old[4], y[1] + (float)old[5]);
+        o.w = pack2(y[2] + (float)old[6], y[3] + (float)old[7]);
+        *reinterpret_cast<uint4*>(crow) = o;
+      } else {
+        const uint32_t x0 = pack2(x[0], x[1]), x1 = pack2(x[2], x[3]);
+        const uint32_t y0 = pack2(y[0], y[1]), y1 = pack2(y[2], y[3]);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(x0, y0, false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(x1, y1, false, false);
+        *reinterpret_cast<uint4*>(crow) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+      }
+    };
+    auto store_rows = [&](bool accumulate) __attribute__((always_inline)) {
+      static_for<8>([&](auto I_) __attribute__((always_inline)) { static_for<4>([&](auto JP_) __attribute__((always_inline)) { store_pair(I_, JP_, accumulate); }); });
+    };
+    if (p.beta) store_rows(true);
+    else store_rows(false);
+    if (!has_next) break;
+    tm = ntm;
+    tn = ntn;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA outstanding at exit
 }
 
 }  // namespace
@@ -312,18 +349,25 @@ bool gemm_nt_k64_supported(int64_t M, int64_t N, int64_t K, int64_t lda, int64_t
   return true;
 }
 
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess) n = prop.multiProcessorCount;
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
 void gemm_nt_k64(const GemmParams& p, hipStream_t stream) {
-  const int nwg = (p.M / 256) * (p.N / 256);
-  if (p.variant == 10) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 1>), dim3(nwg), dim3(256), 0, stream, p);
-  else if (p.variant == 11) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 2>), dim3(nwg), dim3(256), 0, stream, p);
-  else if (p.variant == 12) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 3>), dim3(nwg), dim3(256), 0, stream, p);
-  else if (p.variant == 13) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 4>), dim3(nwg), dim3(256), 0, stream, p);
-  else if (p.variant == 14) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 16>), dim3(nwg), dim3(256), 0, stream, p);
-  else if (p.variant == 16) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 64>), dim3(nwg), dim3(256), 0, stream, p);
-  else if (p.variant == 17) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 128>), dim3(nwg), dim3(256), 0, stream, p);
-  else if (p.variant == 18) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 130>), dim3(nwg), dim3(256), 0, stream, p);
-  else if (p.variant == 15) hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 32>), dim3(nwg), dim3(256), 0, stream, p);
-  else hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, 0>), dim3(nwg), dim3(256), 0, stream, p);
+  const int ntiles = (p.M / 256) * (p.N / 256);
+  if (p.variant == 10) {  // one workgroup per tile (A/B reference)
+    hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, false>), dim3(ntiles), dim3(256), 0, stream, p);
+  } else {
+    const int G = std::min(ntiles, num_cus());
+    hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, true>), dim3(G), dim3(256), 0, stream, p);
+  }
 }
 
 }  // namespace grt

@@ -629,7 +629,7 @@ void gemm_nt(const GemmParams& p, hipStream_t stream) {
   const int nwg = (p.M / GT) * (p.N / GT);
   const dim3 grid(nwg), block(GNT);
   const int variant = p.variant;
-  if (variant >= 9 && variant <= 18 && gemm_nt_k64_supported(p.M, p.N, p.K, p.lda, p.ldb)) {
+  if ((variant == 9 || variant == 10) && gemm_nt_k64_supported(p.M, p.N, p.K, p.lda, p.ldb)) {
     gemm_nt_k64(p, stream);
   } else if (variant == 4 || variant == 5) {
     if (variant == 4) hipLaunchKernelGGL((gemm_nt_w4_kernel<4, true>), grid, dim3(256), 0, stream, p);

@@ -481,7 +481,7 @@ def _coordinator_main(payload: bytes, n: int, equal: bool, authkey: bytes, conn_
         os._exit(0)
     threading.Thread(target=watchdog, daemon=True, name="grt-split-watchdog").start()
     ds = cloudpickle.loads(payload)
-    listener = Listener(("127.0.0.1", 0), authkey=authkey)
+    listener = Listener(("127.0.0.1", 0), authkey=authkey, backlog=128)  # many consumers connect at once
     conn_back.send(listener.address)
     conn_back.close()
     _CoordinatorState(ds, n, equal).serve(listener)

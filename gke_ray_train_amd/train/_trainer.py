@@ -155,7 +155,10 @@ class DataParallelTrainer:
         n = self.scaling.num_workers
         use_gpu = self.scaling.use_gpu
         authkey = secrets.token_bytes(16)
-        listener = Listener(("127.0.0.1", 0), authkey=authkey)
+        # backlog >= workers: with the default of 1, simultaneous connects beyond the first are
+        # dropped by the kernel and retried with SYN back-off (1, 2, 4 ... s); at 8 workers a rank
+        # could sit in back-off for minutes (tests/test_world8_cpu.py)
+        listener = Listener(("127.0.0.1", 0), authkey=authkey, backlog=max(64, 2 * n))
         address = listener.address
         master_port = _free_port()
         backend = self._backend()
