@@ -254,8 +254,12 @@ class _DirectGradLinear(torch.autograd.Function):
         # dY^T written by the producing kernel (ops.fused.swiglu backward: the gate / up gradient)
         dyt = provided_transposed(dy2, dy) if ctx.needs_input_grad[1] else None
         if dyt is not None and not ctx.x_t:  # X was saved untransposed: its transpose now
-            x = transposed(x.reshape(-1, x.shape[-1]))
-            ctx.x_t = True
+            x2 = x.reshape(-1, x.shape[-1])
+            if _tn_wgrad_ok(x2) and w.shape[0] % 64 == 0:
+                x = transposed(x2)
+                ctx.x_t = True
+            else:  # X cannot take the TN path (dtype / shape / layout): plain weight gradient
+                dyt = None
         if ctx.x_t and dyt is None:  # X^T saved by the forward: dY^T now, while dY is fresh from its producer
             if not dy2.is_contiguous():
                 dy2 = dy2.contiguous()

@@ -198,6 +198,7 @@ class FullyShardedDataParallel(nn.Module):
         # waited for before the unit's next all-gather / forward; it also zeroes the grad shards
         self._update_events: Dict[int, torch.cuda.Event] = {}
         self._grad_zero_by_optimizer = False
+        self._grads_consumed = False  # set by an optimizer that zeroed the gradients itself (offload.py)
         self._gstream = None
 
     # ================================================================ optimizer hand-off
@@ -508,9 +509,15 @@ class FullyShardedDataParallel(nn.Module):
     def zero_grad(self, set_to_none: bool = True):
         for u in self.units:
             u.acc_started = False
-        if not self._grad_zero_by_optimizer:  # else: zeroed per unit on the update stream
+        # the overlapped offload optimizer zeroes each unit's gradients on its update stream; a
+        # zero_grad() that no step() consumed (skipped step, zero_grad at the top of a loop) must
+        # still clear them, after the pending updates (replicated params accumulate into rep_grad)
+        if not (self._grad_zero_by_optimizer and self._grads_consumed):
+            if self._grad_zero_by_optimizer:
+                self.wait_updates()
             self.grad_store.zero_()
             self.rep_grad.zero_()
+        self._grads_consumed = False
         o = 0
         for _, p in self.replicated:  # a caller may have set .grad = None: re-attach the views
             p.grad = self.rep_grad[o:o + p.numel()].view_as(p)

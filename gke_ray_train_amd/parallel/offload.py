@@ -82,6 +82,7 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         if dev.type != "cuda":
             return super().step(closure, grad_scale)
         bump_param_generation()
+        fs._grads_consumed = True  # every unit's gradients are zeroed on the update stream below
         C = _native.kernels()
         if self._streams is None:
             self._streams = tuple(torch.cuda.Stream(dev) for _ in range(3))  # up, update, down

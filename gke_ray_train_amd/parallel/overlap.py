@@ -140,6 +140,10 @@ class OverlappedOptimizer:
             return self.opt.step(grad_scale=grad_scale)
         self.synchronize()  # step t-1's chunks all done before we touch shared buffers
         work = self.opt.prepare_gpu_step()
+        # the update runs here, not through self.opt.step(): tell an LR scheduler bound to the inner
+        # optimizer that this step happened (torch's LRScheduler reads this flag; without it every
+        # scheduler.step() warns "lr_scheduler.step() before optimizer.step()")
+        self.opt._opt_called = True
         by_flat = {w[0].data_ptr(): w for w in work}
         per_group = []
         for g in groups:

@@ -17,6 +17,9 @@ from __future__ import annotations
 
 import json
 import os
+
+# kernel arguments in device memory (read by the HIP runtime at its first call; launch-time setting)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 import sys
 import time
 

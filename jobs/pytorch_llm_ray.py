@@ -19,6 +19,9 @@ import hashlib
 import json
 import math
 import os
+
+# kernel arguments in device memory (read by the HIP runtime at its first call; launch-time setting)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 import sys
 import tempfile
 import time

@@ -1070,7 +1070,7 @@ def test_kcat_lora_model_matches_epilogue_form(monkeypatch):
         ids = torch.randint(0, m.config.vocab_size, (2, 256), device=DEV, generator=torch.Generator(device=DEV).manual_seed(4))
         loss = pm(ids, labels=ids)["loss"]
         loss.backward()
-        res[kcat] = (float(loss), {n: p.grad.float().clone() for n, p in pm.named_parameters() if p.grad is not None})
+        res[kcat] = (float(loss.detach()), {n: p.grad.float().clone() for n, p in pm.named_parameters() if p.grad is not None})
         if kcat:
             assert any(lm.kcat_pad for lm in pm.lora_modules.values())
     (l1, g1), (l0, g0) = res[True], res[False]
