@@ -89,10 +89,11 @@ def parse():
                     help="--offload: per-unit update overlapped with the next forward (on) or the serial "
                          "after-backward stream (off)")
     ap.add_argument("--proxy-world", type=int, default=0,
-                    help="one-GPU rehearsal of rank 0 of an N-rank ZeRO job: buckets, optimizer shard (1/N of "
-                         "AdamW) and forward-time W^T exactly as at world N, collectives replaced by local "
-                         "copies of this rank's chunk (xGMI time excluded; loss not meaningful). Reports the "
-                         "per-rank step with n_gpus 1 and proxy_world N")
+                    help="one-GPU rehearsal of rank 0 of an N-rank job: DDP/ZeRO buckets and the 1/N optimizer "
+                         "shard, or (--parallel fsdp) 1/N parameter / gradient / optimizer shards with the full-unit "
+                         "gather buffers of world N; collectives replaced by local copies of this rank's chunk "
+                         "(xGMI time excluded; loss not meaningful). Reports the per-rank step with n_gpus 1 and "
+                         "proxy_world N")
     ap.add_argument("--layers", type=int, default=0,
                     help="rehearsal only: keep the first N decoder layers of --model (the JSON names the model "
                          "'<model>[N/L layers]', so it is never mistaken for the full model's number)")
@@ -119,7 +120,9 @@ def build(a, cfg, dev, dtype, world):
                     m.weight.fill_(1.0)
         if a.checkpointing:
             model.gradient_checkpointing_enable()
-        eng = FullyShardedDataParallel(model, param_init_fn=init, device=dev, cpu_offload=a.offload)
+        proxy = a.proxy_world > 1 and world == 1  # rank 0 of an N-rank full-shard job on one device
+        eng = FullyShardedDataParallel(model, param_init_fn=init, device=dev, cpu_offload=a.offload,
+                                       proxy_world=a.proxy_world if proxy else 0)
         opt = eng.build_optimizer(lr=a.lr, overlap=a.offload_overlap == "on",
                                   resident_fraction=getattr(a, "resident_fraction", 0.0))
         return model, eng, eng, opt

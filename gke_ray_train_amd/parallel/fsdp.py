@@ -89,6 +89,13 @@ class _Unit:
         self.slots: Dict[int, GradSlot] = {}
 
 
+class _DoneWork:
+    """Stand-in for a collective's Work in proxy mode (the local copy already ran in stream order)."""
+
+    def wait(self):
+        return None
+
+
 def partition_units(module: nn.Module, world: int, unit_types=DEFAULT_UNITS):
     """The FSDP partition: one unit per transformer block plus a root unit (embeddings, LM head)
     holding every other matrix; 1-D parameters are replicated. Allocates nothing, so it also runs
@@ -117,7 +124,8 @@ def partition_units(module: nn.Module, world: int, unit_types=DEFAULT_UNITS):
 class FullyShardedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, process_group=None, unit_types=DEFAULT_UNITS, reshard_after_forward=True,
                  cpu_offload: bool = False, sync_module_states: bool = True, param_init_fn=None, device=None,
-                 offload_chunk_elems: int = 1 << 26, force_collectives: Optional[bool] = None):
+                 offload_chunk_elems: int = 1 << 26, force_collectives: Optional[bool] = None,
+                 proxy_world: int = 0):
         super().__init__()
         self.module = module
         self.pg = process_group
@@ -125,7 +133,17 @@ class FullyShardedDataParallel(nn.Module):
         self.rank = dist.get_rank(process_group) if self.world > 1 else 0
         if force_collectives is None:
             force_collectives = os.environ.get("GRT_FORCE_COLLECTIVES", "0") == "1"
-        self.comm = self.world > 1 or (bool(force_collectives) and dist.is_initialized())
+        # proxy_world = N on ONE process (no process group): rank 0 of an N-rank job — 1/N shards of
+        # every unit, full-unit gather buffers allocated and released exactly as at world N, the
+        # AdamW (or offload) state of 1/N — with each collective replaced by the local copy of this
+        # rank's part (all-gather: own shard into its slot; reduce-scatter: own chunk of the full
+        # gradient). The step an N-GPU run executes minus the xGMI transfers (bench.py
+        # --parallel fsdp --proxy-world N; every slot of a gathered unit holds a copy of this rank's
+        # shard, so the loss is not meaningful). Mirrors parallel/ddp.py's proxy mode.
+        self.proxy = int(proxy_world) > 1 and self.world == 1
+        if self.proxy:
+            self.world, self.rank = int(proxy_world), 0
+        self.comm = self.proxy or self.world > 1 or (bool(force_collectives) and dist.is_initialized())
         self._pool: Dict[int, List[torch.Tensor]] = {}
         self._rs_inflight = collections.deque()
         self._rs_cap = max(1, int(os.environ.get("GRT_FSDP_RS_INFLIGHT", "2")))
@@ -134,7 +152,7 @@ class FullyShardedDataParallel(nn.Module):
         self.offload_chunk = offload_chunk_elems
         self._sync = True
         # GRT_GLOO_TENSOR_COLLECTIVES=1: run the RCCL code path over gloo (CPU tests), see ddp.py
-        self.gloo = (self.comm and dist.get_backend(process_group) == "gloo"
+        self.gloo = (self.comm and not self.proxy and dist.get_backend(process_group) == "gloo"
                      and os.environ.get("GRT_GLOO_TENSOR_COLLECTIVES", "0") != "1")
         first = next(module.parameters())
         self.device = torch.device(device) if device is not None else (
@@ -180,7 +198,7 @@ class FullyShardedDataParallel(nn.Module):
                 p.data = self.rep_flat[o:o + p.numel()].view_as(p)
                 p.grad = self.rep_grad[o:o + p.numel()].view_as(p)
                 o += p.numel()
-        if sync_module_states and self.world > 1 and rn:
+        if sync_module_states and self.world > 1 and rn and not self.proxy:
             dist.broadcast(self.rep_flat, 0, group=process_group)
         self._rep_hooks = [p.register_post_accumulate_grad_hook(self._rep_hook) for _, p in self.replicated]
         self._rep_fresh = True
@@ -242,7 +260,7 @@ class FullyShardedDataParallel(nn.Module):
         full = torch.zeros(u.total, dtype=self.dtype, device=self.device)
         for p, o, n in zip(u.params, u.offsets, u.numels):
             full[o:o + n].copy_(p.data.reshape(-1))
-        if sync and self.world > 1:
+        if sync and self.world > 1 and not self.proxy:
             dist.broadcast(full, 0, group=self.pg)
         u.shard.copy_(full[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel])
         if not self.comm:
@@ -299,7 +317,12 @@ class FullyShardedDataParallel(nn.Module):
         u._pending_buf = buf
 
     def _gather_into(self, u: _Unit, buf):
-        if self.gloo:
+        if self.proxy:  # stand-in for the all-gather: this rank's shard into EVERY slot (one local
+            # copy of the full unit; the other ranks' slots must hold real-magnitude weights, not
+            # zeros: zero operands would let the GEMMs clock higher and flatter the proxy timing)
+            buf.view(self.world, u.shard_numel).copy_(u.shard.unsqueeze(0).expand(self.world, -1))
+            u.gather_work = _DoneWork()
+        elif self.gloo:
             parts = list(buf.chunk(self.world))
             u.gather_work = dist.all_gather(parts, u.shard, group=self.pg, async_op=True)
         else:
@@ -421,8 +444,9 @@ class FullyShardedDataParallel(nn.Module):
                 u.shard_grad.copy_(g)
             self._release(g)
         else:
-            if self.gloo:
-                dist.all_reduce(g, group=self.pg)
+            if self.gloo or self.proxy:
+                if not self.proxy:
+                    dist.all_reduce(g, group=self.pg)
                 part = g[self.rank * u.shard_numel:(self.rank + 1) * u.shard_numel]
                 if self._accumulating(u):
                     u.shard_grad.add_(part)
@@ -501,7 +525,7 @@ class FullyShardedDataParallel(nn.Module):
             if u.rs_work is not None:
                 self._finish_rs(u)
         self._rs_inflight.clear()
-        if self.comm and self.replicated and self._sync:
+        if self.comm and self.replicated and self._sync and not self.proxy:
             dist.all_reduce(self.rep_grad, group=self.pg)
         if self._root_unit is not None and self.comm:
             self._unbind(self._root_unit)
@@ -566,7 +590,7 @@ class FullyShardedDataParallel(nn.Module):
         ss_shard = st.buf[0] ** 2
         st2 = _clip([self.rep_grad], 0.0, prescale=1.0)
         ss_rep = st2.buf[0] ** 2
-        if self.comm:
+        if self.comm and not self.proxy:
             small_all_reduce(ss_shard, group=self.pg)
         total = (ss_shard + ss_rep).sqrt() / self.world
         coef = torch.clamp(max_norm / (total + 1e-6), max=1.0) if max_norm > 0 else torch.ones_like(total)
@@ -596,10 +620,13 @@ class FullyShardedDataParallel(nn.Module):
         """Unsharded gradients (sum over ranks), module parameter names — tests / debugging."""
         out = {}
         for u in self.units:
-            if self.comm:
+            if self.comm and not self.proxy:
                 parts = [torch.empty_like(u.shard_grad) for _ in range(self.world)]
                 dist.all_gather(parts, u.shard_grad.contiguous(), group=self.pg)
                 full = torch.cat(parts)
+            elif self.proxy:  # only rank 0's chunk exists
+                full = torch.zeros(u.total, dtype=u.shard_grad.dtype, device=u.shard_grad.device)
+                full[:u.shard_numel].copy_(u.shard_grad)
             else:
                 full = u.shard_grad
             for n, o, k, s in zip(u.names, u.offsets, u.numels, u.shapes):

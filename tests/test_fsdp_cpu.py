@@ -190,3 +190,34 @@ def test_fsdp_sharded_checkpoint_roundtrip_consolidate_and_reshard(tmp_path):
     sd = m.state_dict()
     for k, v in res[0][0].items():
         assert np.array_equal(sd[k].numpy(), v), k
+
+
+def test_fsdp_proxy_world_lays_out_rank0_of_n():
+    """FullyShardedDataParallel(proxy_world=4) on one process (no process group): every unit holds
+    1/4 of its flat parameters (rank 0's shard), gathers / reduce-scatters run as local copies of
+    rank 0's part, and a full step (with accumulation and the optimizer on the shards) runs
+    (bench.py --parallel fsdp --proxy-world N)."""
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.ops import FusedAdamW
+    from gke_ray_train_amd.parallel.fsdp import FullyShardedDataParallel
+    m = build_llama("llama-tiny", device="cpu", dtype=torch.float32, seed=5)
+    n_total = sum(p.numel() for p in m.parameters() if p.dim() >= 2)
+    f = FullyShardedDataParallel(m, proxy_world=4)
+    assert f.proxy and f.world == 4 and f.rank == 0 and f.comm
+    assert all(u.total == 4 * u.shard_numel for u in f.units)
+    assert f.shard_store.numel() * 4 >= n_total and f.shard_store.numel() * 4 < n_total + 4 * 4096 * len(f.units)
+    opt = FusedAdamW(f.optimizer_param_groups(0.01), lr=1e-3)
+    assert sum(p.numel() for g in opt.param_groups for p in g["params"]) <= f.shard_store.numel() + f.rep_flat.numel()
+    ids = torch.randint(0, 512, (4, 32))
+    before = f.shard_store.clone()
+    for j in range(2):
+        with f.no_sync(j < 1):
+            f(ids[2 * j:2 * j + 2], labels=ids[2 * j:2 * j + 2])["loss"].backward()
+    f.finish_gradient_sync()
+    assert f.grad_store.abs().sum() > 0  # rank 0's chunk of the (local) gradient arrived
+    st = f.clip_grad_norm_(1.0)
+    opt.step(grad_scale=st)
+    f.zero_grad()
+    assert not torch.equal(before, f.shard_store)
+    # units are resharded after their forward / backward: no full buffer stays bound
+    assert all(u.full is None for u in f.units if u.module is not f.module)

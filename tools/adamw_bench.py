@@ -51,6 +51,15 @@ def main():
             us = med(lambda: C.adamw(p.view(-1), g.view(-1), m.view(-1), v.view(-1), None, hyper, None, 0, 0), a.reps)
             row[f"adamw_sr{int(sr)}_us"] = round(us, 1)
             row[f"adamw_sr{int(sr)}_TBps"] = round(22 * p.numel() / us / 1e6, 2)
+            # flat update + a separate transpose pass for W^T (26 B / param in two streaming passes)
+            def flat_t():
+                C.adamw(p.view(-1), g.view(-1), m.view(-1), v.view(-1), None, hyper, None, 0, 0)
+                C.transpose_into(p, pt)
+            us = med(flat_t, a.reps)
+            row[f"flat+transpose_sr{int(sr)}_us"] = round(us, 1)
+            us = med(lambda: C.transpose_into(p, pt), a.reps)
+            row["transpose_us"] = round(us, 1)
+            row["transpose_TBps"] = round(4 * p.numel() / us / 1e6, 2)
         print(json.dumps(row), flush=True)
 
 
