@@ -3,32 +3,34 @@
 // (ray-jobs/pytorch_llm_ray.py:82-87) and the HF Llama projections under SFTTrainer.train()
 // (ray-jobs/fine_tune_llama_ray.py:333); SURVEY §2.3 N02, §2.6 K-B04.
 //
+// Status (profiles/r5_gemm_k64.md): 91-99 % of the tuned hipBLASLt kernel on the 15 Llama-2-7B
+// step shapes, every element checked against fp32 (tests/test_gemm_gpu.py). The training step keeps
+// the library for plain GEMMs; this kernel is reachable through gemm_nt variants 9-16.
+//
 // Structure (one workgroup per CU: 4 waves, one per SIMD, 128 x 128 outputs per wave):
-//   * accumulators: 8 x 8 blocks of v_mfma_f32_16x16x32_bf16 = 256 AGPRs, pinned by inline-asm
-//     MFMAs ("+a"); 128 MFMAs per 64-deep K-tile;
-//   * fragments: 128 VGPRs = the tile's two 32-deep halves (kk0, kk1) for A and B. The kk1 half of
-//     tile t is read from LDS under the kk0 MFMAs of tile t, the kk0 half of tile t+1 under the kk1
-//     MFMAs of tile t, so every ds_read has >= 20 MFMAs of cover;
+//   * accumulators: 8 x 8 blocks of v_mfma_f32_16x16x32_bf16 in LITERAL AGPRs a0-a255 (one
+//     clobber statement at entry allocates them; the MFMA statements name them directly, so the
+//     compiler never copies or spills accumulators); 128 MFMAs per 64-deep K-tile;
+//   * fragments: the K-tile's two 32-deep halves (kk0, kk1) of A and B in VGPRs (SCHED 2: kk1
+//     double-buffered, read one period ahead);
 //   * LDS: two K-tile buffers (A + B each), 130 KiB. An operand tile is 32 chunks of 1040 B; chunk
 //     c holds rows {128 (c >> 4) + 16 b + (c & 15)}, b = 0..7, as 128-B lines (the row's 64 k) at
-//     b * 128 — one LDS-DMA instruction of one wave fills one chunk with eight whole cache lines,
-//     and the 16-B pad makes the 16 rows a 16x16x32 fragment read sit in 16 different bank
-//     quads (conflict-free up to one 2-way pair per lane group);
-//   * global -> LDS: buffer_load ... lds (LDS-DMA, no VGPR round trip), 16 per wave per K-tile, one
-//     SALU (M0) each; the tile origin lives in the buffer descriptor base (scalar), per-instruction
-//     row offsets in SGPR soffsets, the lane part in one VGPR per operand;
-//   * one K-tile period = 128 MFMAs with three barriers (cdna_hip_programming.md §5, "glds >1 tile in
-//     flight": raw s_barrier, counted vmcnt, never vmcnt(0) in the loop):
-//       MFMA  0-21  read A kk1 (tile t, buffer u)                      -> lgkmcnt(0), barrier 1
-//       MFMA 22-51  read B kk1 (tile t); DMA A of tile t+2 into u (5)  -> lgkmcnt(0), barrier 2
-//       MFMA 52-92  DMA A (3) + B (5) of tile t+2 into u               -> vmcnt(13), barrier 3
-//       MFMA 93-127 read kk0 of tile t+1 (buffer u^1); DMA B (3)
-//     Barrier 1 proves every wave has read A of buffer u for the last time (its kk0 half was read in
-//     the previous period, its kk1 half before barrier 1), barrier 2 the same for B, so the DMAs of
-//     tile t+2 may overwrite them. vmcnt(13) at barrier 3 leaves exactly this period's 13 DMAs in
-//     flight: the 16 of the previous period (tile t+1) have landed before anyone reads tile t+1.
-//     DMAs get >= one full period to land; past the last tile they re-fetch tile T-1 into a buffer
-//     nobody reads again (branch-free loop, constant vmcnt);
+//     b * 128 -- one LDS-DMA instruction of one wave fills one chunk with eight whole cache lines,
+//     and the 16-B pad puts the 16 rows of a fragment read in different bank quads;
+//   * global -> LDS: buffer_load ... lds (LDS-DMA, no VGPR round trip), 16 per wave per K-tile. The
+//     tile origin lives in the buffer descriptor (SGPRs), per-instruction row offsets in SGPR
+//     soffsets, the lane part in one VGPR per operand; each DMA rides in one asm statement with an
+//     MFMA (M0 written first: the MFMA covers the M0 -> DMA wait state);
+//   * SCHED 1 (variants 9, 10): per period three barriers -- A kk1 reads -> lgkmcnt(0), barrier 1;
+//     B kk1 reads + A DMAs of K-tile t+2 -> lgkmcnt(0), barrier 2; A/B DMAs -> vmcnt(12), barrier 3;
+//     kk0 reads of K-tile t+1 + the last B DMAs (schedule tables kReadA1 ... below);
+//     SCHED 2 (variants 11, 12): two barriers, reads of the next K-tile bunched after barrier B
+//     (slower: the LDS port, not the barriers, is the constraint -- profiles/r5_gemm_k64.md);
+//   * PERSIST (variants 9, 11): grid = #CUs, the K pipeline runs across a workgroup's output tiles
+//     (the last two periods of a tile DMA the next tile's first two K-tiles), so between tiles only
+//     the epilogue remains; an out-of-range DMA uses a zero-record descriptor (no memory traffic);
+//   * epilogue: AGPR reads after the MFMA -> VALU wait states, bf16 pack, v_permlane16_swap so each
+//     lane stores 8 consecutive columns (16-B stores); beta = 1 adds the old C;
 //   * blockIdx -> tile: bijective XCD remap, then 8-row groups (T1).
 // Requirements (host-checked): M % 256 == 0, N % 256 == 0, K % 128 == 0, K >= 128, row strides
 // multiples of 8 elements, 16-byte aligned bases, every operand byte offset below 2^31.
@@ -49,13 +51,13 @@ constexpr int BUFB = 2 * TEN;    // A + B of one K-tile
 constexpr int LDSB = 2 * BUFB;   // two K-tile buffers = 133,120 B
 constexpr int kGroupRows = 8;
 
-// The 8 x 8 accumulator blocks live in LITERAL AGPRs: block (i, j) = a[4 (8 i + j) .. +3]. One
+// The 8 x 8 accumulator blocks live in LITERAL AGPRs: block (i, j) = a[4 (8 i + j) .. +3]. A
 // statement at kernel entry declares all 256 AGPRs clobbered, which makes the kernel descriptor
-// allocate them; the compiler's own values need ~140 arch VGPRs, so it never allocates, copies or
-// spills into the AGPR file (checked: no v_accvgpr_* outside these statements in the .s;
-// cdna_hip_programming.md §5.7 item 4). The MFMA statements themselves list no clobbers: with them
-// hipcc pads an s_nop between every two consecutive statements. ZERO: the first K-tile of an output
-// tile starts from the inline constant 0.
+// allocate them; the compiler's own values need ~140-190 arch VGPRs, so it never allocates into the
+// AGPR file. Every MFMA statement repeats the clobber list: without it the compiler treats the AGPRs
+// as dead between statements and adds accvgpr copies of its own; the price is an s_nop 0 between
+// consecutive MFMA statements (free here: removing every wait and barrier gains only 1-3 %,
+// profiles/r5_gemm_k64.md). ZERO: the first K-tile of an output tile starts from the constant 0.
 #define GRT_ACC_CLOBBERS "a0", "a1", "a2", "a3", "a4", "a5", "a6", "a7", "a8", "a9", "a10", "a11", "a12", "a13", "a14", "a15", "a16", "a17", "a18", "a19", "a20", "a21", "a22", "a23", "a24", "a25", "a26", "a27", "a28", "a29", "a30", "a31", "a32", "a33", "a34", "a35", "a36", "a37", "a38", "a39", "a40", "a41", "a42", "a43", "a44", "a45", "a46", "a47", "a48", "a49", "a50", "a51", "a52", "a53", "a54", "a55", "a56", "a57", "a58", "a59", "a60", "a61", "a62", "a63", "a64", "a65", "a66", "a67", "a68", "a69", "a70", "a71", "a72", "a73", "a74", "a75", "a76", "a77", "a78", "a79", "a80", "a81", "a82", "a83", "a84", "a85", "a86", "a87", "a88", "a89", "a90", "a91", "a92", "a93", "a94", "a95", "a96", "a97", "a98", "a99", "a100", "a101", "a102", "a103", "a104", "a105", "a106", "a107", "a108", "a109", "a110", "a111", "a112", "a113", "a114", "a115", "a116", "a117", "a118", "a119", "a120", "a121", "a122", "a123", "a124", "a125", "a126", "a127", "a128", "a129", "a130", "a131", "a132", "a133", "a134", "a135", "a136", "a137", "a138", "a139", "a140", "a141", "a142", "a143", "a144", "a145", "a146", "a147", "a148", "a149", "a150", "a151", "a152", "a153", "a154", "a155", "a156", "a157", "a158", "a159", "a160", "a161", "a162", "a163", "a164", "a165", "a166", "a167", "a168", "a169", "a170", "a171", "a172", "a173", "a174", "a175", "a176", "a177", "a178", "a179", "a180", "a181", "a182", "a183", "a184", "a185", "a186", "a187", "a188", "a189", "a190", "a191", "a192", "a193", "a194", "a195", "a196", "a197", "a198", "a199", "a200", "a201", "a202", "a203", "a204", "a205", "a206", "a207", "a208", "a209", "a210", "a211", "a212", "a213", "a214", "a215", "a216", "a217", "a218", "a219", "a220", "a221", "a222", "a223", "a224", "a225", "a226", "a227", "a228", "a229", "a230", "a231", "a232", "a233", "a234", "a235", "a236", "a237", "a238", "a239", "a240", "a241", "a242", "a243", "a244", "a245", "a246", "a247", "a248", "a249", "a250", "a251", "a252", "a253", "a254", "a255"
 template <int N, bool ZERO>
 __device__ __forceinline__ void mfma_acc(const bf16x8& a, const bf16x8& b) {
@@ -124,6 +126,15 @@ constexpr int kRead0First = 80;  // 16 reads at 80, 82, ..., 110
 constexpr int kBar1 = 21, kBar2 = 47, kBar3 = 79;
 constexpr int kDmaBeforeBar3 = 12;
 
+// SCHED 2: every fragment of a K-tile is read in the period BEFORE it is multiplied (kk1 fragments
+// double-buffered in registers: a1[U] / b1[U]), so a period needs only two barriers and its DMAs can
+// start right after the first:
+// seg 1 (0-15): lgkmcnt(0), barrier A (every wave's reads of this buffer done)
+// seg 2 (16-79): 16 DMAs of K-tile t+2 into this buffer at 16, 20, ..., 76 -> vmcnt(16), barrier B
+// seg 3 (80-127): 32 reads of the next buffer (kk0 into a0 / b0, then kk1 into a1[U^1] / b1[U^1])
+// The last DMA of a period has 131 MFMAs (~1.3 us) before the barrier that waits for it (SCHED 1: 92).
+constexpr int kBarA2 = 15, kDma2First = 16, kBarB2 = 79, kRead2First = 80;
+
 constexpr int find8(const int (&t)[8], int i) {
   for (int q = 0; q < 8; ++q)
     if (t[q] == i) return q;
@@ -136,7 +147,9 @@ constexpr int find8(const int (&t)[8], int i) {
 // the last period's kk0 reads are already that tile's first fragments, so between tiles only the
 // epilogue remains (no prologue, no pipeline drain). Without PERSIST the grid is one workgroup per
 // tile (A/B reference).
-template <int EPI, bool PERSIST>
+// DIAG (timing experiments only, results wrong): 1 = no vmcnt wait at barrier 3, 2 = no lgkmcnt(0)
+// at barriers 1 / 2, 4 = no s_barrier
+template <int EPI, bool PERSIST, int SCHED, int DIAG = 0>
 __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
   __shared__ __attribute__((aligned(16))) char smem[LDSB];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -195,7 +208,7 @@ __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
   int tm, tn;
   if (!tile_of(0, tm, tn)) return;  // whole workgroup: uniform
   asm volatile("" ::: GRT_ACC_CLOBBERS);  // allocates the AGPR file (see mfma_acc)
-  bf16x8 a0[8], a1[8], b0[8], b1[8];
+  bf16x8 a0[8], b0[8], a1[SCHED == 2 ? 2 : 1][8], b1[SCHED == 2 ? 2 : 1][8];
 
   // ---- prologue (once per workgroup): K-tiles 0 and 1 of the first tile in flight, kk0 of K-tile 0
   {
@@ -211,6 +224,10 @@ __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) { b0[j] = frag(fb[0], j, 0); a0[j] = frag(fa[0], j, 0); }
+    if constexpr (SCHED == 2) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { b1[0][j] = frag(fb[0], j, 1); a1[0][j] = frag(fa[0], j, 1); }
+    }
   }
 
   // ---- one K-tile period on buffer U (compile-time); FIRST: K-tile 0 of an output tile (its kk0
@@ -219,14 +236,61 @@ __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
   auto period = [&](auto U_, auto FIRST_, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb) __attribute__((always_inline)) {
     constexpr int U = decltype(U_)::value;
     constexpr bool ZERO = decltype(FIRST_)::value && (true);
+    if constexpr (SCHED == 2) {
+      static_for<128>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int I = decltype(I_)::value;
+        constexpr int kk = I / 64, i = (I % 64) / 8, j = I % 8;
+        constexpr int dq = (I >= kDma2First && I < kDma2First + 64 && (I - kDma2First) % 4 == 0) ? (I - kDma2First) / 4 : -1;
+        constexpr int dqa = dq >= 0 && dq < 8 ? dq : 0, dqb = dq >= 8 ? dq - 8 : 0;
+        constexpr uint32_t m0off = dq < 8 ? U * BUFB + 0 + dqa * 4 * CH : U * BUFB + TEN + dqb * 4 * CH;
+        bf16x8& af = kk == 0 ? a0[i] : a1[U][i];
+        bf16x8& bfr = kk == 0 ? b0[j] : b1[U][j];
+        if constexpr (dq >= 0) {
+          const uint32_t vo = dq < 8 ? avoff : bvoff;
+          const uint32_t so = dq < 8 ? soa[dqa] : sob[dqb];
+          const auto rs = dq < 8 ? ra : rb;
+          mfma_acc_dma<4 * (8 * i + j), ZERO && kk == 0, m0off>(bfr, af, vo, rs, so, mbase);
+        } else {
+          mfma_acc<4 * (8 * i + j), ZERO && kk == 0>(bfr, af);
+        }
+        if constexpr (I >= kRead2First) {
+          // 32 reads at 80, 81, 83, 84, ... 126: x = 0..15 kk0, 16..31 kk1; within each,
+          // B[0], A[0], B[1..7], A[1..7]
+          constexpr int x0 = (2 * (I - kRead2First) + 2) / 3;  // first x with 80 + 3x/2 >= I
+          constexpr bool hit = x0 < 32 && kRead2First + (3 * x0) / 2 == I;
+          if constexpr (hit) {
+            constexpr int x = x0 & 15, rk = x0 >> 4;
+            constexpr bool isb = x == 0 || (x >= 2 && x <= 8);
+            constexpr int blk = x == 0 ? 0 : x == 1 ? 0 : x <= 8 ? x - 1 : x - 8;
+            if constexpr (rk == 0) {
+              if constexpr (isb) b0[blk] = frag(fb[U ^ 1], blk, 0);
+              else a0[blk] = frag(fa[U ^ 1], blk, 0);
+            } else {
+              if constexpr (isb) b1[U ^ 1][blk] = frag(fb[U ^ 1], blk, 1);
+              else a1[U ^ 1][blk] = frag(fa[U ^ 1], blk, 1);
+            }
+          }
+        }
+        if constexpr (I == kBarA2) {
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        }
+        if constexpr (I == kBarB2) {
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_waitcnt vmcnt(16)\n\ts_barrier" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      return;
+    }
     static_for<128>([&](auto I_) __attribute__((always_inline)) {
       constexpr int I = decltype(I_)::value;
       constexpr int kk = I / 64, i = (I % 64) / 8, j = I % 8;
       constexpr int ra1q = find8(kReadA1, I), rb1q = find8(kReadB1, I);
       constexpr int dAq = find8(kDmaA, I), dBq = find8(kDmaB, I);
       constexpr uint32_t m0off = dAq >= 0 ? U * BUFB + 0 + dAq * 4 * CH : U * BUFB + TEN + (dBq >= 0 ? dBq : 0) * 4 * CH;
-      bf16x8& af = kk == 0 ? a0[i] : a1[i];
-      bf16x8& bfr = kk == 0 ? b0[j] : b1[j];
+      bf16x8& af = kk == 0 ? a0[i] : a1[0][i];
+      bf16x8& bfr = kk == 0 ? b0[j] : b1[0][j];
       if constexpr (dAq >= 0 || dBq >= 0) {
         constexpr int q = dAq >= 0 ? dAq : dBq;
         const uint32_t vo = dAq >= 0 ? avoff : bvoff;
@@ -236,8 +300,8 @@ __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
       } else {
         mfma_acc<4 * (8 * i + j), ZERO && kk == 0>(bfr, af);
       }
-      if constexpr (ra1q >= 0) a1[ra1q] = frag(fa[U], ra1q, 1);
-      if constexpr (rb1q >= 0) b1[rb1q] = frag(fb[U], rb1q, 1);
+      if constexpr (ra1q >= 0) a1[0][ra1q] = frag(fa[U], ra1q, 1);
+      if constexpr (rb1q >= 0) b1[0][rb1q] = frag(fb[U], rb1q, 1);
       if constexpr (I >= kRead0First && I < kRead0First + 32 && (I - kRead0First) % 2 == 0) {
         constexpr int x = (I - kRead0First) / 2;  // 0: B0[0], 1: A0[0], 2..8: B0[1..7], 9..15: A0[1..7]
         if constexpr (x == 0) b0[0] = frag(fb[U ^ 1], 0, 0);
@@ -247,12 +311,14 @@ __global__ __launch_bounds__(256, 1) void gemm_k64_kernel(const GemmParams p) {
       }
       if constexpr (I == kBar1 || I == kBar2) {
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if constexpr (!(DIAG & 2)) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!(DIAG & 4)) asm volatile("s_barrier" ::: "memory");
       }
       if constexpr (I == kBar3) {
         static_assert(kDmaBeforeBar3 == 12, "vmcnt below");
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+        if constexpr (!(DIAG & 1)) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        if constexpr (!(DIAG & 4)) asm volatile("s_barrier" ::: "memory");
       }
       __builtin_amdgcn_sched_barrier(0);
     });
@@ -362,11 +428,16 @@ static int num_cus() {
 
 void gemm_nt_k64(const GemmParams& p, hipStream_t stream) {
   const int ntiles = (p.M / 256) * (p.N / 256);
-  if (p.variant == 10) {  // one workgroup per tile (A/B reference)
-    hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, false>), dim3(ntiles), dim3(256), 0, stream, p);
-  } else {
-    const int G = std::min(ntiles, num_cus());
-    hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, true>), dim3(G), dim3(256), 0, stream, p);
+  const int G = std::min(ntiles, num_cus());
+  switch (p.variant) {
+    case 10: hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, false, 1>), dim3(ntiles), dim3(256), 0, stream, p); break;
+    case 11: hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, true, 2>), dim3(G), dim3(256), 0, stream, p); break;
+    case 12: hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, false, 2>), dim3(ntiles), dim3(256), 0, stream, p); break;
+    case 13: hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, true, 1, 1>), dim3(G), dim3(256), 0, stream, p); break;
+    case 14: hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, true, 1, 2>), dim3(G), dim3(256), 0, stream, p); break;
+    case 15: hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, true, 1, 4>), dim3(G), dim3(256), 0, stream, p); break;
+    case 16: hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, true, 1, 7>), dim3(G), dim3(256), 0, stream, p); break;
+    default: hipLaunchKernelGGL((gemm_k64_kernel<GEMM_EPI_STORE, true, 1>), dim3(G), dim3(256), 0, stream, p); break;
   }
 }
 

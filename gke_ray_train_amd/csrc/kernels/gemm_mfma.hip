@@ -1,11 +1,12 @@
 // Projection GEMM for gfx950:  C[M][N] (+)= sum_k A[M][K] * B[N][K]    (bf16 in, fp32 acc, bf16 out)
 //
-// Role: every Linear of the Llama step that hipBLASLt used to run — the forward Y = X W^T and the
-// input gradient dX = dY W (as dY (W^T)^T on the W^T copy the optimizer writes) — reference: the
-// cuBLAS GEMMs under nn.Linear in ray-jobs/pytorch_llm_ray.py:82-87 and the HF Llama projections
-// under SFTTrainer.train(), ray-jobs/fine_tune_llama_ray.py:333.
-// Owning it lets the producer/consumer elementwise work ride in the epilogue (EPI_SWIGLU: the
-// gate/up GEMM writes silu(g) * u as well, so no separate SwiGLU pass re-reads [M, 2F]).
+// Role: hand-written forms of the Llama projection GEMMs (reference: the cuBLAS GEMMs under
+// nn.Linear in ray-jobs/pytorch_llm_ray.py:82-87 and the HF Llama projections under
+// SFTTrainer.train(), ray-jobs/fine_tune_llama_ray.py:333). The
+// training step runs the tuned hipBLASLt kernels for these (faster, profiles/r4_gemm_family.md,
+// profiles/r5_gemm_k64.md); this file holds the round-4 family (variants 1-8: ping-pong 8-wave,
+// 4-wave AGPR, TT / NN operand forms) and dispatches variants 9-16 to gemm_k64.hip. Only the plain
+// store / accumulate epilogues exist (no fused elementwise epilogue).
 //
 // Design (cdna_hip_programming.md §5 "256² 8-phase template", T1-T5; MI355X_MICROARCH.md §LDS):
 //   * 256 x 256 output tile per workgroup, 8 waves = 2 wave groups (rows) x 4 (cols), 128 x 64 per
@@ -629,7 +630,7 @@ void gemm_nt(const GemmParams& p, hipStream_t stream) {
   const int nwg = (p.M / GT) * (p.N / GT);
   const dim3 grid(nwg), block(GNT);
   const int variant = p.variant;
-  if ((variant == 9 || variant == 10) && gemm_nt_k64_supported(p.M, p.N, p.K, p.lda, p.ldb)) {
+  if (variant >= 9 && variant <= 16 && gemm_nt_k64_supported(p.M, p.N, p.K, p.lda, p.ldb)) {
     gemm_nt_k64(p, stream);
   } else if (variant == 4 || variant == 5) {
     if (variant == 4) hipLaunchKernelGGL((gemm_nt_w4_kernel<4, true>), grid, dim3(256), 0, stream, p);

@@ -79,13 +79,14 @@ def all_reduce_scalar(x: float, op=None, device=None) -> float:
 
 
 def small_all_reduce(t: torch.Tensor, group=None) -> torch.Tensor:
-    """In-place SUM all-reduce of a small (latency-bound) tensor: over the xGMI IPC one-shot
-    kernel (``parallel/ipc.py``) when ``GRT_IPC_COLLECTIVES=1`` on a single-node RCCL group, else
-    through the process group. Grad-norm scalars, logged losses and metrics go through here."""
-    if group is None and t.is_cuda and t.dtype in (torch.float32, torch.bfloat16):
-        from .ipc import default_communicator
-        comm = default_communicator()
-        if comm is not None and t.numel() * t.element_size() <= comm.cap:
+    """In-place SUM all-reduce of a small (latency-bound) tensor: over the xGMI IPC kernels
+    (``parallel/ipc.py``) when the message routes there (``GRT_IPC_COLLECTIVES``: auto by size on a
+    single-node RCCL group), else through the process group. Grad-norm scalars, logged losses,
+    metrics and FSDP's replicated-parameter gradients go through here."""
+    if t.is_cuda and t.dtype in (torch.float32, torch.bfloat16):
+        from .ipc import communicator, ipc_mode, route_limit, routes
+        comm = communicator(group, "default")
+        if comm is not None and routes(t.numel() * t.element_size(), t.dtype, route_limit(ipc_mode(), comm.cap)):
             return comm.all_reduce(t)
     dist.all_reduce(t, group=group)
     return t

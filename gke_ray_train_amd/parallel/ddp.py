@@ -56,6 +56,17 @@ class _DoneWork:
         return None
 
 
+class _StreamWork:
+    """Work of a collective issued on a side stream (IPC kernels): wait() orders the current
+    stream after it, without a host synchronisation."""
+
+    def __init__(self, event: torch.cuda.Event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+
+
 def shared_param_ids(module: nn.Module) -> set:
     """ids of parameters owned by more than one module (tied embeddings): their gradient has two
     producers, so they must not use the single-writer direct gradient slots."""
@@ -228,6 +239,22 @@ class DistributedDataParallel(nn.Module):
                 for m in module.modules():
                     if isinstance(m, _DirectLinear) and id(m.weight) in self._direct:
                         m.weight._grt_fwd_transpose = True
+        # buckets small enough for the xGMI IPC kernels (parallel/ipc.py; e.g. the no-decay group of
+        # norm weights) are all-reduced by them on a side stream instead of by RCCL. The decision
+        # is a function of the bucket layout only, identical on every rank.
+        self._ipc = None
+        self._ipc_limit = 0
+        self._ipc_stream = None
+        self.ipc_bucket_launches = 0  # buckets all-reduced over IPC so far (tests / logs)
+        if self.comm and not self.proxy and dev0.type == "cuda":
+            from .ipc import communicator, ipc_mode, route_limit, routes
+            if ipc_mode() != "0" and any(
+                    routes((b.end - b.start) * g.grad.element_size(), g.grad.dtype, route_limit(ipc_mode(), 8 << 20))
+                    for g in self.groups for b in g.buckets):
+                self._ipc = communicator(process_group, "ddp-buckets")
+                if self._ipc is not None:
+                    self._ipc_limit = route_limit(ipc_mode(), self._ipc.cap)
+                    self._ipc_stream = torch.cuda.Stream(dev0)
         self._norm_ws = None
         self._norm_stream = None
         self._norm_bad = False  # a step whose early norm cannot be trusted (fall back)
@@ -376,6 +403,22 @@ class DistributedDataParallel(nn.Module):
                 g.shard_grad[b.shard_off:b.shard_off + c].copy_(g.grad[b.start + self.rank * c:b.start + (self.rank + 1) * c])
             b.work = _DoneWork()
             return
+        if self._ipc is not None:
+            from .ipc import routes
+            view = g.grad[b.start:b.end]
+            if routes(view.numel() * view.element_size(), view.dtype, self._ipc_limit):
+                cur = torch.cuda.current_stream(view.device)
+                self._ipc_stream.wait_stream(cur)
+                with torch.cuda.stream(self._ipc_stream):
+                    self._ipc.all_reduce(view)
+                    if self.zero:  # all-reduce + keep our chunk = the reduce-scatter's output
+                        c = (b.end - b.start) // self.world_size
+                        g.shard_grad[b.shard_off:b.shard_off + c].copy_(view[self.rank * c:(self.rank + 1) * c])
+                    ev = torch.cuda.Event()
+                    ev.record(self._ipc_stream)
+                b.work = _StreamWork(ev)
+                self.ipc_bucket_launches += 1
+                return
         if not self.zero or self.gloo:  # gloo has no reduce-scatter: all-reduce, keep our chunk later
             b.work = dist.all_reduce(g.grad[b.start:b.end], op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
         else:

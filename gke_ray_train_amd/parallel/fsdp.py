@@ -526,7 +526,7 @@ class FullyShardedDataParallel(nn.Module):
                 self._finish_rs(u)
         self._rs_inflight.clear()
         if self.comm and self.replicated and self._sync and not self.proxy:
-            dist.all_reduce(self.rep_grad, group=self.pg)
+            small_all_reduce(self.rep_grad, group=self.pg)  # IPC kernels when small enough
         if self._root_unit is not None and self.comm:
             self._unbind(self._root_unit)
 

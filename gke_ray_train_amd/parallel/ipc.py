@@ -49,7 +49,8 @@ class IpcCommunicator:
         if self.world > C.IPC_MAX_RANKS:
             raise ValueError(f"IPC collectives cover one node (<= {C.IPC_MAX_RANKS} ranks), got {self.world}")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        self.dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        self.dev_index = self.device.index if self.device.index is not None else (
+            torch.cuda.current_device() if self.device.type == "cuda" else 0)
         self.cap = (int(max_bytes) + 15) // 16 * 16
         # two-shot pays once each GPU would otherwise read (W-1) x the message over the fabric
         self.two_shot_bytes = int(two_shot_bytes) if two_shot_bytes is not None else (
@@ -62,21 +63,43 @@ class IpcCommunicator:
                      C.ipc_alloc(2 * self.cap, False, self.dev_index),
                      C.ipc_alloc(C.IPC_SIGNAL_BYTES, True, self.dev_index)]
         self.err = torch.zeros(4, dtype=torch.int32, device=self.device)
-        handles = [C.ipc_handle(p, self.dev_index) for p in self._own]
+        failure: Optional[BaseException] = None
+        try:
+            handles = [C.ipc_handle(p, self.dev_index) for p in self._own]
+        except Exception as e:  # noqa: BLE001 -- still take part in the exchange, fail below
+            handles, failure = None, e
         gathered: List[Optional[list]] = [None] * self.world
-        dist.all_gather_object(gathered, [os.getpid(), handles], group=group)
+        dist.all_gather_object(gathered, [os.getpid(), handles, self.cap], group=group)
         self._opened = []
         ptrs = [[0] * self.world for _ in range(3)]
-        for r, (_pid, hs) in enumerate(gathered):
-            for k in range(3):
-                if r == self.rank:
-                    ptrs[k][r] = self._own[k]
-                else:
-                    p = C.ipc_open(hs[k], self.dev_index)
-                    self._opened.append(p)
-                    ptrs[k][r] = p
+        caps = {int(g[2]) for g in gathered}
+        if failure is not None or any(g[1] is None for g in gathered):
+            failure = failure or RuntimeError("a peer could not export its IPC handles")
+        elif len(caps) != 1:
+            # the kernel addresses a peer's parity halves with OUR cap: every rank must agree
+            failure = ValueError(f"IPC buffer sizes differ across ranks: {sorted(caps)}")
+        else:
+            try:
+                for r, (_pid, hs, _cap) in enumerate(gathered):
+                    for k in range(3):
+                        if r == self.rank:
+                            ptrs[k][r] = self._own[k]
+                        else:
+                            p = C.ipc_open(hs[k], self.dev_index)
+                            self._opened.append(p)
+                            ptrs[k][r] = p
+            except Exception as e:  # noqa: BLE001 -- reported to every rank below
+                failure = e
         self.staging, self.result, self.signal = ptrs
-        dist.barrier(group=group)  # every peer has mapped every buffer before first use
+        # every peer has mapped every buffer before first use; and all ranks learn whether any
+        # rank failed (a rank that raised alone would leave the others waiting in a collective)
+        ok = torch.tensor([0 if failure else 1], dtype=torch.int32,
+                          device=self.device if dist.get_backend(group) == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if int(ok.item()) != 1:
+            self._release()
+            raise RuntimeError(f"IPC communicator setup failed on rank(s) of the group"
+                               f"{'' if failure is None else f' (here: {failure})'}")
 
     # ------------------------------------------------------------------ collectives
     def _next_epoch(self) -> int:
@@ -117,12 +140,7 @@ class IpcCommunicator:
             peers = [i for i in range(32) if e >> i & 1]
             raise RuntimeError(f"IPC collective timed out waiting for rank(s) {peers} (rank {self.rank})")
 
-    def close(self):
-        if self._C is None:
-            return
-        torch.cuda.synchronize(self.device)
-        if dist.is_initialized():
-            dist.barrier(group=self.group)  # no peer kernel still reads our buffers
+    def _release(self):
         for p in self._opened:
             self._C.ipc_close(p, self.dev_index)
         self._opened = []
@@ -131,13 +149,83 @@ class IpcCommunicator:
         self._own = []
         self._C = None
 
+    def close(self):
+        if self._C is None:
+            return
+        torch.cuda.synchronize(self.device)
+        if dist.is_initialized():
+            dist.barrier(group=self.group)  # no peer kernel still reads our buffers
+        self._release()
 
-_default: Optional[IpcCommunicator] = None
+    def self_test(self) -> bool:
+        """One 16-byte all-reduce with known inputs, checked on the host, agreed over the group:
+        True on every rank or False on every rank (the automatic path is then left unused)."""
+        x = torch.full((4,), float(self.rank + 1), dtype=torch.float32, device=self.device)
+        self.all_reduce(x)
+        torch.cuda.synchronize(self.device)
+        want = self.world * (self.world + 1) / 2
+        good = bool(torch.all(x == want).item()) and int(self.err[0].item()) == 0
+        ok = torch.tensor([1 if good else 0], dtype=torch.int32,
+                          device=self.device if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
+        return int(ok.item()) == 1
+
+
+# ---------------------------------------------------------------------- routing (data plane)
+# GRT_IPC_COLLECTIVES: "auto" (default) -> messages up to IPC_AUTO_BYTES go over the IPC kernels on
+# a single-node RCCL group; "1" -> everything up to the buffer capacity; "0" -> RCCL only.
+IPC_AUTO_BYTES = 2 << 20
+
+
+def ipc_mode() -> str:
+    v = os.environ.get("GRT_IPC_COLLECTIVES", "auto").strip().lower()
+    return {"1": "1", "on": "1", "true": "1", "0": "0", "off": "0", "false": "0"}.get(v, "auto")
+
+
+def route_limit(mode: str, cap: int) -> int:
+    """Largest message (bytes) routed over IPC; 0 = none."""
+    if mode == "0":
+        return 0
+    return int(cap) if mode == "1" else min(int(cap), IPC_AUTO_BYTES)
+
+
+def routes(nbytes: int, dtype: torch.dtype, limit: int) -> bool:
+    """Pure function of (size, dtype, limit): identical on every rank, so every rank takes the same
+    path for the same collective (a split decision would deadlock the group)."""
+    return dtype in (torch.float32, torch.bfloat16) and 0 < nbytes <= limit
+
+
+_comms: dict = {}
+
+
+def communicator(group=None, tag: str = "default", max_bytes: int = 8 << 20) -> Optional[IpcCommunicator]:
+    """Communicator for (group, tag), created collectively on first use, or None when IPC is off,
+    unavailable, or failed its set-up or self-test on any rank (then every rank uses RCCL). Each
+    tag has its own buffers and epoch sequence, so a tag may be driven from its own stream."""
+    key = (id(group) if group is not None else None, tag)
+    if key in _comms:
+        return _comms[key]
+    comm = None
+    if ipc_mode() != "0" and ipc_available(group):
+        try:
+            comm = IpcCommunicator(group, max_bytes=max_bytes)
+        except RuntimeError:
+            comm = None  # every rank raised the same way (agreed in __init__)
+        if comm is not None and not comm.self_test():
+            comm.close()
+            comm = None
+    _comms[key] = comm
+    return comm
 
 
 def ipc_available(group=None) -> bool:
-    """True when every rank of the group is a GPU process on this node and the kernels load."""
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend(group) != "nccl":
+    """True when every rank of the group is a GPU process on this node and the kernels load.
+    ``GRT_IPC_ALLOW_GLOO=1`` also accepts a gloo group (tests: several processes sharing one GPU,
+    where RCCL refuses duplicate devices)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    backend = dist.get_backend(group)
+    if backend != "nccl" and not (backend == "gloo" and os.environ.get("GRT_IPC_ALLOW_GLOO") == "1"):
         return False
     if not torch.cuda.is_available() or not _native.kernels_available():
         return False
@@ -147,9 +235,5 @@ def ipc_available(group=None) -> bool:
 
 
 def default_communicator() -> Optional[IpcCommunicator]:
-    """Process-wide communicator over the default group when ``GRT_IPC_COLLECTIVES=1`` and
-    :func:`ipc_available`; otherwise None (callers fall back to RCCL)."""
-    global _default
-    if _default is None and os.environ.get("GRT_IPC_COLLECTIVES", "0") == "1" and ipc_available():
-        _default = IpcCommunicator()
-    return _default
+    """Process-wide communicator over the default group (see :func:`communicator`)."""
+    return communicator(None, "default")

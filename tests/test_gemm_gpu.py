@@ -57,6 +57,28 @@ def test_gemm_nt_strided_operands_and_unsupported_shapes():
     assert not C.gemm_nt(_rand(300, 256), b, bad, False, 0)
 
 
+@pytest.mark.parametrize("variant", [9, 10, 11, 12])
+@pytest.mark.parametrize("M,N,K,lda", [(256, 256, 128, None), (512, 768, 256, None), (768, 256, 4096, None),
+                                       (256, 1280, 384, 392), (4096, 4352, 256, None)])
+def test_gemm_k64_matches_fp32(variant, M, N, K, lda):
+    """gemm_k64.hip: one tile, the shortest reduction (two K-tiles), a long reduction, a padded row
+    stride, and 272 tiles (> 256 CUs: the persistent grid's second, partial round of tiles and
+    the cross-tile K pipeline into a tile that another workgroup's round ends on)."""
+    C = _C()
+    torch.manual_seed(M + N + K + variant)
+    a, b = _rand(M, K, ld=lda), _rand(N, K)
+    out = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+    assert C.gemm_nt(a, b, out, False, variant)
+    ref = a.float() @ b.float().t()
+    _check(out, ref, f"k64 v{variant} {M}x{N}x{K}")
+    out2 = torch.empty_like(out)
+    assert C.gemm_nt(a, b, out2, False, variant)
+    assert torch.equal(out, out2), "run-to-run difference (race)"
+    acc = out.clone()
+    assert C.gemm_nt(a, b, acc, True, variant)
+    _check(acc, out.float() + ref, f"k64 v{variant} accumulate")
+
+
 @pytest.mark.parametrize("P,Q,R", [(256, 256, 64), (512, 768, 192), (256, 1280, 1024)])
 def test_gemm_wgrad_token_major_matches_fp32(P, Q, R):
     C = _C()

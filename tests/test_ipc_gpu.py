@@ -104,3 +104,156 @@ def test_ipc_allreduce_matches_host_sum(world):
         for r in range(1, world):  # fixed reduction order: bit-identical on every rank
             assert torch.equal(torch.from_numpy(res[r][i]), torch.from_numpy(res[0][i]))
     print(f"world {world}: 4-byte all-reduce {res[0]['us']:.1f} us")
+
+
+# ----------------------------------------------------------------------------- buffer shapes
+def _shapes_worker(rank, world, port, q):
+    """Separately allocated inputs of many sizes (1 element .. exactly the buffer capacity), at
+    16-B aligned and unaligned offsets, alternating between two communicators (own buffers and
+    epoch sequences, different capacities) so both parities of each are reused many times."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    try:
+        from gke_ray_train_amd.parallel.ipc import IpcCommunicator
+        small = IpcCommunicator(max_bytes=4096, timeout_s=20.0)
+        big = IpcCommunicator(max_bytes=1 << 20, timeout_s=20.0, two_shot_bytes=64 << 10)
+        cases = []
+        for cap_c, c in ((4096, small), (1 << 20, big)):
+            for dt in (torch.float32, torch.bfloat16):
+                e = torch.tensor([], dtype=dt).element_size()
+                for n in (1, 3, 7, 8, 9, cap_c // e - 1, cap_c // e):
+                    cases.append((c, n, dt))
+        for i, (c, n, dt) in enumerate(cases):
+            g = torch.Generator().manual_seed(7000 + 100 * i + rank)
+            host = torch.randn(n + 1, generator=g).to(dt)
+            buf = host.cuda()                        # its own allocation
+            x = buf[1:] if i % 2 else buf[:n]         # odd cases: a view at a 2/4-byte offset
+            c.all_reduce(x)
+            out[i] = x.float().cpu().numpy()
+        try:  # one element beyond the capacity is refused, not truncated
+            small.all_reduce(torch.zeros(4096 // 4 + 1, device="cuda"))
+            out["over"] = "accepted"
+        except ValueError:
+            out["over"] = "refused"
+        torch.cuda.synchronize()
+        small.check()
+        big.check()
+        small.close()
+        big.close()
+        q.put((rank, out))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _shape_cases():
+    cases = []
+    for cap_c in (4096, 1 << 20):
+        for dt in (torch.float32, torch.bfloat16):
+            e = torch.tensor([], dtype=dt).element_size()
+            for n in (1, 3, 7, 8, 9, cap_c // e - 1, cap_c // e):
+                cases.append((n, dt))
+    return cases
+
+
+def _spawn(target, world, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, o = q.get(timeout=timeout)
+            res[r] = o
+    finally:
+        for p in ps:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert isinstance(res[r], dict), f"rank {r}: {res[r]}"
+    return res
+
+
+def test_ipc_buffer_sizes_offsets_parities():
+    world = 2
+    res = _spawn(_shapes_worker, world)
+    for i, (n, dt) in enumerate(_shape_cases()):
+        ins = []
+        for r in range(world):
+            g = torch.Generator().manual_seed(7000 + 100 * i + r)
+            host = torch.randn(n + 1, generator=g).to(dt)
+            ins.append((host[1:] if i % 2 else host[:n]).float())
+        exp = sum(ins)
+        tol = 1e-6 if dt == torch.float32 else 1e-2
+        for r in range(world):
+            got = torch.from_numpy(res[r][i])
+            assert got.shape == exp.shape
+            assert torch.allclose(got, exp, atol=tol * 4, rtol=tol), (i, n, dt, r)
+    assert res[0]["over"] == res[1]["over"] == "refused"
+
+
+# ----------------------------------------------------------------------------- DDP data plane
+def _ddp_worker(rank, world, port, q):
+    """DDP with the automatic IPC route: the no-decay group (a 1-D weight, a few KiB) is
+    all-reduced by the IPC kernels on a side stream, the 4 MiB decay group by the process group."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GRT_IPC_ALLOW_GLOO="1",
+                      GRT_IPC_COLLECTIVES="auto", LOCAL_WORLD_SIZE=str(world))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import torch.nn as nn
+        from gke_ray_train_amd.parallel.ddp import DistributedDataParallel
+
+        class Net(nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.fc1 = nn.Linear(1024, 1024, bias=False)
+                self.norm = nn.Module()
+                self.norm.weight = nn.Parameter(torch.ones(1024))
+
+            def forward(self, x):
+                return (self.fc1(x) * self.norm.weight).square().mean()
+
+        torch.manual_seed(0)
+        net = Net().cuda()
+        ddp = DistributedDataParallel(net, broadcast_params=True)
+        g = torch.Generator().manual_seed(50 + rank)
+        x = torch.randn(16, 1024, generator=g).cuda()
+        ddp(x).backward()
+        ddp.finish_gradient_sync()
+        torch.cuda.synchronize()
+        out = {"ipc": ddp.ipc_bucket_launches,
+               "fc1": net.fc1.weight.grad.float().cpu().numpy(),
+               "norm": net.norm.weight.grad.float().cpu().numpy()}
+        # the same gradients without DDP on this rank's data (summed over ranks by the parent)
+        torch.manual_seed(0)
+        ref = Net().cuda()
+        ref(x).backward()
+        out["ref_fc1"] = ref.fc1.weight.grad.float().cpu().numpy()
+        out["ref_norm"] = ref.norm.weight.grad.float().cpu().numpy()
+        q.put((rank, out))
+    except Exception as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_small_bucket_over_ipc():
+    world = 2
+    res = _spawn(_ddp_worker, world)
+    for k in ("fc1", "norm"):
+        exp = sum(torch.from_numpy(res[r][f"ref_{k}"]) for r in range(world))
+        for r in range(world):
+            got = torch.from_numpy(res[r][k])
+            assert torch.allclose(got, exp, atol=1e-5, rtol=1e-4), (k, r, (got - exp).abs().max())
+    for r in range(world):
+        assert res[r]["ipc"] >= 1, "the no-decay bucket did not take the IPC route"
