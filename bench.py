@@ -85,6 +85,9 @@ def parse():
                     help="--offload: share of the AdamW moments kept in HBM (0..1), 'auto' = what the memory "
                          "planner says fits beside everything else (the rest streams over the host link, "
                          "overlapped with the next forward, parallel/offload.py)")
+    ap.add_argument("--offload-prefetch-gib", default="auto",
+                    help="--offload: device ring for the streamed moments, filled during the backward (GiB); "
+                         "'auto' = min(streamed moments, 32 GiB, planner headroom)")
     ap.add_argument("--offload-overlap", default="on", choices=["on", "off"],
                     help="--offload: per-unit update overlapped with the next forward (on) or the serial "
                          "after-backward stream (off)")
@@ -124,7 +127,8 @@ def build(a, cfg, dev, dtype, world):
         eng = FullyShardedDataParallel(model, param_init_fn=init, device=dev, cpu_offload=a.offload,
                                        proxy_world=a.proxy_world if proxy else 0)
         opt = eng.build_optimizer(lr=a.lr, overlap=a.offload_overlap == "on",
-                                  resident_fraction=getattr(a, "resident_fraction", 0.0))
+                                  resident_fraction=getattr(a, "resident_fraction", 0.0),
+                                  prefetch_slots=getattr(a, "prefetch_slots", 0))
         return model, eng, eng, opt
     from gke_ray_train_amd.parallel import DistributedDataParallel
     model = build_llama(cfg, device=dev, dtype=dtype, seed=1234)
@@ -269,19 +273,31 @@ def run(a):
                        seq=a.seq, zero=(a.zero == "on" or (a.zero == "auto" and (plan_world > 1 or a.force_collectives))),
                        checkpointing=a.checkpointing, lora_r=a.lora_r,
                        hbm_capacity=None if not cpu else float("inf"))
+    if a.proxy_world > 1 and world == 1:
+        plan.host_ranks_here = 1  # this process holds rank 0's host state only
+    a.resident_fraction = 0.0
+    a.prefetch_slots = 0
+    if a.offload and a.parallel == "fsdp":
+        from gke_ray_train_amd.parallel.offload import (PREFETCH_CAP_BYTES, prefetch_slots_for,
+                                                        resident_fraction_from_plan)
+        if a.offload_resident == "auto":
+            a.resident_fraction = resident_fraction_from_plan(plan, None)
+        else:
+            a.resident_fraction = float(a.offload_resident)
+        moved = plan.host_per_rank.get("adam_moments_fp32", 0.0)
+        streamed = (1.0 - a.resident_fraction) * moved
+        room = max(0.0, plan.hbm_capacity - plan.hbm_total - a.resident_fraction * moved - 8 * GiB)
+        budget = (min(streamed, PREFETCH_CAP_BYTES, room) if a.offload_prefetch_gib == "auto"
+                  else float(a.offload_prefetch_gib) * GiB)
+        a.prefetch_slots = prefetch_slots_for(budget, 1 << 26)
+        plan.hbm_per_rank["offload_resident_moments"] = a.resident_fraction * moved
+        plan.hbm_per_rank["offload_prefetch_ring"] = a.prefetch_slots * 8.0 * (1 << 26)
     if a.plan_only:
         if rank == 0:
             print(json.dumps({"memory_plan": plan.to_dict()}), flush=True)
         if dist.is_initialized():
             dist.destroy_process_group()
         return
-    a.resident_fraction = 0.0
-    if a.offload and a.parallel == "fsdp":
-        if a.offload_resident == "auto":
-            from gke_ray_train_amd.parallel.offload import resident_fraction_from_plan
-            a.resident_fraction = resident_fraction_from_plan(plan, None)
-        else:
-            a.resident_fraction = float(a.offload_resident)
     if not plan.fits:  # refuse up front with the numbers instead of an allocator error mid-step
         print(f"bench.py: memory preflight failed for {cfg.name} {a.parallel} world={world}: "
               + "; ".join(plan.problems()), file=sys.stderr, flush=True)
@@ -453,6 +469,8 @@ def run(a):
             "proxy_world": a.proxy_world if proxy else None,
             "offload_resident_units": getattr(opt, "resident_units", None) if a.offload else None,
             "offload_units": len(getattr(opt, "segments", [])) if a.offload else None,
+            "offload_prefetch_slots": getattr(opt, "prefetch_slots", None) if a.offload else None,
+            "offload_resident_fraction": round(a.resident_fraction, 3) if a.offload else None,
             "mfu_bf16_dense": round(mfu, 4),
             "hbm_plan_gib": round(plan.hbm_total / GiB, 1),
             "hbm_peak_gib": round(torch.cuda.max_memory_allocated(dev) / GiB, 1) if not cpu else None,

@@ -96,6 +96,17 @@ class _DoneWork:
         return None
 
 
+class _StreamDoneWork:
+    """Proxy-mode stand-in for a gather issued on the side stream: wait() orders the current stream
+    after the copy (as a real collective's Work.wait() does)."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.event)
+
+
 def partition_units(module: nn.Module, world: int, unit_types=DEFAULT_UNITS):
     """The FSDP partition: one unit per transformer block plus a root unit (embeddings, LM head)
     holding every other matrix; 1-D parameters are replicated. Allocates nothing, so it also runs
@@ -215,6 +226,7 @@ class FullyShardedDataParallel(nn.Module):
         # overlapped offloaded optimizer (parallel/offload.py): per-unit "shard updated" events,
         # waited for before the unit's next all-gather / forward; it also zeroes the grad shards
         self._update_events: Dict[int, torch.cuda.Event] = {}
+        self._forward_tail_hooks = []
         self._grad_zero_by_optimizer = False
         self._grads_consumed = False  # set by an optimizer that zeroed the gradients itself (offload.py)
         self._gstream = None
@@ -312,6 +324,10 @@ class FullyShardedDataParallel(nn.Module):
             self._wait_update(u, self._gstream)
             with torch.cuda.stream(self._gstream):
                 self._gather_into(u, buf)
+                if self.proxy:  # the local copy ran on the side stream: the consumer must wait for it
+                    ev = torch.cuda.Event()
+                    ev.record(self._gstream)
+                    u.gather_work = _StreamDoneWork(ev)
         else:
             self._gather_into(u, buf)
         u._pending_buf = buf
@@ -347,12 +363,21 @@ class FullyShardedDataParallel(nn.Module):
         i = seq.index(u) + step
         return seq[i] if 0 <= i < len(seq) else None
 
+    def add_forward_tail_hook(self, fn):
+        """``fn()`` runs when the LAST decoder unit's training forward starts (the offloaded
+        optimizer starts its moment uploads there, so they cross the host link during backward)."""
+        self._forward_tail_hooks.append(fn)
+
     def _make_pre_fwd(self, u: _Unit):
         def hook(mod, args):
             self._wait_gather(u)
             nxt = self._next(u, +1)
             if nxt is not None and not u.in_backward:
                 self._issue_gather(nxt)
+            elif (nxt is None and not u.in_backward and self._forward_tail_hooks and u.module is not self.module
+                  and torch.is_grad_enabled() and self.module.training):
+                for fn in self._forward_tail_hooks:
+                    fn()
         return hook
 
     def _make_post_fwd(self, u: _Unit):
@@ -556,7 +581,8 @@ class FullyShardedDataParallel(nn.Module):
         return self.world
 
     def build_optimizer(self, lr: float, weight_decay: float = 0.0, betas=(0.9, 0.999), eps=1e-8,
-                        overlap: Optional[bool] = None, resident_fraction: Optional[float] = None):
+                        overlap: Optional[bool] = None, resident_fraction: Optional[float] = None,
+                        prefetch_slots: int = 0):
         """Fused AdamW over this rank's shards. With ``cpu_offload`` the moments live in pinned host
         memory: by default the update is split by unit and overlapped with the next forward, with
         the first ``resident_fraction`` of the moments kept in HBM (parallel/offload.py);
@@ -571,7 +597,8 @@ class FullyShardedDataParallel(nn.Module):
                 if resident_fraction is None:
                     resident_fraction = float(os.environ.get("GRT_OFFLOAD_RESIDENT", "0"))
                 return OverlappedOffloadAdamW(self, chunk_elems=self.offload_chunk, resident_fraction=resident_fraction,
-                                              lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+                                              prefetch_slots=prefetch_slots, lr=lr, betas=betas, eps=eps,
+                                              weight_decay=weight_decay)
             return OffloadedAdamW(self.optimizer_param_groups(weight_decay), chunk_elems=self.offload_chunk, lr=lr,
                                   betas=betas, eps=eps)
         return FusedAdamW(self.optimizer_param_groups(weight_decay), lr=lr, betas=betas, eps=eps)

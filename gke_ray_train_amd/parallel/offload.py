@@ -20,7 +20,15 @@ MI355X design:
   the rest stream. ``resident_fraction`` (bench.py ``--offload-resident auto``) is derived from the
   memory planner: the share of the moments that fits beside everything else;
 * gradient shards of a unit are zeroed on the update stream right after its update (FSDP's
-  ``zero_grad`` would otherwise memset them on the compute stream while updates still read them).
+  ``zero_grad`` would otherwise memset them on the compute stream while updates still read them);
+* PREFETCH into the backward window: the streamed moments use a ring of ``prefetch_slots`` device
+  chunk slots. When the last decoder unit's forward starts, the uploads of the first slots' chunks
+  (forward order: the units the next forward needs first) are issued, so they cross the host link
+  during the backward, when it is otherwise idle; ``step()`` then updates those chunks at once and
+  only the remaining chunks upload under the next forward, while the downloads run beside them
+  (full duplex) and may spill into the next backward. A slot is reused only after the download of
+  its previous chunk (event per slot), which also orders every upload after the previous step's
+  download of the same host range.
 """
 from __future__ import annotations
 
@@ -36,7 +44,8 @@ from ..ops.optim import GradClipState, OffloadedAdamW, bump_param_generation, up
 class OverlappedOffloadAdamW(OffloadedAdamW):
     NSLOT = 3
 
-    def __init__(self, fsdp, chunk_elems: int = 1 << 26, resident_fraction: float = 0.0, **kw):
+    def __init__(self, fsdp, chunk_elems: int = 1 << 26, resident_fraction: float = 0.0, prefetch_slots: int = 0,
+                 **kw):
         groups = fsdp.optimizer_param_groups(kw.pop("weight_decay", 0.0))
         super().__init__(groups, chunk_elems=chunk_elems, **kw)
         self.fsdp = fsdp
@@ -59,8 +68,16 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         self._dev_m: Dict[int, torch.Tensor] = {}
         self._dev_v: Dict[int, torch.Tensor] = {}
         self._streams = None
-        self._slot_free: List[Optional[torch.cuda.Event]] = [None] * self.NSLOT
+        # streamed chunks in forward order: (unit, start, end) of the flat shard
+        self.chunks = [(u, s, min(hi, s + self.chunk)) for u, lo, hi in self.segments if id(u) not in self.resident
+                       for s in range(lo, hi, self.chunk)]
+        self.nslot = max(self.NSLOT, min(int(prefetch_slots), len(self.chunks)))
+        self.prefetch_slots = min(int(prefetch_slots), len(self.chunks))
+        self._slot_free: List[Optional[torch.cuda.Event]] = [None] * self.nslot
+        self._landed: Dict[int, torch.cuda.Event] = {}  # chunk index -> upload done (prefetched)
         fsdp._grad_zero_by_optimizer = True
+        if self.prefetch_slots > 0:
+            fsdp.add_forward_tail_hook(self.prefetch)
 
     @property
     def resident_units(self) -> int:
@@ -84,10 +101,7 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         bump_param_generation()
         fs._grads_consumed = True  # every unit's gradients are zeroed on the update stream below
         C = _native.kernels()
-        if self._streams is None:
-            self._streams = tuple(torch.cuda.Stream(dev) for _ in range(3))  # up, update, down
-            self._stage = [(torch.empty(self.chunk, device=dev), torch.empty(self.chunk, device=dev))
-                           for _ in range(self.NSLOT)]
+        self._ensure_streams(dev)
         up, upd, down = self._streams
         comp = torch.cuda.current_stream(dev)
         fs.wait_updates()  # the previous step's updates all landed (normally long done)
@@ -112,9 +126,10 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
             # (the flaky loss mismatch of tests/test_parallel_gpu.py's overlapped-offload test)
             gs.record_stream(upd)
         (sp, sst, shb), (rp, rst, rhb) = work[0], work[1]
-        for s in (up, upd, down):
+        for s in (upd, down):
             s.wait_event(entry)
-        up.wait_stream(down)  # host moments of the previous step fully downloaded
+        # uploads need no gradient: they only wait for their slot (and so for the previous step's
+        # download of the same host range, issued earlier on the in-order download stream)
         # replicated 1-D parameters (norm weights): tiny, device moments, first on the update stream
         with torch.cuda.stream(upd):
             if "dev_m" not in rst:
@@ -124,8 +139,8 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
             rp.grad.zero_()
         pf, gf = sp.data.view(-1), sp.grad.view(-1)
         m_h, v_h = sst["exp_avg"], sst["exp_avg_sq"]
-        slot = 0
         events = {}
+        ci = 0
         for u, lo, hi in self.segments:
             if id(u) in self.resident:
                 with torch.cuda.stream(upd):
@@ -135,16 +150,11 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
                     C.adamw(pf[lo:hi], gf[lo:hi], self._dev_m[id(u)], self._dev_v[id(u)], None, shb, gs, 0, lo)
                     gf[lo:hi].zero_()
             else:
-                for s in range(lo, hi, self.chunk):
-                    e = min(hi, s + self.chunk)
+                while ci < len(self.chunks) and self.chunks[ci][0] is u:
+                    _, s, e = self.chunks[ci]
+                    slot = ci % self.nslot
                     mb, vb = self._stage[slot]
-                    with torch.cuda.stream(up):
-                        if self._slot_free[slot] is not None:
-                            up.wait_event(self._slot_free[slot])
-                        mb[:e - s].copy_(m_h[s:e], non_blocking=True)
-                        vb[:e - s].copy_(v_h[s:e], non_blocking=True)
-                        landed = torch.cuda.Event()
-                        landed.record(up)
+                    landed = self._landed.pop(ci, None) or self._upload(ci)
                     with torch.cuda.stream(upd):
                         upd.wait_event(landed)
                         C.adamw(pf[s:e], gf[s:e], mb[:e - s], vb[:e - s], None, shb, gs, 0, s)
@@ -158,11 +168,48 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
                         free = torch.cuda.Event()
                         free.record(down)
                     self._slot_free[slot] = free
-                    slot = (slot + 1) % self.NSLOT
+                    ci += 1
             ev = torch.cuda.Event()
             ev.record(upd)
             events[u] = ev
+        self._landed.clear()
         fs.set_update_events(events)
+
+    def _ensure_streams(self, dev):
+        if self._streams is None:
+            self._streams = tuple(torch.cuda.Stream(dev) for _ in range(3))  # up, update, down
+            self._stage = [(torch.empty(self.chunk, device=dev), torch.empty(self.chunk, device=dev))
+                           for _ in range(self.nslot)]
+
+    def _upload(self, ci: int) -> torch.cuda.Event:
+        """Host -> device copy of streamed chunk ``ci`` into its slot on the upload stream, after the
+        slot's previous download."""
+        up = self._streams[0]
+        _, s, e = self.chunks[ci]
+        slot = ci % self.nslot
+        mb, vb = self._stage[slot]
+        sst = self.state[self.param_groups[0]["params"][0]]
+        with torch.cuda.stream(up):
+            if self._slot_free[slot] is not None:
+                up.wait_event(self._slot_free[slot])
+            mb[:e - s].copy_(sst["exp_avg"][s:e], non_blocking=True)
+            vb[:e - s].copy_(sst["exp_avg_sq"][s:e], non_blocking=True)
+            landed = torch.cuda.Event()
+            landed.record(up)
+        return landed
+
+    @torch.no_grad()
+    def prefetch(self):
+        """Upload the first ``prefetch_slots`` streamed chunks for the coming ``step()`` (called by
+        FSDP when the last decoder unit's training forward starts: the uploads cross the host link
+        during the backward)."""
+        fs = self.fsdp
+        if fs.device.type != "cuda" or self._landed or not self.chunks:
+            return
+        self._state(self.param_groups[0]["params"][0])
+        self._ensure_streams(fs.device)
+        for ci in range(self.prefetch_slots):
+            self._landed[ci] = self._upload(ci)
 
     def synchronize(self):
         """Current stream waits for every pending unit update and the moment downloads."""
@@ -201,6 +248,14 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         for st in self.state.values():
             st.pop("dev_m", None)
             st.pop("dev_v", None)
+
+
+PREFETCH_CAP_BYTES = 32 * (1 << 30)
+
+
+def prefetch_slots_for(budget_bytes: float, chunk_elems: int) -> int:
+    """Device chunk slots (m + v fp32, 8 B per element) that fit in ``budget_bytes``."""
+    return max(0, int(budget_bytes // (8.0 * chunk_elems)))
 
 
 def resident_fraction_from_plan(plan_offload, plan_resident, margin_bytes: float = 8 * (1 << 30)) -> float:

@@ -45,6 +45,9 @@ class MemoryPlan:
     hbm_capacity: float = MI355X_HBM_BYTES
     host_capacity: Optional[float] = None                          # node RAM available (bytes)
     units: Optional[Dict[str, float]] = None                       # FSDP partition facts
+    # ranks whose host memory THIS machine holds for the run at hand: world on a real node, 1 for a
+    # one-process proxy of rank 0 (bench.py --proxy-world); host_total_node always covers every rank
+    host_ranks_here: Optional[int] = None
 
     @property
     def hbm_total(self) -> float:
@@ -59,8 +62,10 @@ class MemoryPlan:
         if self.hbm_total > self.hbm_capacity:
             out.append(f"HBM: needs {self.hbm_total / GiB:.1f} GiB per rank, the GPU has "
                        f"{self.hbm_capacity / GiB:.1f} GiB ({self._top(self.hbm_per_rank)})")
-        if self.host_capacity is not None and self.host_total_node > self.host_capacity:
-            out.append(f"host RAM: needs {self.host_total_node / GiB:.1f} GiB pinned across {self.world} ranks, "
+        here = self.host_ranks_here if self.host_ranks_here is not None else self.world
+        need = sum(self.host_per_rank.values()) * here
+        if self.host_capacity is not None and need > self.host_capacity:
+            out.append(f"host RAM: needs {need / GiB:.1f} GiB pinned across {here} ranks, "
                        f"{self.host_capacity / GiB:.1f} GiB available ({self._top(self.host_per_rank)} per rank)")
         return out
 
@@ -75,7 +80,10 @@ class MemoryPlan:
     def to_dict(self) -> dict:
         d = asdict(self)
         d["hbm_total_gib"] = round(self.hbm_total / GiB, 2)
-        d["host_total_node_gib"] = round(self.host_total_node / GiB, 2)
+        d["host_total_node_gib"] = round(self.host_total_node / GiB, 2)  # every rank of the job
+        d["host_per_rank_gib"] = round(sum(self.host_per_rank.values()) / GiB, 2)
+        d["host_capacity_gib"] = None if self.host_capacity is None else round(self.host_capacity / GiB, 1)
+        d["host_fits_full_node"] = self.host_capacity is None or self.host_total_node <= self.host_capacity
         d["fits"] = self.fits
         d["problems"] = self.problems()
         return d

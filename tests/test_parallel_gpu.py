@@ -214,11 +214,16 @@ def test_ddp_early_grad_norm_matches_full_norm(accum, bucket_mb):
         ddp.zero_grad()
 
 
-@pytest.mark.parametrize("resident", [0.0, 0.5])
-def test_fsdp_overlapped_offload_matches_serial_offload(resident):
+@pytest.mark.parametrize("resident,prefetch,proxy", [(0.0, 0, 0), (0.5, 0, 0), (0.0, 5, 0), (0.5, 4096, 0),
+                                                   (0.0, 5, 4), (1.0, 0, 4)])
+def test_fsdp_overlapped_offload_matches_serial_offload(resident, prefetch, proxy):
     """The per-unit offloaded AdamW issued on side streams at step() and waited for by each unit's
-    next forward (parallel/offload.py), with part of the moments HBM-resident, gives bit-identical
-    parameters, moments and losses to the serial after-backward stream (same kernel, same data)."""
+    next forward (parallel/offload.py), with part of the moments HBM-resident and the first
+    ``prefetch`` streamed chunks uploaded during the backward (a ring smaller than the chunk count:
+    slots reused within a step; larger: every chunk prefetched), gives the parameters, moments and
+    losses of the serial after-backward stream (same kernel, same data). ``proxy``: rank 0 of a
+    ``proxy``-rank job on one device, whose gathers of an updated unit run on a side stream (a
+    missing wait there let the forward read a half-written gather buffer)."""
     from gke_ray_train_amd.models.llama import LlamaForCausalLM, RMSNorm, get_config
     from gke_ray_train_amd.parallel.fsdp import FullyShardedDataParallel
     from gke_ray_train_amd.parallel.offload import OverlappedOffloadAdamW
@@ -235,11 +240,15 @@ def test_fsdp_overlapped_offload_matches_serial_offload(resident):
         torch.manual_seed(0)
         m = LlamaForCausalLM(cfg, device="meta", dtype=torch.bfloat16)
         f = FullyShardedDataParallel(m, param_init_fn=init, device="cuda", cpu_offload=True,
-                                     offload_chunk_elems=1 << 14)
-        opt = f.build_optimizer(lr=1e-3, overlap=overlap, resident_fraction=resident)
+                                     offload_chunk_elems=1 << 14, proxy_world=proxy)
+        opt = f.build_optimizer(lr=1e-3, overlap=overlap, resident_fraction=resident,
+                                prefetch_slots=prefetch if overlap else 0)
         assert isinstance(opt, OverlappedOffloadAdamW) == overlap
         if overlap:
-            assert (opt.resident_units > 0) == (resident > 0) and opt.resident_units < len(opt.segments)
+            assert (opt.resident_units > 0) == (resident > 0)
+            assert opt.resident_units < len(opt.segments) or resident == 1.0
+            assert opt.prefetch_slots == min(prefetch, len(opt.chunks))
+            assert prefetch == 0 or prefetch >= len(opt.chunks) or len(opt.chunks) > opt.nslot
         g = torch.Generator(device="cuda").manual_seed(4)
         losses = []
         for _ in range(4):

@@ -89,3 +89,27 @@ def test_bench_plan_only_cli():
     assert r.returncode == 0, r.stdout[-2000:]
     d = json.loads(r.stdout.strip().splitlines()[-1])["memory_plan"]
     assert d["model"] == "llama2-7b" and d["fits"] is True
+
+
+def test_proxy_host_ram_counts_one_rank_and_reports_the_node():
+    """A one-process proxy of rank 0 (bench.py --proxy-world 8) holds rank 0's pinned moments only:
+    the fit check counts one rank, while the plan still reports what the 8-rank node needs."""
+    cfg = get_config("llama3-70b")
+    plan = plan_memory(cfg, 8, "fsdp", offload=True, micro_batch=8, seq=1024, checkpointing=True,
+                       hbm_capacity=HBM, host_capacity=200 * GiB)
+    per_rank = plan.host_per_rank["adam_moments_fp32"]
+    assert 60 * GiB < per_rank < 70 * GiB  # 8 B x 70.6e9 / 8
+    assert not plan.fits and "across 8 ranks" in plan.problems()[0]  # the real node: 526 GiB > 200
+    plan.host_ranks_here = 1
+    assert plan.fits
+    d = plan.to_dict()
+    assert d["host_total_node_gib"] > 500 and d["host_fits_full_node"] is False
+    assert abs(d["host_per_rank_gib"] - per_rank / GiB) < 0.01
+
+
+def test_offload_prefetch_ring_sizing():
+    from gke_ray_train_amd.parallel.offload import PREFETCH_CAP_BYTES, prefetch_slots_for
+    chunk = 1 << 26  # 64 Mi elements: m + v = 512 MiB per slot
+    assert prefetch_slots_for(PREFETCH_CAP_BYTES, chunk) == 64
+    assert prefetch_slots_for(511 * (1 << 20), chunk) == 0
+    assert prefetch_slots_for(0, chunk) == 0
