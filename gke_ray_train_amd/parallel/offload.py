@@ -21,14 +21,14 @@ MI355X design:
   memory planner: the share of the moments that fits beside everything else;
 * gradient shards of a unit are zeroed on the update stream right after its update (FSDP's
   ``zero_grad`` would otherwise memset them on the compute stream while updates still read them);
-* PREFETCH into the backward window: the streamed moments use a ring of ``prefetch_slots`` device
-  chunk slots. When the last decoder unit's forward starts, the uploads of the first slots' chunks
-  (forward order: the units the next forward needs first) are issued, so they cross the host link
-  during the backward, when it is otherwise idle; ``step()`` then updates those chunks at once and
-  only the remaining chunks upload under the next forward, while the downloads run beside them
-  (full duplex) and may spill into the next backward. A slot is reused only after the download of
-  its previous chunk (event per slot), which also orders every upload after the previous step's
-  download of the same host range.
+* PREFETCH into the backward window: the first ``prefetch_slots`` streamed chunks (forward order:
+  the units the next forward needs first) own one device slot each; the remaining chunks share a
+  ring of NSLOT slots. When the last decoder unit's forward starts, the uploads of the owned slots
+  are issued, so they cross the host link during the backward, when it is otherwise idle;
+  ``step()`` then updates those chunks at once and only the remaining chunks upload under the next
+  forward, while the downloads run beside them (full duplex) and may spill into the next backward.
+  A slot is reused only after the download of its previous chunk (event per slot), which also
+  orders every upload after the previous step's download of the same host range.
 """
 from __future__ import annotations
 
@@ -71,8 +71,11 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         # streamed chunks in forward order: (unit, start, end) of the flat shard
         self.chunks = [(u, s, min(hi, s + self.chunk)) for u, lo, hi in self.segments if id(u) not in self.resident
                        for s in range(lo, hi, self.chunk)]
-        self.nslot = max(self.NSLOT, min(int(prefetch_slots), len(self.chunks)))
+        # slots 0 .. P-1 belong to the prefetched chunks 0 .. P-1 (one each: the next step's upload of
+        # chunk i waits only for this step's download of chunk i, among the first to finish); the
+        # remaining chunks share a ring of NSLOT slots behind them
         self.prefetch_slots = min(int(prefetch_slots), len(self.chunks))
+        self.nslot = self.prefetch_slots + self.NSLOT
         self._slot_free: List[Optional[torch.cuda.Event]] = [None] * self.nslot
         self._landed: Dict[int, torch.cuda.Event] = {}  # chunk index -> upload done (prefetched)
         fsdp._grad_zero_by_optimizer = True
@@ -152,7 +155,7 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
             else:
                 while ci < len(self.chunks) and self.chunks[ci][0] is u:
                     _, s, e = self.chunks[ci]
-                    slot = ci % self.nslot
+                    slot = self._slot(ci)
                     mb, vb = self._stage[slot]
                     landed = self._landed.pop(ci, None) or self._upload(ci)
                     with torch.cuda.stream(upd):
@@ -181,12 +184,16 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
             self._stage = [(torch.empty(self.chunk, device=dev), torch.empty(self.chunk, device=dev))
                            for _ in range(self.nslot)]
 
+    def _slot(self, ci: int) -> int:
+        P = self.prefetch_slots
+        return ci if ci < P else P + (ci - P) % self.NSLOT
+
     def _upload(self, ci: int) -> torch.cuda.Event:
         """Host -> device copy of streamed chunk ``ci`` into its slot on the upload stream, after the
         slot's previous download."""
         up = self._streams[0]
         _, s, e = self.chunks[ci]
-        slot = ci % self.nslot
+        slot = self._slot(ci)
         mb, vb = self._stage[slot]
         sst = self.state[self.param_groups[0]["params"][0]]
         with torch.cuda.stream(up):

@@ -4,7 +4,7 @@
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/${1:-r5basicllm}; rm -rf $OUT; mkdir -p $OUT
 cd /tmp
-timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bl -- python3 -u $GRAFT_REPO_ROOT/jobs/pytorch_llm_ray.py --workers 1 --max-windows ${WINDOWS:-3200} > $OUT/job.log 2>&1; rc=$?
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o bl -- python3 -u $GRAFT_REPO_ROOT/tools/basicllm_inproc.py --max-windows ${WINDOWS:-3200} > $OUT/job.log 2>&1; rc=$?
 tail -5 $OUT/job.log; [ $rc = 0 ] || { echo "rc=$rc"; exit $rc; }
 cd $GRAFT_REPO_ROOT && python3 tools/prof_steps.py --help > /dev/null 2>&1
 find $OUT/prof -name "*kernel_stats.csv" | head -3

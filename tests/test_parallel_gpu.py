@@ -131,6 +131,32 @@ def test_overlapped_optimizer_matches_serial(transpose, monkeypatch):
             assert d < 2e-2 * max(1.0, v.float().abs().max().item()), (k, d)
 
 
+def test_overlapped_optimizer_lr_scheduler_sees_the_step():
+    """An LR scheduler bound to the inner optimizer (trainer/sft.py) must not warn
+    "lr_scheduler.step() before optimizer.step()": the overlapped step marks the inner optimizer."""
+    import warnings
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.ops import FusedAdamW, clip_grad_norm_
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    from gke_ray_train_amd.parallel.overlap import OverlappedOptimizer
+    m = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=5)
+    ddp = DistributedDataParallel(m)
+    inner = FusedAdamW(ddp.optimizer_param_groups(0.01), lr=1e-3)
+    sched = torch.optim.lr_scheduler.LambdaLR(inner, lambda s: 1.0 / (1 + s))
+    opt = OverlappedOptimizer(ddp, inner)
+    ids = torch.randint(0, m.config.vocab_size, (2, 64), device="cuda")
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        for _ in range(2):
+            ddp(ids, labels=ids)["loss"].backward()
+            ddp.finish_gradient_sync()
+            opt.step(grad_scale=clip_grad_norm_(ddp.grad_buffers(), 0.5))
+            sched.step()
+            ddp.zero_grad()
+    opt.synchronize()
+    assert abs(inner.param_groups[0]["lr"] - 1e-3 / 3) < 1e-9
+
+
 def test_sequence_parallel_single_rank_matches_plain_on_gpu():
     """Ulysses path on the GPU (RoPE at absolute positions through the HIP kernel's position array,
     all-to-all degenerate at P=1, flash kernel) == the fused rope_attention path."""
