@@ -8,11 +8,14 @@ links of ~153 GB/s, one to every peer. A single ring uses ONE outbound link per 
 all-reduce of B bytes costs ~2(p-1)/p * B / 153 GB/s; RCCL recovers the other links by running
 several channels over different ring permutations, which needs messages large enough to give
 every channel multi-MB chunks. Bucket sizing therefore trades:
-  * per-collective fixed cost (launch + channel setup, tens of µs) -> wants FEW, LARGE buckets;
-  * exposed tail: the last bucket's transfer cannot overlap backward -> wants a small last bucket.
-``plan_bucket_bytes`` picks ~1/32 of the gradient bytes clamped to [32 MiB, 256 MiB] (a 7B bf16
-model -> 256 MiB buckets, ~54 all-reduces/step; a 125M model -> 32 MiB), and ``RCCL_*`` knobs
-are left to RCCL's own tuner unless the user sets them.
+  * per-collective fixed cost alpha (launch + channel setup, tens of µs) -> wants FEW, LARGE buckets;
+  * exposed tail: the last bucket's transfer b / beta cannot overlap backward -> wants a SMALL last
+    bucket.
+``plan_bucket_bytes`` minimises (G / b) alpha + b / beta over the bucket size b for G gradient
+bytes: b* = sqrt(G alpha beta), clamped to [16 MiB, 1 GiB]. alpha / beta per collective come from a
+calibration file measured on the node (``tools/rccl_calibrate.py`` under torchrun writes it;
+``GRT_COMM_CALIBRATION=<path>``), else from the xGMI prior below (not a measurement). ``RCCL_*``
+knobs are left to RCCL's own tuner unless the user sets them.
 """
 from __future__ import annotations
 
@@ -26,14 +29,46 @@ XGMI_LINK_GBPS = 153.0
 XGMI_LINKS = 7
 
 
-def plan_bucket_bytes(total_grad_bytes: int, world_size: int) -> int:
+# Prior for 8 MI355X over xGMI when no calibration file is given: ~30 µs per collective, bus
+# bandwidth ~ 7 links x ~50 GB/s of usable ring throughput. Algorithm bandwidth = bytes of the
+# collective's input per second: all-reduce busbw * W / (2 (W - 1)), reduce-scatter / all-gather
+# busbw * W / (W - 1).
+PRIOR_ALPHA_US = 30.0
+PRIOR_BUSBW_GBPS = 350.0
+
+
+def _prior(op: str, world: int) -> dict:
+    w = max(world, 2)
+    scale = w / (2.0 * (w - 1)) if op == "all_reduce" else w / (w - 1.0)
+    return {"alpha_us": PRIOR_ALPHA_US, "beta_GBps": PRIOR_BUSBW_GBPS * scale, "source": "prior"}
+
+
+def comm_model(op: str, world: int) -> dict:
+    """alpha (µs) / beta (GB/s of collective input) for ``op`` at ``world`` ranks: the calibration
+    file's entry for the nearest measured world size, else the prior."""
+    path = os.environ.get("GRT_COMM_CALIBRATION")
+    if path and os.path.exists(path):
+        import json
+        with open(path) as f:
+            cal = json.load(f)
+        ent = cal.get(op)
+        if ent and ent.get("beta_GBps", 0) > 0:
+            return {"alpha_us": float(ent["alpha_us"]), "beta_GBps": float(ent["beta_GBps"]),
+                    "source": path, "world": cal.get("world")}
+    return _prior(op, world)
+
+
+def plan_bucket_bytes(total_grad_bytes: int, world_size: int, op: str = "all_reduce") -> int:
     env = os.environ.get("GRT_BUCKET_MB")
     if env:
         return int(float(env) * 2 ** 20)
     if world_size <= 1:
         return max(total_grad_bytes, 1)
-    lo, hi = 32 * 2 ** 20, 256 * 2 ** 20
-    return int(min(hi, max(lo, total_grad_bytes // 32)))
+    m = comm_model(op, world_size)
+    best = (float(total_grad_bytes) * m["alpha_us"] * 1e-6 * m["beta_GBps"] * 1e9) ** 0.5
+    lo, hi = 16 * 2 ** 20, 2 ** 30
+    b = min(hi, max(lo, best))
+    return int(b // (8 * 2 ** 20) * (8 * 2 ** 20)) if b >= 8 * 2 ** 20 else int(b)
 
 
 def ring_allreduce_seconds(nbytes: float, world: int, links: int = 1, link_gbps: float = XGMI_LINK_GBPS) -> float:

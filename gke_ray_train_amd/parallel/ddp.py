@@ -202,7 +202,8 @@ class DistributedDataParallel(nn.Module):
         elif self._early_norm and not os.environ.get("GRT_BUCKET_MB"):
             self.bucket_bytes = 256 * 2 ** 20  # norm granularity only: no collectives on one GPU
         else:
-            self.bucket_bytes = plan_bucket_bytes(total_bytes, max(self.world_size, 2 if self.comm else 1))
+            self.bucket_bytes = plan_bucket_bytes(total_bytes, max(self.world_size, 2 if self.comm else 1),
+                                                  "reduce_scatter" if (shard_optimizer and self.comm) else "all_reduce")
         # group by (dtype, decay), reverse registration order inside each group
         groups: Dict[tuple, List[tuple]] = {}
         for n, p in named:

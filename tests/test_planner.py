@@ -113,3 +113,34 @@ def test_offload_prefetch_ring_sizing():
     assert prefetch_slots_for(PREFETCH_CAP_BYTES, chunk) == 64
     assert prefetch_slots_for(511 * (1 << 20), chunk) == 0
     assert prefetch_slots_for(0, chunk) == 0
+
+
+def test_bucket_plan_cost_model_and_calibration_file(tmp_path, monkeypatch):
+    """Bucket size = argmin (G / b) alpha + b / beta = sqrt(G alpha beta), clamped; alpha / beta from
+    a calibration file written by tools/rccl_calibrate.py (run here over gloo, 2 ranks)."""
+    from gke_ray_train_amd.parallel.comm import comm_model, plan_bucket_bytes
+    monkeypatch.delenv("GRT_BUCKET_MB", raising=False)
+    monkeypatch.delenv("GRT_COMM_CALIBRATION", raising=False)
+    G = 13_476_831_232  # Llama-2-7B bf16 gradient bytes
+    m = comm_model("all_reduce", 8)
+    assert m["source"] == "prior"
+    b = plan_bucket_bytes(G, 8)
+    assert abs(b - (G * m["alpha_us"] * 1e-6 * m["beta_GBps"] * 1e9) ** 0.5) <= 8 * 2 ** 20
+    assert plan_bucket_bytes(G, 8, "reduce_scatter") > b  # reduce-scatter moves half the bytes
+    assert plan_bucket_bytes(10 ** 6, 8) == 16 * 2 ** 20 and plan_bucket_bytes(10 ** 13, 8) == 2 ** 30
+    assert plan_bucket_bytes(G, 1) == G
+    out = tmp_path / "cal.json"
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(29500 + os.getpid() % 1000),
+                        os.path.join(ROOT, "tools", "rccl_calibrate.py"), "--device", "cpu", "--out", str(out),
+                        "--min-kib", "64", "--max-mib", "4", "--reps", "3"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    cal = json.loads(out.read_text())
+    assert cal["world"] == 2 and cal["all_reduce"]["beta_GBps"] > 0 and cal["all_reduce"]["alpha_us"] >= 0
+    monkeypatch.setenv("GRT_COMM_CALIBRATION", str(out))
+    m2 = comm_model("all_reduce", 8)
+    assert m2["source"] == str(out) and m2["beta_GBps"] == cal["all_reduce"]["beta_GBps"]
+    b2 = plan_bucket_bytes(G, 8)
+    assert 16 * 2 ** 20 <= b2 <= 2 ** 30
