@@ -8,4 +8,5 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 tail -5 $OUT/job.log; [ $rc = 0 ] || { echo "rc=$rc"; exit $rc; }
 cd $GRAFT_REPO_ROOT && python3 tools/prof_steps.py --help > /dev/null 2>&1
 find $OUT/prof -name "*kernel_stats.csv" | head -3
-f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); head -25 "$f" | cut -c1-300
+f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); cp "$f" $OUT/kernel_stats.csv; head -25 "$f" | cut -c1-300
+rm -rf $OUT/prof

@@ -7,3 +7,6 @@ cd /tmp
 timeout -k 10 500 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv -d $OUT/prof -o off -- python3 -u $GRAFT_REPO_ROOT/bench.py --model llama3-70b --parallel fsdp --offload --proxy-world 8 --checkpointing --steps 2 --warmup 1 --offload-resident ${RES:-0} --offload-prefetch-gib ${PF:-auto} > $OUT/bench.log 2>&1; rc=$?
 tail -1 $OUT/bench.log | cut -c1-300; [ $rc = 0 ] || { echo "rc=$rc"; exit $rc; }
 cd $GRAFT_REPO_ROOT && python3 tools/offload_timeline.py $OUT/prof > $OUT/timeline.md 2>&1; cat $OUT/timeline.md | head -60
+f=$(find $OUT/prof -name "*kernel_stats.csv" | head -1); cp "$f" $OUT/kernel_stats.csv; head -12 $OUT/kernel_stats.csv | cut -c1-160
+f=$(find $OUT/prof -name "*memory_copy_stats.csv" | head -1); [ -n "$f" ] && cp "$f" $OUT/memory_copy_stats.csv && cat $OUT/memory_copy_stats.csv
+rm -rf $OUT/prof  # raw traces exceed what gpurun copies back

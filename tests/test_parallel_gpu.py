@@ -296,3 +296,52 @@ def test_fsdp_overlapped_offload_matches_serial_offload(resident, prefetch, prox
     for a, b in zip(runs[0][3], runs[1][3]):
         d = (a.cpu() - b.cpu()).abs().max().item()
         assert d <= 1e-2 * max(1e-6, a.abs().max().item()), d
+
+
+@pytest.mark.parametrize("resident,prefetch", [(0.0, 3), (0.5, 0)])
+def test_overlapped_offload_optimizer_resume_continues_identically(resident, prefetch):
+    """Checkpoint / resume of the overlapped offloaded AdamW: after load_state_dict the
+    moments are fp32 pinned host tensors again (resident units re-uploaded on first use), and two
+    more steps give the parameters of the uninterrupted run."""
+    from gke_ray_train_amd.models.llama import LlamaForCausalLM, RMSNorm, get_config
+    from gke_ray_train_amd.parallel.fsdp import FullyShardedDataParallel
+    cfg = get_config("llama-tiny-gqa")
+
+    def init(mod):
+        with torch.no_grad():
+            if isinstance(mod, (torch.nn.Linear, torch.nn.Embedding)):
+                mod.weight.normal_(0, 0.02)
+            elif isinstance(mod, RMSNorm):
+                mod.weight.fill_(1.0)
+
+    def build():
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(cfg, device="meta", dtype=torch.bfloat16)
+        f = FullyShardedDataParallel(m, param_init_fn=init, device="cuda", cpu_offload=True,
+                                     offload_chunk_elems=1 << 14)
+        return f, f.build_optimizer(lr=1e-3, overlap=True, resident_fraction=resident, prefetch_slots=prefetch)
+
+    g = torch.Generator(device="cuda").manual_seed(11)
+    batches = [torch.randint(0, cfg.vocab_size, (2, 64), device="cuda", generator=g) for _ in range(4)]
+    f1, o1 = build()
+    for ids in batches[:2]:
+        _step(f1, o1, ids)
+    import copy
+    sd_opt = copy.deepcopy(o1.state_dict())  # as if saved: torch's state_dict aliases the live moments
+    sd_par = {k: v.clone() for k, v in f1.sharded_state_dict().items()}
+    for ids in batches[2:]:
+        _step(f1, o1, ids)
+    o1.synchronize()
+    f2, o2 = build()
+    f2.load_sharded_state_dict(sd_par)
+    o2.load_state_dict(sd_opt)
+    for st in o2.state.values():
+        for k in ("exp_avg", "exp_avg_sq"):
+            if k in st:
+                assert st[k].dtype == torch.float32 and st[k].device.type == "cpu" and st[k].is_pinned(), k
+    for ids in batches[2:]:
+        _step(f2, o2, ids)
+    o2.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(f1.shard_store, f2.shard_store)
+    assert torch.equal(f1.rep_flat, f2.rep_flat)

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Host link of one MI355X as the offloaded optimizer uses it: pinned host <-> HBM copies of 512 MiB
+chunks (torch ``copy_(non_blocking=True)`` on side streams, as parallel/offload.py issues them),
+alone, both directions at once, and beside a GEMM loop on the compute stream (the GEMM's slowdown is
+what an overlapped copy costs the step). Under ``rocprofv3 --kernel-trace --memory-copy-trace`` the
+trace shows which engine each direction uses (SDMA copies vs ``__amd_rocclr_copyBuffer`` blit
+kernels on the CUs).
+
+    python tools/hostlink_bench.py [--mib 512] [--reps 4] [--wg 128]
+
+``stream_copy`` rows: the same device -> host copy as a kernel of ours (csrc/kernels/optim.hip)
+with 32-512 workgroups, plain or non-temporal stores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mib", type=int, default=512)
+    ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--wg", type=int, default=128, help="workgroups of the kernel D2H in the overlap runs")
+    a = ap.parse_args()
+    n = a.mib * 2 ** 20 // 4
+    dev = torch.device("cuda")
+    h_src = torch.ones(n, dtype=torch.float32).pin_memory()
+    h_dst = torch.empty(n, dtype=torch.float32).pin_memory()
+    d_a = torch.empty(n, device=dev)
+    d_b = torch.ones(n, device=dev)
+    up, down = torch.cuda.Stream(), torch.cuda.Stream()
+    nbytes = n * 4
+    out = {"chunk_mib": a.mib}
+
+    def timed(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
+    def h2d():
+        with torch.cuda.stream(up):
+            for _ in range(a.reps):
+                d_a.copy_(h_src, non_blocking=True)
+
+    def d2h():
+        with torch.cuda.stream(down):
+            for _ in range(a.reps):
+                h_dst.copy_(d_b, non_blocking=True)
+
+    h2d(), d2h()  # warm
+    t = timed(h2d)
+    out["h2d_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
+    t = timed(d2h)
+    out["d2h_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
+    t = timed(lambda: (h2d(), d2h()))
+    out["duplex_total_GBps"] = round(2 * a.reps * nbytes / t / 1e9, 1)
+
+    from gke_ray_train_amd import _native
+    C = _native.kernels()
+    for nb in (32, 128, 512):
+        for nt in (False, True):
+            def kd2h(nb=nb, nt=nt):
+                with torch.cuda.stream(down):
+                    for _ in range(a.reps):
+                        C.stream_copy(d_b, h_dst, nb, nt)
+            kd2h()
+            t = timed(kd2h)
+            out[f"kernel_d2h_wg{nb}_nt{int(nt)}_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
+    h_dst.zero_()
+    C.stream_copy(d_b, h_dst, 128, True)
+    torch.cuda.synchronize()
+    out["kernel_d2h_exact"] = bool(torch.equal(h_dst, d_b.cpu()))
+
+    def kd2h_best():
+        with torch.cuda.stream(down):
+            for _ in range(a.reps):
+                C.stream_copy(d_b, h_dst, a.wg, True)
+    t = timed(lambda: (h2d(), kd2h_best()))
+    out[f"duplex_sdma_h2d_kernel_d2h_wg{a.wg}_total_GBps"] = round(2 * a.reps * nbytes / t / 1e9, 1)
+
+    x = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    y = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
+    z = torch.empty(8192, 8192, device=dev, dtype=torch.bfloat16)
+
+    def gemms(k=40):
+        for _ in range(k):
+            torch.mm(x, y, out=z)
+
+    gemms(5)
+    tg = timed(gemms)
+    out["gemm_alone_ms"] = round(tg * 1e3, 1)
+    for name, fn in (("h2d", h2d), ("d2h", d2h), ("both", lambda: (h2d(), d2h())),
+                     ("kernel_d2h", kd2h_best), ("h2d_and_kernel_d2h", lambda: (h2d(), kd2h_best()))):
+        def run():
+            fn()
+            gemms()
+        torch.cuda.synchronize()
+        t = timed(run)
+        out[f"gemm_with_{name}_ms"] = round(t * 1e3, 1)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -61,10 +61,12 @@ def main(d):
         dirn = r.get("Direction") or r.get("Kind") or "?"
         size = int(r.get("Bytes") or r.get("Size") or 0)
         copies.setdefault(dirn, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), size))
-    print(f"copy directions: {sorted(copies)}; steps found: {max(0, len(starts) - 1)}\n")
-    print("| step | wall ms | kernel busy ms | fwd window ms | " +
+    print(f"copy directions: {sorted(copies)}; steps found: {max(0, len(starts) - 1)}; "
+          f"copy trace columns: {list(cs[0].keys()) if cs else []}\n")
+    blits = [(s, e) for s, e, n in kiv if "copyBuffer" in n]
+    print("| step | wall ms | kernel busy ms | blit-copy kernel busy ms | fwd window ms | " +
           " | ".join(f"{k} GB / busy ms / GB/s / in fwd window ms" for k in sorted(copies)) + " |")
-    print("|---|---|---|---|" + "---|" * len(copies))
+    print("|---|---|---|---|---|" + "---|" * len(copies))
     for i in range(len(starts) - 1):
         lo, hi = starts[i], starts[i + 1]
         b0 = next((s for s in bwd if s > lo), hi)
@@ -76,7 +78,9 @@ def main(d):
             busy = _busy(iv, lo, hi)
             fw = _busy(iv, lo, b0)
             cells.append(f"{by / 1e9:.1f} / {busy / 1e6:.0f} / {by / max(busy, 1):.1f} / {fw / 1e6:.0f}")
-        print(f"| {i} | {(hi - lo) / 1e6:.0f} | {kb / 1e6:.0f} | {(b0 - lo) / 1e6:.0f} | " + " | ".join(cells) + " |")
+        bb = _busy(blits, lo, hi)
+        print(f"| {i} | {(hi - lo) / 1e6:.0f} | {kb / 1e6:.0f} | {bb / 1e6:.0f} | {(b0 - lo) / 1e6:.0f} | "
+              + " | ".join(cells) + " |")
     return 0
 
 
