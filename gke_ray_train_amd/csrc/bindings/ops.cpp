@@ -685,8 +685,7 @@ void scale_(Tensor& x, double a, const optional<Tensor>& a_ptr) {
 // dst.copy_(src) by a kernel when one side is pinned host memory (device-mapped): the moment
 // write-back of the offloaded optimizer (ops/optim.py, parallel/offload.py)
 void stream_copy(const Tensor& src, Tensor& dst, int64_t nblocks, bool nt) {
-  check_contig(src, "src");
-  check_contig(dst, "dst");
+  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous(), "stream_copy: contiguous operands");
   const int64_t nbytes = src.numel() * src.element_size();
   TORCH_CHECK(dst.numel() * dst.element_size() == nbytes, "stream_copy: size mismatch");
   TORCH_CHECK(nbytes % 16 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
@@ -781,7 +780,8 @@ void set_dropout(grt::AttnParams& p, double dropout_p, int64_t seed) {
 
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, const optional<Tensor>& out,
                              double scale, bool causal, const optional<Tensor>& seqlens_k, double dropout_p,
-                             int64_t seed, const optional<Tensor>& cu_seqlens, int64_t max_seqlen) {
+                             int64_t seed, const optional<Tensor>& cu_seqlens, int64_t max_seqlen,
+                             const optional<Tensor>& o_t) {
   c10::OptionalDeviceGuard g(q.device());
   Tensor o = out.has_value() ? *out : at::empty(q.sizes(), q.options());
   auto lse = cu_seqlens.has_value()
@@ -789,6 +789,14 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
                  : at::empty({q.size(0), q.size(2), q.size(1)}, q.options().dtype(at::kFloat));
   auto p = make_params(q, k, v, o, lse, scale, causal, seqlens_k, cu_seqlens, max_seqlen);
   set_dropout(p, dropout_p, seed);
+  if (o_t.has_value()) {  // transposed output [Hq * D, B * S] beside o (o projection's weight gradient)
+    check_contig(*o_t, "o_t");
+    TORCH_CHECK(q.scalar_type() == at::kBFloat16 && p.D == 128 && o_t->scalar_type() == at::kBFloat16 &&
+                    o_t->dim() == 2 && o_t->size(0) == (int64_t)p.Hq * p.D && o_t->size(1) == q.size(0) * q.size(1),
+                "attn_fwd o_t: bf16, head_dim 128, shape [Hq * D, B * S]");
+    p.o_t = o_t->data_ptr();
+    p.ot_ld = o_t->size(1);
+  }
   if (q.scalar_type() == at::kFloat) grt::attn_fwd_f32(p, cur_stream(q));
   else grt::attn_fwd(p, cur_stream(q));
   return {o, lse};
@@ -799,7 +807,7 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
                              const optional<Tensor>& dv_out, double scale, bool causal,
                              const optional<Tensor>& seqlens_k, double dropout_p, int64_t seed,
                              const optional<Tensor>& rope_cos, const optional<Tensor>& rope_sin,
-                             const optional<Tensor>& cu_seqlens, int64_t max_seqlen) {
+                             const optional<Tensor>& cu_seqlens, int64_t max_seqlen, const optional<Tensor>& dqkv_t) {
   c10::OptionalDeviceGuard g(q.device());
   check_bshd(dout, "dout");
   TORCH_CHECK(dout.sizes() == q.sizes(), "dout shape");
@@ -835,6 +843,19 @@ std::vector<Tensor> attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& 
   }
   TORCH_CHECK(dout.scalar_type() == q.scalar_type() && dq.scalar_type() == q.scalar_type() &&
                   dk.scalar_type() == q.scalar_type() && dv.scalar_type() == q.scalar_type(), "grad dtype mismatch");
+  if (dqkv_t.has_value()) {  // transposed fused-QKV gradient [(Hq + 2 Hkv) D, B * S] beside dq / dk / dv
+    check_contig(*dqkv_t, "dqkv_t");
+    TORCH_CHECK(q.scalar_type() == at::kBFloat16 && p.D == 128 && dqkv_t->scalar_type() == at::kBFloat16,
+                "attn_bwd dqkv_t: bf16, head_dim 128");
+    TORCH_CHECK(p.Sq == p.Sk && dqkv_t->dim() == 2 && dqkv_t->size(0) == (int64_t)(p.Hq + 2 * p.Hkv) * p.D &&
+                    dqkv_t->size(1) == q.size(0) * q.size(1),
+                "attn_bwd dqkv_t: self-attention, shape [(Hq + 2 Hkv) * D, B * S]");
+    bp.dqkv_t = dqkv_t->data_ptr();
+    bp.t_ld = dqkv_t->size(1);
+    bp.t_row_q = 0;
+    bp.t_row_k = p.Hq * p.D;
+    bp.t_row_v = (p.Hq + p.Hkv) * p.D;
+  }
   if (q.scalar_type() == at::kFloat) grt::attn_bwd_f32(bp, cur_stream(q));
   else grt::attn_bwd(bp, cur_stream(q));
   return {dq, dk, dv};
@@ -1246,11 +1267,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stream_copy", &stream_copy, py::arg("src"), py::arg("dst"), py::arg("nblocks") = 64, py::arg("nt") = true);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("scale"),
         py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0,
-        py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0);
+        py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0, py::arg("o_t") = py::none());
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("o"),
         py::arg("lse"), py::arg("dq"), py::arg("dk"), py::arg("dv"), py::arg("scale"), py::arg("causal"),
         py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0, py::arg("rope_cos") = py::none(),
-        py::arg("rope_sin") = py::none(), py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0);
+        py::arg("rope_sin") = py::none(), py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0,
+        py::arg("dqkv_t") = py::none());
   m.def("attn_set_schedule", &grt::attn_set_schedule,
         "bf16 attention causal-pair / XCD-grouped schedule, bit mask: 1 = forward, 2 = dQ, 4 = dK/dV");
   m.def("attn_get_schedule", &grt::attn_get_schedule);

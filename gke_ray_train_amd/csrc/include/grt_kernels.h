@@ -196,6 +196,9 @@ struct AttnParams {
   // sequence take their LDS-DMA source addresses as a uniform tile base + per-lane offsets fixed for
   // the sweep (one 64-bit add per DMA) instead of the clamped per-lane row arithmetic
   int dma_fast;
+  // optional (bf16 forward, D = 128): the output also written transposed, o_t[(hq D + d) * ot_ld + token]
+  // ([Hq D, tokens]) for the o projection's TN weight gradient
+  void* o_t; int64_t ot_ld;
 };
 void attn_set_schedule(int s);
 int attn_get_schedule();
@@ -213,6 +216,10 @@ struct AttnBwdParams {
   // optional (bf16 kernels, D = 128): q / k were RoPE-rotated at position = sequence index; the
   // epilogues write dQ / dK already un-rotated (cos / sin fp32 [>= max(Sq, Sk), D / 2])
   const float* rope_cos; const float* rope_sin;
+  // optional (bf16 kernels, self-attention over a fused QKV gradient): the epilogues also write the
+  // transposed gradient dqkv^T [(Hq + 2 Hkv) D, tokens] (row stride t_ld = tokens) for the TN weight
+  // gradient of the QKV projection; rows t_row_q / t_row_k / t_row_v start the Q / K / V sections
+  void* dqkv_t; int64_t t_ld; int t_row_q, t_row_k, t_row_v;
 };
 void attn_bwd(const AttnBwdParams& p, hipStream_t s);
 int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int D);

@@ -390,8 +390,20 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
       }
       const auto r0 = __builtin_amdgcn_permlane32_swap(a.u[0], c2.u[0], false, false);
       const auto r1 = __builtin_amdgcn_permlane32_swap(a.u[1], c2.u[1], false, false);
-      if (myq < Sq)
+      if (myq < Sq) {
         *reinterpret_cast<uint4*>(O + db * 32 + 16 * gp + 8 * h) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+        if (p.o_t != nullptr) {  // O^T: this lane's row, head dims d of a (before the swap): one 64-B
+          // segment per element across the 32 lanes of a half-wave
+          bf16* ot = static_cast<bf16*>(p.o_t) + (int64_t)(hq * D) * p.ot_ld + (p.cu_seqlens ? 0 : (int64_t)b * p.Sq) +
+                     tok0 + myq;
+          const int d0 = db * 32 + 8 * (2 * gp) + 4 * h, d1 = db * 32 + 8 * (2 * gp + 1) + 4 * h;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            ot[(int64_t)(d0 + j) * p.ot_ld] = a.v[j];
+            ot[(int64_t)(d1 + j) * p.ot_ld] = c2.v[j];
+          }
+        }
+      }
     }
   if (myq < Sq) {
     if (h == 0 && p.lse)
@@ -460,8 +472,28 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(const AttnBwdParams p
 // (db, 4 gg + j) is head dim d = 32 db + 8 gg + 4 h + j, so the rotation pair (d, d + 64) is
 // (db, db + 2) of the same lane — x1 c + x2 s / x2 c - x1 s with the position's cos / sin rows
 // (rope_kernel<.., false>), rounded to bf16 once.
+// Optional transposed copy of a [tokens, heads x D] gradient for the TN weight-gradient GEMM of the
+// fused QKV projection (the producer writes dqkv^T beside dqkv, so no transpose kernel re-reads it):
+// element (token, d) of this lane's row at p[d * ld]; p == nullptr when not requested. The 32
+// lanes of a half-wave hold 32 consecutive tokens, so each element store is one 64-byte segment.
+struct TCopy {
+  bf16* p;
+  int64_t ld;
+};
+__device__ __forceinline__ void st_t(const TCopy& tc, int d, const bf16x4& v) {
+  if (tc.p != nullptr) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) tc.p[(int64_t)(d + j) * tc.ld] = v[j];
+  }
+}
+__device__ __forceinline__ TCopy tcopy(const AttnBwdParams& P, int row0, int head, int64_t tok) {
+  if (P.dqkv_t == nullptr) return TCopy{nullptr, 0};
+  return TCopy{static_cast<bf16*>(P.dqkv_t) + (int64_t)(row0 + head * D) * P.t_ld + tok, P.t_ld};
+}
+
 __device__ __forceinline__ void store_unrotated(const f32x16 (&acc)[4], float scale, const float* __restrict__ cr,
-                                                const float* __restrict__ sr, bf16* dst, int h) {
+                                                const float* __restrict__ sr, bf16* dst, int h,
+                                                const TCopy& tc = TCopy{nullptr, 0}) {
 #pragma unroll
   for (int db = 0; db < 2; ++db)
 #pragma unroll
@@ -478,6 +510,8 @@ __device__ __forceinline__ void store_unrotated(const f32x16 (&acc)[4], float sc
       }
       *reinterpret_cast<bf16x4*>(dst + d) = lo;
       *reinterpret_cast<bf16x4*>(dst + d + D / 2) = hi;
+      st_t(tc, d, lo);
+      st_t(tc, d + D / 2, hi);
     }
 }
 
@@ -740,8 +774,11 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
   if (mykey < Sk) {
     bf16* dK = (bf16*)P.dk + (int64_t)b * P.dk_bs + (int64_t)hkv * P.dk_hs + (tok0 + mykey) * P.dk_ss;
     bf16* dV = (bf16*)P.dv + (int64_t)b * P.dv_bs + (int64_t)hkv * P.dv_hs + (tok0 + mykey) * P.dv_ss;
+    const int64_t tokg = (p.cu_seqlens ? 0 : (int64_t)b * p.Sk) + tok0 + mykey;
+    const TCopy tk = tcopy(P, P.t_row_k, hkv, tokg), tv = tcopy(P, P.t_row_v, hkv, tokg);
     if (P.rope_cos)
-      store_unrotated(dk, p.scale, P.rope_cos + (int64_t)mykey * (D / 2), P.rope_sin + (int64_t)mykey * (D / 2), dK, h);
+      store_unrotated(dk, p.scale, P.rope_cos + (int64_t)mykey * (D / 2), P.rope_sin + (int64_t)mykey * (D / 2), dK, h,
+                      tk);
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
@@ -752,8 +789,12 @@ __global__ __launch_bounds__(K2NT, 1) void attn_bwd_dkdv_kernel(const AttnBwdPar
           a[j] = static_cast<bf16>(dk[db][4 * gg + j] * p.scale);
           v[j] = static_cast<bf16>(dv[db][4 * gg + j]);
         }
-        if (!P.rope_cos) *reinterpret_cast<bf16x4*>(dK + db * 32 + 8 * gg + 4 * h) = a;
+        if (!P.rope_cos) {
+          *reinterpret_cast<bf16x4*>(dK + db * 32 + 8 * gg + 4 * h) = a;
+          st_t(tk, db * 32 + 8 * gg + 4 * h, a);
+        }
         *reinterpret_cast<bf16x4*>(dV + db * 32 + 8 * gg + 4 * h) = v;
+        st_t(tv, db * 32 + 8 * gg + 4 * h, v);
       }
   }
   };
@@ -1010,8 +1051,10 @@ __global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdPa
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   if (mykey < Sk) {
+    const int64_t tokg = (p.cu_seqlens ? 0 : (int64_t)b * p.Sk) + tok0 + mykey;
     if constexpr (SW) {
       bf16* dV = (bf16*)P.dv + (int64_t)b * P.dv_bs + (int64_t)hkv * P.dv_hs + (tok0 + mykey) * P.dv_ss;
+      const TCopy tv = tcopy(P, P.t_row_v, hkv, tokg);
 #pragma unroll
       for (int db = 0; db < 4; ++db)
 #pragma unroll
@@ -1020,11 +1063,14 @@ __global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdPa
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(acc[db][4 * gg + j]);
           *reinterpret_cast<bf16x4*>(dV + db * 32 + 8 * gg + 4 * h) = v;
+          st_t(tv, db * 32 + 8 * gg + 4 * h, v);
         }
     } else {
       bf16* dK = (bf16*)P.dk + (int64_t)b * P.dk_bs + (int64_t)hkv * P.dk_hs + (tok0 + mykey) * P.dk_ss;
+      const TCopy tk = tcopy(P, P.t_row_k, hkv, tokg);
       if (P.rope_cos) {
-        store_unrotated(acc, p.scale, P.rope_cos + (int64_t)mykey * (D / 2), P.rope_sin + (int64_t)mykey * (D / 2), dK, h);
+        store_unrotated(acc, p.scale, P.rope_cos + (int64_t)mykey * (D / 2), P.rope_sin + (int64_t)mykey * (D / 2), dK, h,
+                        tk);
       } else {
 #pragma unroll
         for (int db = 0; db < 4; ++db)
@@ -1034,6 +1080,7 @@ __global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdPa
 #pragma unroll
             for (int j = 0; j < 4; ++j) a[j] = static_cast<bf16>(acc[db][4 * gg + j] * p.scale);
             *reinterpret_cast<bf16x4*>(dK + db * 32 + 8 * gg + 4 * h) = a;
+            st_t(tk, db * 32 + 8 * gg + 4 * h, a);
           }
       }
     }
@@ -1225,8 +1272,9 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
 
   if (qok) {
     bf16* dQ = (bf16*)P.dq + (int64_t)b * P.dq_bs + (int64_t)hq * P.dq_hs + (tok0 + myq) * P.dq_ss;
+    const TCopy tq = tcopy(P, P.t_row_q, hq, (p.cu_seqlens ? 0 : (int64_t)b * p.Sq) + tok0 + myq);
     if (P.rope_cos) {
-      store_unrotated(dq, p.scale, P.rope_cos + (int64_t)myq * (D / 2), P.rope_sin + (int64_t)myq * (D / 2), dQ, h);
+      store_unrotated(dq, p.scale, P.rope_cos + (int64_t)myq * (D / 2), P.rope_sin + (int64_t)myq * (D / 2), dQ, h, tq);
     } else {
 #pragma unroll
       for (int db = 0; db < 4; ++db)
@@ -1236,6 +1284,7 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = static_cast<bf16>(dq[db][4 * gg + j] * p.scale);
           *reinterpret_cast<bf16x4*>(dQ + db * 32 + 8 * gg + 4 * h) = v;
+          st_t(tq, db * 32 + 8 * gg + 4 * h, v);
         }
     }
   }

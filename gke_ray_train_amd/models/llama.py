@@ -156,7 +156,8 @@ class LlamaAttention(nn.Module):
             o = ulysses_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, sp, causal=True)
         else:
             o = ops.rope_attention(qkv, cos, sin, B, S, self.hq, self.hkv, self.hd, causal=True, varlen=varlen,
-                                   pad=_tail_pad(self.o_proj))
+                                   pad=_tail_pad(self.o_proj), bwd_t=_direct_wgrad(self.qkv_proj),
+                                   fwd_t=_direct_wgrad(self.o_proj))
         return self.o_proj(o)
 
 

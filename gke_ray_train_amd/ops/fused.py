@@ -331,6 +331,9 @@ class Varlen:
         return [b - a for a, b in zip(self.cu_host[:-1], self.cu_host[1:])]
 
 
+_ATTN_DQKV_T = os.environ.get("GRT_ATTN_DQKV_T", "1") != "0"
+
+
 class _RopeAttention(torch.autograd.Function):
     """qkv [B*S, (Hq + 2 Hkv) * D] -> o [B*S, Hq * D]: RoPE + causal flash attention fused.
 
@@ -340,8 +343,10 @@ class _RopeAttention(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen=None, pad=0):
+    def forward(ctx, qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen=None, pad=0, bwd_t=False, fwd_t=False):
         C = _native.kernels()
+        ctx.bwd_t = bwd_t
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the o^T output
         qkv = qkv.contiguous()
         cu, ml = (varlen.cu, varlen.max_len) if varlen is not None else (None, 0)
         q, k = C.rope_fwd(qkv, cos, sin, varlen.pos if varlen is not None else None, hq, hkv, D,
@@ -353,14 +358,18 @@ class _RopeAttention(torch.autograd.Function):
         ld = hq * D + pad
         ow = torch.empty(B * S, ld, device=qkv.device, dtype=qkv.dtype)
         o = ow.as_strided((B, S, hq, D), (S * ld, ld, D, 1))
-        _, lse = C.attn_fwd(q4, k4, v4, o, scale, causal, None, cu_seqlens=cu, max_seqlen=ml)
+        ot = (torch.empty(hq * D, B * S, device=qkv.device, dtype=qkv.dtype)
+              if fwd_t and (B * S) % 64 == 0 and (hq * D) % 64 == 0 else None)
+        _, lse = C.attn_fwd(q4, k4, v4, o, scale, causal, None, cu_seqlens=cu, max_seqlen=ml, o_t=ot)
         ctx.save_for_backward(qkv, q, k, o, lse, cos, sin)
         ctx.dims = (B, S, hq, hkv, D, causal, scale)
         ctx.varlen = varlen
-        return ow[:, :hq * D]
+        if ot is not None:
+            ctx.mark_non_differentiable(ot)
+        return ow[:, :hq * D], ot
 
     @staticmethod
-    def backward(ctx, do):
+    def backward(ctx, do, _dot=None):
         qkv, q, k, o, lse, cos, sin = ctx.saved_tensors
         B, S, hq, hkv, D, causal, scale = ctx.dims
         vl = ctx.varlen
@@ -374,24 +383,39 @@ class _RopeAttention(torch.autograd.Function):
         dv4 = d4[:, :, hq + hkv:, :]
         if _ROPE_BWD_FUSED and cos.dim() == 2 and cos.shape[0] >= (ml if vl is not None else S):
             # the kernels' epilogues undo the RoPE and write dQ / dK straight into dqkv's columns
-            # (packed: the key / query index inside its sequence IS its RoPE position)
+            # (packed: the key / query index inside its sequence IS its RoPE position); with bwd_t
+            # they also write dqkv^T for the QKV projection's TN weight gradient (ops/linear.py
+            # takes it from dqkv._grt_T instead of transposing dqkv)
+            T, W = dqkv.shape[0], dqkv.shape[1]
+            dqkv_t = (torch.empty(W, T, device=dqkv.device, dtype=dqkv.dtype)
+                      if ctx.bwd_t and T % 64 == 0 and W % 64 == 0 else None)
             C.attn_bwd(do.contiguous().view(B, S, hq, D), q4, k4, v4, o, lse, d4[:, :, :hq], d4[:, :, hq:hq + hkv],
-                       dv4, scale, causal, None, rope_cos=cos, rope_sin=sin, cu_seqlens=cu, max_seqlen=ml)
+                       dv4, scale, causal, None, rope_cos=cos, rope_sin=sin, cu_seqlens=cu, max_seqlen=ml,
+                       dqkv_t=dqkv_t)
+            if dqkv_t is not None:
+                dqkv._grt_T = dqkv_t
         else:
             dq, dk, _ = C.attn_bwd(do.contiguous().view(B, S, hq, D), q4, k4, v4, o, lse, None, None, dv4,
                                    scale, causal, None, cu_seqlens=cu, max_seqlen=ml)
             C.rope_bwd(dq, dk, dqkv, cos, sin, vl.pos if vl is not None else None, hq, hkv, D,
                        ml if vl is not None else S)
-        return dqkv, None, None, None, None, None, None, None, None, None, None, None
+        return dqkv, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def rope_attention(qkv, cos, sin, B, S, hq, hkv, D, causal=True, scale=None, varlen: "Varlen" = None,
-                   pad: int = 0):
+                   pad: int = 0, bwd_t: bool = False, fwd_t: bool = False):
     """``varlen``: the B*S rows are padding-free packed sequences (B = 1; see ``Varlen``).
-    ``pad`` as in ``rms_norm``: the o_proj's LoRA tail after each output row."""
+    ``pad`` as in ``rms_norm``: the o_proj's LoRA tail after each output row. ``bwd_t``: the
+    backward also writes dqkv^T for a trainable QKV projection's weight gradient, ``fwd_t``: the
+    forward also writes o^T for a trainable o projection's (GRT_ATTN_DQKV_T=0: neither)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if _gpu(qkv) and qkv.dtype == torch.bfloat16 and D == 128:
-        return _tail(_RopeAttention.apply(qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen, pad), pad)
+        bwd_t = bwd_t and _ATTN_DQKV_T
+        fwd_t = fwd_t and _ATTN_DQKV_T and not pad
+        o, ot = _RopeAttention.apply(qkv, cos, sin, B, S, hq, hkv, D, causal, scale, varlen, pad, bwd_t, fwd_t)
+        if ot is not None:
+            o._grt_T = ot
+        return _tail(o, pad)
     x = qkv.view(B * S, hq + 2 * hkv, D)
     pos = varlen.pos if varlen is not None else None
     q = _ref.apply_rope(x[:, :hq], cos, sin, pos)

@@ -1170,3 +1170,59 @@ def test_dkdv_wave_pair_matches_four_wave_kernel(B, S, hq, hkv, causal, pad, p, 
         C.attn_set_dkdv_form(2)
     for name, a, b in zip(("dq", "dk", "dv"), out[1], out[2]):
         assert torch.equal(a, b), f"{name}: max diff {(a.float() - b.float()).abs().max().item():.3g}"
+
+
+@pytest.mark.parametrize("B,S,hq,hkv,rope,form,varlen", [
+    (2, 256, 4, 4, True, 2, False),       # wave-pair dK / dV kernel, RoPE epilogue
+    (2, 256, 4, 2, False, 2, False),      # GQA, plain epilogue
+    (1, 192, 4, 2, True, 1, False),       # 4-wave dK / dV kernel, partial tail block
+    (1, 384, 4, 4, True, 2, True),        # padding-free packed sequences (cu_seqlens)
+    (8, 1024, 32, 32, True, 2, False),    # Llama-2-7B step shape
+])
+def test_attn_bwd_writes_transposed_dqkv(B, S, hq, hkv, rope, form, varlen):
+    """The epilogues' transposed copies — the forward's o^T (attn_fwd o_t, the o projection's TN
+    weight-gradient operand) and the backward's dqkv^T (attn_bwd dqkv_t, the QKV projection's) —
+    equal o^T / dqkv^T bit for bit, and the row-major outputs are unchanged by them."""
+    from gke_ray_train_amd import _native
+    from gke_ray_train_amd.ops import _ref
+    C = _native.kernels()
+    D = 128
+    g = torch.Generator(device=DEV).manual_seed(B * S + hq + form)
+    W = (hq + 2 * hkv) * D
+    qkv = torch.randn(B * S, W, device=DEV, dtype=torch.bfloat16, generator=g)
+    do = torch.randn(B, S, hq, D, device=DEV, dtype=torch.bfloat16, generator=g)
+    cu, ml, pos = None, 0, None
+    if varlen:
+        cu = torch.tensor([0, 100, 228, 384], device=DEV, dtype=torch.int32)
+        ml = 156
+        pos = torch.cat([torch.arange(b - a, device=DEV) for a, b in ((0, 100), (100, 228), (228, 384))]).int()
+    cos, sin = _ref.rope_tables(S, D, 10000.0, device=DEV)
+    cos, sin = cos.float().contiguous(), sin.float().contiguous()
+    q, k = C.rope_fwd(qkv, cos, sin, pos, hq, hkv, D, ml if varlen else S)
+    q4, k4 = q.view(B, S, hq, D), k.view(B, S, hkv, D)
+    v4 = qkv.view(B, S, hq + 2 * hkv, D)[:, :, hq + hkv:, :]
+    o = torch.empty(B, S, hq, D, device=DEV, dtype=torch.bfloat16)
+    o_t = torch.full((hq * D, B * S), float("nan"), device=DEV, dtype=torch.bfloat16)
+    _, lse = C.attn_fwd(q4, k4, v4, o, D ** -0.5, True, None, cu_seqlens=cu, max_seqlen=ml, o_t=o_t)
+    o2 = torch.empty_like(o)
+    C.attn_fwd(q4, k4, v4, o2, D ** -0.5, True, None, cu_seqlens=cu, max_seqlen=ml)
+    torch.cuda.synchronize()
+    assert torch.equal(o, o2)  # the transposed copy changes nothing in o
+    assert torch.equal(o_t, o.view(B * S, hq * D).t().contiguous())  # forward epilogue's o^T
+    outs = []
+    try:
+        C.attn_set_dkdv_form(form)
+        for with_t in (False, True):
+            dqkv = torch.full_like(qkv, float("nan"))
+            d4 = dqkv.view(B, S, hq + 2 * hkv, D)
+            dqkv_t = torch.full((W, B * S), float("nan"), device=DEV, dtype=torch.bfloat16) if with_t else None
+            C.attn_bwd(do, q4, k4, v4, o, lse, d4[:, :, :hq], d4[:, :, hq:hq + hkv], d4[:, :, hq + hkv:], D ** -0.5,
+                       True, None, rope_cos=cos if rope else None, rope_sin=sin if rope else None, cu_seqlens=cu,
+                       max_seqlen=ml, dqkv_t=dqkv_t)
+            outs.append((dqkv, dqkv_t))
+        torch.cuda.synchronize()
+    finally:
+        C.attn_set_dkdv_form(2)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert not torch.isnan(outs[1][0].float()).any()
+    assert torch.equal(outs[1][1], outs[1][0].t().contiguous())
