@@ -32,7 +32,6 @@ MI355X design:
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -79,8 +78,6 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         self._slot_free: List[Optional[torch.cuda.Event]] = [None] * self.nslot
         self._landed: Dict[int, torch.cuda.Event] = {}  # chunk index -> upload done (prefetched)
         fsdp._grad_zero_by_optimizer = True
-        self._d2h_kernel = os.environ.get("GRT_OFFLOAD_D2H", "copy") == "kernel"
-        self._d2h_wg = int(os.environ.get("GRT_OFFLOAD_D2H_WG", "128"))
         if self.prefetch_slots > 0:
             fsdp.add_forward_tail_hook(self.prefetch)
 
@@ -168,8 +165,8 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
                         done.record(upd)
                     with torch.cuda.stream(down):
                         down.wait_event(done)
-                        self._download(mb[:e - s], m_h[s:e])
-                        self._download(vb[:e - s], v_h[s:e])
+                        m_h[s:e].copy_(mb[:e - s], non_blocking=True)
+                        v_h[s:e].copy_(vb[:e - s], non_blocking=True)
                         free = torch.cuda.Event()
                         free.record(down)
                     self._slot_free[slot] = free
@@ -185,16 +182,6 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
             self._streams = tuple(torch.cuda.Stream(dev) for _ in range(3))  # up, update, down
             self._stage = [(torch.empty(self.chunk, device=dev), torch.empty(self.chunk, device=dev))
                            for _ in range(self.nslot)]
-
-    def _download(self, dev_t: torch.Tensor, host_t: torch.Tensor):
-        """Device -> pinned host on the current (download) stream. ROCclr runs such a copy as a blit
-        kernel at ~30 GB/s; ``stream_copy`` (a kernel of ours writing the mapped host memory with
-        non-temporal stores on D2H_WG workgroups) is used when GRT_OFFLOAD_D2H=kernel
-        (profiles/r5_offload70.md, tools/hostlink_bench.py)."""
-        if self._d2h_kernel and (dev_t.numel() * 4) % 16 == 0 and host_t.data_ptr() % 16 == 0:
-            _native.kernels().stream_copy(dev_t, host_t, self._d2h_wg, True)
-        else:
-            host_t.copy_(dev_t, non_blocking=True)
 
     def _slot(self, ci: int) -> int:
         P = self.prefetch_slots

@@ -6,27 +6,19 @@ what an overlapped copy costs the step). Under ``rocprofv3 --kernel-trace --memo
 trace shows which engine each direction uses (SDMA copies vs ``__amd_rocclr_copyBuffer`` blit
 kernels on the CUs).
 
-    python tools/hostlink_bench.py [--mib 512] [--reps 4] [--wg 128]
-
-``stream_copy`` rows: the same device -> host copy as a kernel of ours (csrc/kernels/optim.hip)
-with 32-512 workgroups, plain or non-temporal stores.
+    python tools/hostlink_bench.py [--mib 512] [--reps 4]
 """
 import argparse
 import json
-import os
-import sys
 import time
 
 import torch
-
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=512)
     ap.add_argument("--reps", type=int, default=4)
-    ap.add_argument("--wg", type=int, default=128, help="workgroups of the kernel D2H in the overlap runs")
     a = ap.parse_args()
     n = a.mib * 2 ** 20 // 4
     dev = torch.device("cuda")
@@ -63,29 +55,6 @@ def main():
     t = timed(lambda: (h2d(), d2h()))
     out["duplex_total_GBps"] = round(2 * a.reps * nbytes / t / 1e9, 1)
 
-    from gke_ray_train_amd import _native
-    C = _native.kernels()
-    for nb in (32, 128, 512):
-        for nt in (False, True):
-            def kd2h(nb=nb, nt=nt):
-                with torch.cuda.stream(down):
-                    for _ in range(a.reps):
-                        C.stream_copy(d_b, h_dst, nb, nt)
-            kd2h()
-            t = timed(kd2h)
-            out[f"kernel_d2h_wg{nb}_nt{int(nt)}_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
-    h_dst.zero_()
-    C.stream_copy(d_b, h_dst, 128, True)
-    torch.cuda.synchronize()
-    out["kernel_d2h_exact"] = bool(torch.equal(h_dst, d_b.cpu()))
-
-    def kd2h_best():
-        with torch.cuda.stream(down):
-            for _ in range(a.reps):
-                C.stream_copy(d_b, h_dst, a.wg, True)
-    t = timed(lambda: (h2d(), kd2h_best()))
-    out[f"duplex_sdma_h2d_kernel_d2h_wg{a.wg}_total_GBps"] = round(2 * a.reps * nbytes / t / 1e9, 1)
-
     x = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     y = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     z = torch.empty(8192, 8192, device=dev, dtype=torch.bfloat16)
@@ -97,8 +66,7 @@ def main():
     gemms(5)
     tg = timed(gemms)
     out["gemm_alone_ms"] = round(tg * 1e3, 1)
-    for name, fn in (("h2d", h2d), ("d2h", d2h), ("both", lambda: (h2d(), d2h())),
-                     ("kernel_d2h", kd2h_best), ("h2d_and_kernel_d2h", lambda: (h2d(), kd2h_best()))):
+    for name, fn in (("h2d", h2d), ("d2h", d2h), ("both", lambda: (h2d(), d2h()))):
         def run():
             fn()
             gemms()
