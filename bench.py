@@ -226,6 +226,10 @@ def run(a):
         idx = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(idx)
         dev = torch.device("cuda", idx)
+        if os.environ.get("GRT_COMPUTE_STREAM_PRIORITY", "normal") == "high":
+            # the training step on a high-priority stream: the side streams (overlapped AdamW,
+            # grad-norm partials, gathers) keep the default priority and yield to it
+            torch.cuda.set_stream(torch.cuda.Stream(dev, priority=torch.cuda.Stream.priority_range()[1]))
     if a.force_collectives:
         os.environ["GRT_FORCE_COLLECTIVES"] = "1"
     if (world > 1 or a.force_collectives) and not dist.is_initialized():

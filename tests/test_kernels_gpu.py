@@ -832,10 +832,12 @@ def test_swiglu_transposing_kernels_exact():
     assert not C.swiglu_fwd_t(gu[:100].contiguous(), 0) and not C.swiglu_bwd_t(gu[:100].contiguous(), dout[:100].contiguous())
 
 
-def test_swiglu_transposed_wgrad_path_matches(monkeypatch):
-    """Llama MLP under the DDP engine: with the transposing SwiGLU the down / gate_up weight
-    gradients take h^T / dgu^T from the SwiGLU kernels (two fewer transposes per layer) and every
-    gradient is bit-identical to the separate-transpose path."""
+@pytest.mark.parametrize("producer", ["swiglu", "attention"])
+def test_swiglu_transposed_wgrad_path_matches(producer, monkeypatch):
+    """Llama layers under the DDP engine: with the transposing producers the weight gradients take
+    their transposed operand from the producing kernel (SwiGLU: h^T for down, dgu^T for gate_up;
+    attention: o^T from the forward for o_proj, dqkv^T from the backward for qkv_proj), two fewer
+    transposes per layer each, and every gradient is bit-identical to the separate-transpose path."""
     from gke_ray_train_amd.models import build_llama, get_config
     from gke_ray_train_amd.ops import fused as Fu
     from gke_ray_train_amd.ops import linear as L
@@ -851,7 +853,8 @@ def test_swiglu_transposed_wgrad_path_matches(monkeypatch):
     monkeypatch.setattr(L, "wgrad_tn", counting)
     out, ncalls = [], []
     for flag in (False, True):
-        monkeypatch.setattr(Fu, "_SWIGLU_T", flag)
+        monkeypatch.setattr(Fu, "_SWIGLU_T", flag and producer == "swiglu")
+        monkeypatch.setattr(Fu, "_ATTN_DQKV_T", flag and producer == "attention")
         calls["n"] = 0
         m = build_llama(cfg, device=DEV, dtype=torch.bfloat16, seed=2)
         ddp = DistributedDataParallel(m)
@@ -862,8 +865,7 @@ def test_swiglu_transposed_wgrad_path_matches(monkeypatch):
         ncalls.append(calls["n"])
     for n in out[0]:
         assert torch.equal(out[0][n], out[1][n]), n
-    # with the flag: the down (h^T from the forward kernel) and gate_up (dgu^T from the backward
-    # kernel) weight gradients of both layers ran on the provided copies
+    # with the flag: two weight gradients per layer ran on the provided copies
     assert ncalls == [0, 2 * cfg.num_hidden_layers], ncalls
 
 
