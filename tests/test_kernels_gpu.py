@@ -381,13 +381,14 @@ def test_adamw_slices_and_alignment_bit_identical(sr):
             assert torch.equal(a, b), f"cuts {cuts}: {what} differs"
 
 
+@pytest.mark.parametrize("rows", [192, 512])
 @pytest.mark.parametrize("sr", [0.0, 1.0])
-def test_adamw_t_matches_flat_update_and_transposes(sr):
+def test_adamw_t_matches_flat_update_and_transposes(sr, rows):
     """adamw_t (update of a [rows, cols] weight that also writes W^T) == the flat AdamW kernel on
     the same data (same rounding stream for a matching index offset), and pt == p^T exactly."""
     C = _C()
     torch.manual_seed(8)
-    rows, cols, off = 192, 384, 128
+    cols, off = 384, 128
     p0 = torch.randn(rows, cols, device=DEV).bfloat16()
     g = torch.randn(rows, cols, device=DEV).bfloat16()
     m0 = torch.randn(rows, cols, device=DEV).abs() * 0.01
