@@ -142,6 +142,7 @@ class DistributedDataParallel(nn.Module):
     every world size so that access always works.
     """
     UNIT_TYPES = ("LlamaDecoderLayer", "EncoderLayer")
+    _ipc_engines = 0  # engines that created a bucket communicator (collective order = creation order)
 
     def __init__(self, module: nn.Module, process_group=None, bucket_cap_mb: Optional[float] = None,
                  broadcast_params: bool = True, grad_dtype: Optional[torch.dtype] = None,
@@ -252,7 +253,10 @@ class DistributedDataParallel(nn.Module):
             if ipc_mode() != "0" and any(
                     routes((b.end - b.start) * g.grad.element_size(), g.grad.dtype, route_limit(ipc_mode(), 8 << 20))
                     for g in self.groups for b in g.buckets):
-                self._ipc = communicator(process_group, "ddp-buckets")
+                # one communicator per engine: its epoch sequence is driven from this engine's
+                # side stream only (two engines sharing one would interleave calls across streams)
+                DistributedDataParallel._ipc_engines += 1
+                self._ipc = communicator(process_group, f"ddp-buckets-{DistributedDataParallel._ipc_engines}")
                 if self._ipc is not None:
                     self._ipc_limit = route_limit(ipc_mode(), self._ipc.cap)
                     self._ipc_stream = torch.cuda.Stream(dev0)

@@ -26,11 +26,15 @@ MI355X design:
   ring of NSLOT slots. When the last decoder unit's forward starts, the uploads of the owned slots
   are issued, so they cross the host link during the backward, when it is otherwise idle;
   ``step()`` then updates those chunks at once and only the remaining chunks upload under the next
-  forward, while the downloads run beside them (full duplex) and may spill into the next backward.
+  forward. The owned slots' write-backs are deferred to the next forward tail, just before their
+  next uploads, so both directions of the owned chunks use the backward window and the forward
+  window carries only the ring chunks' traffic.
   A slot is reused only after the download of its previous chunk (event per slot), which also
   orders every upload after the previous step's download of the same host range.
 """
 from __future__ import annotations
+
+import os
 
 from typing import Dict, List, Optional
 
@@ -77,6 +81,8 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         self.nslot = self.prefetch_slots + self.NSLOT
         self._slot_free: List[Optional[torch.cuda.Event]] = [None] * self.nslot
         self._landed: Dict[int, torch.cuda.Event] = {}  # chunk index -> upload done (prefetched)
+        self._pending_down: List[tuple] = []  # (chunk index, update done) of deferred write-backs
+        self.defer_writeback = os.environ.get("GRT_OFFLOAD_DEFER_WRITEBACK", "1") != "0"
         fsdp._grad_zero_by_optimizer = True
         if self.prefetch_slots > 0:
             fsdp.add_forward_tail_hook(self.prefetch)
@@ -107,6 +113,7 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         up, upd, down = self._streams
         comp = torch.cuda.current_stream(dev)
         fs.wait_updates()  # the previous step's updates all landed (normally long done)
+        self._flush_downloads()  # no forward tail since the last step (prefetch() did not run)
         hbs, work = [], []
         for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
@@ -163,19 +170,40 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
                         gf[s:e].zero_()
                         done = torch.cuda.Event()
                         done.record(upd)
-                    with torch.cuda.stream(down):
-                        down.wait_event(done)
-                        m_h[s:e].copy_(mb[:e - s], non_blocking=True)
-                        v_h[s:e].copy_(vb[:e - s], non_blocking=True)
-                        free = torch.cuda.Event()
-                        free.record(down)
-                    self._slot_free[slot] = free
+                    if ci < self.prefetch_slots and self.defer_writeback:
+                        # an owned slot: its write-back is deferred to the backward window (the slot
+                        # holds the only current copy until then; see _flush_downloads)
+                        self._pending_down.append((ci, done))
+                    else:
+                        self._download(ci, done)
                     ci += 1
             ev = torch.cuda.Event()
             ev.record(upd)
             events[u] = ev
         self._landed.clear()
         fs.set_update_events(events)
+
+    def _download(self, ci: int, done: torch.cuda.Event):
+        """Device -> pinned host write-back of chunk ``ci`` after its update (``done``), on the
+        in-order download stream; the event it records frees the chunk's slot."""
+        down = self._streams[2]
+        _, s, e = self.chunks[ci]
+        slot = self._slot(ci)
+        mb, vb = self._stage[slot]
+        sst = self.state[self.param_groups[0]["params"][0]]
+        with torch.cuda.stream(down):
+            down.wait_event(done)
+            sst["exp_avg"][s:e].copy_(mb[:e - s], non_blocking=True)
+            sst["exp_avg_sq"][s:e].copy_(vb[:e - s], non_blocking=True)
+            free = torch.cuda.Event()
+            free.record(down)
+        self._slot_free[slot] = free
+
+    def _flush_downloads(self):
+        """Issue the deferred write-backs of the owned (prefetch) slots."""
+        pend, self._pending_down = self._pending_down, []
+        for ci, done in pend:
+            self._download(ci, done)
 
     def _ensure_streams(self, dev):
         if self._streams is None:
@@ -214,6 +242,10 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
             return
         self._state(self.param_groups[0]["params"][0])
         self._ensure_streams(fs.device)
+        # the owned slots' write-backs of the last step go first (their uploads wait for them): both
+        # directions of the owned slots cross the link in the backward window, leaving the forward
+        # window to the ring chunks
+        self._flush_downloads()
         for ci in range(self.prefetch_slots):
             self._landed[ci] = self._upload(ci)
 
@@ -221,6 +253,7 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         """Current stream waits for every pending unit update and the moment downloads."""
         self.fsdp.wait_updates()
         if self._streams is not None:
+            self._flush_downloads()
             torch.cuda.current_stream(self.fsdp.device).wait_stream(self._streams[2])
 
     def state_dict(self):
