@@ -201,7 +201,7 @@ def test_ipc_buffer_sizes_offsets_parities():
 
 
 # ----------------------------------------------------------------------------- DDP data plane
-def _ddp_worker(rank, world, port, q):
+def _ddp_worker(rank, world, port, q, zero=False):
     """DDP with the automatic IPC route: the no-decay group (a 1-D weight, a few KiB) is
     all-reduced by the IPC kernels on a side stream, the 4 MiB decay group by the process group."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GRT_IPC_ALLOW_GLOO="1",
@@ -224,7 +224,7 @@ def _ddp_worker(rank, world, port, q):
 
         torch.manual_seed(0)
         net = Net().cuda()
-        ddp = DistributedDataParallel(net, broadcast_params=True)
+        ddp = DistributedDataParallel(net, broadcast_params=True, shard_optimizer=zero)
         g = torch.Generator().manual_seed(50 + rank)
         x = torch.randn(16, 1024, generator=g).cuda()
         ddp(x).backward()
@@ -233,6 +233,9 @@ def _ddp_worker(rank, world, port, q):
         out = {"ipc": ddp.ipc_bucket_launches,
                "fc1": net.fc1.weight.grad.float().cpu().numpy(),
                "norm": net.norm.weight.grad.float().cpu().numpy()}
+        if zero:  # this rank's reduced shard of every group (what the sharded AdamW consumes)
+            out["shards"] = [sg.float().cpu().numpy() for sg in ddp.grad_buffers()]
+            out["layout"] = [[(b.start, b.end, b.shard_off) for b in grp.buckets] for grp in ddp.groups]
         # the same gradients without DDP on this rank's data (summed over ranks by the parent)
         torch.manual_seed(0)
         ref = Net().cuda()
@@ -247,9 +250,16 @@ def _ddp_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_ddp_small_bucket_over_ipc():
+def _ddp_zero_worker(rank, world, port, q):
+    _ddp_worker(rank, world, port, q, zero=True)
+
+
+@pytest.mark.parametrize("zero", [False, True])
+def test_ddp_small_bucket_over_ipc(zero):
+    """zero: the ZeRO engine's IPC bucket (all-reduce over IPC + this rank's chunk copied into the
+    gradient shard on the side stream) gives the same shard as the reduce-scatter would."""
     world = 2
-    res = _spawn(_ddp_worker, world)
+    res = _spawn(_ddp_zero_worker if zero else _ddp_worker, world)
     for k in ("fc1", "norm"):
         exp = sum(torch.from_numpy(res[r][f"ref_{k}"]) for r in range(world))
         for r in range(world):
@@ -257,3 +267,17 @@ def test_ddp_small_bucket_over_ipc():
             assert torch.allclose(got, exp, atol=1e-5, rtol=1e-4), (k, r, (got - exp).abs().max())
     for r in range(world):
         assert res[r]["ipc"] >= 1, "the no-decay bucket did not take the IPC route"
+    if zero:
+        import numpy as np
+        for r in range(world):
+            full = {"fc1": sum(torch.from_numpy(res[k]["ref_fc1"]) for k in range(world)).reshape(-1),
+                    "norm": sum(torch.from_numpy(res[k]["ref_norm"]) for k in range(world)).reshape(-1)}
+            # one parameter per group: the shard is rank r's 1/world chunk of that parameter's summed
+            # gradient (fc1: 1024 x 1024 over RCCL-path gloo, norm: 1024 over the IPC kernel)
+            for shard, buckets in zip(res[r]["shards"], res[r]["layout"]):
+                assert len(buckets) == 1 and np.isfinite(shard).all()
+                c = (buckets[0][1] - buckets[0][0]) // world
+                name = "fc1" if c * world >= 1024 * 1024 else "norm"
+                exp = full[name][r * c:(r + 1) * c]
+                got = torch.from_numpy(shard[:c])
+                assert torch.allclose(got, exp, atol=1e-5, rtol=1e-4), (name, r, (got - exp).abs().max())
