@@ -682,21 +682,6 @@ void scale_(Tensor& x, double a, const optional<Tensor>& a_ptr) {
                      a_ptr.has_value() ? a_ptr->data_ptr<float>() : nullptr, cur_stream(x));
 }
 
-// dst.copy_(src) by a kernel when one side is pinned host memory (device-mapped): the moment
-// write-back of the offloaded optimizer on boxes whose device -> host blit copy is slow
-void stream_copy(const Tensor& src, Tensor& dst, int64_t nblocks, bool nt) {
-  TORCH_CHECK(src.is_contiguous() && dst.is_contiguous(), "stream_copy: contiguous operands");
-  const int64_t nbytes = src.numel() * src.element_size();
-  TORCH_CHECK(dst.numel() * dst.element_size() == nbytes, "stream_copy: size mismatch");
-  TORCH_CHECK(nbytes % 16 == 0 && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(dst.data_ptr()) % 16 == 0, "stream_copy: 16-byte multiple / alignment");
-  TORCH_CHECK(src.is_cuda() || dst.is_cuda(), "stream_copy: one side on the device");
-  TORCH_CHECK((src.is_cuda() || src.is_pinned()) && (dst.is_cuda() || dst.is_pinned()), "stream_copy: host side must be pinned");
-  const auto& d = src.is_cuda() ? src : dst;
-  c10::OptionalDeviceGuard g(d.device());
-  grt::stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, (int)nblocks, nt, cur_stream(d), !src.is_cuda(), !dst.is_cuda());
-}
-
 // ------------------------------------------------------------------ attention
 void check_bshd(const Tensor& t, const char* name) {
   check_cuda(t, name);
@@ -1264,7 +1249,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("hyper"), py::arg("gscale"), py::arg("max_blocks") = 0, py::arg("index_offset") = 0);
   m.def("adamw_t", &adamw_t);
   m.def("scale_", &scale_);
-  m.def("stream_copy", &stream_copy, py::arg("src"), py::arg("dst"), py::arg("nblocks") = 16, py::arg("nt") = true);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("out"), py::arg("scale"),
         py::arg("causal"), py::arg("seqlens_k"), py::arg("dropout_p") = 0.0, py::arg("seed") = 0,
         py::arg("cu_seqlens") = py::none(), py::arg("max_seqlen") = 0, py::arg("o_t") = py::none());

@@ -97,10 +97,6 @@ void adamw_t_step(void* p, const void* g, float* m, float* v, void* pt, int64_t 
                   const float* hyper, const float* grad_scale_ptr, hipStream_t s, int64_t ioff);
 // Scale in place: x *= a (device scalar pointer or host value when a_ptr == null).
 void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s);
-// HBM <-> pinned host copy by a kernel (nbytes % 16 == 0, 16-byte aligned; nblocks workgroups; host
-// operands validated with hipHostGetDevicePointer)
-void stream_copy(const void* src, void* dst, int64_t nbytes, int nblocks, bool nt, hipStream_t s, bool src_host,
-                 bool dst_host);
 
 // ---------------- LoRA adapter (lora.hip) ----------------
 // h[M][R] = (x ⊙ keep/(1-p)) · A^T, A [R][K]; keep = the element-dropout hash of x's element index

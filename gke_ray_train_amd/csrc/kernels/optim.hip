@@ -16,7 +16,6 @@
 #include <cstdlib>
 
 #include <algorithm>
-#include <stdexcept>
 
 #include "grt_common.h"
 #include "grt_kernels.h"
@@ -405,55 +404,6 @@ void adamw_t_step(void* p, const void* g, float* m, float* v, void* pt, int64_t 
   const dim3 grid((unsigned)((rows / 64) * (cols / 128)));
   hipLaunchKernelGGL(adamw_t_kernel, grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, (bf16*)pt, rows,
                      cols, hyper, gsp, (uint64_t)ioff);
-}
-
-// Device-driven copy between HBM and pinned (device-mapped) host memory, for the offloaded
-// optimizer's moment write-back: ROCclr runs a pinned device -> host hipMemcpyAsync as its blit
-// kernel at ~30 GB/s on MI355X while SDMA moves host -> device at ~57 GB/s
-// (tools/hostlink_bench.py, profiles/r5_offload70.md). Each thread keeps 4 x 16 B in flight; NT:
-// non-temporal stores (streaming writes to the host). nblocks bounds the CUs the copy occupies.
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-template <bool NT>
-__global__ __launch_bounds__(256) void stream_copy_kernel(const u32x4_t* __restrict__ src, u32x4_t* __restrict__ dst,
-                                                          int64_t n16) {
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  auto st = [&](int64_t k, const u32x4_t& v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, dst + k);
-    else dst[k] = v;
-  };
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const u32x4_t a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    st(i, a);
-    st(i + stride, b);
-    st(i + 2 * stride, c);
-    st(i + 3 * stride, d);
-  }
-  for (; i < n16; i += stride) st(i, src[i]);
-}
-
-// host-side operands are translated with hipHostGetDevicePointer (same VA on ROCm for pinned
-// memory) and REFUSED when the runtime does not know them as device-mapped host memory: a kernel
-// dereferencing unmapped host memory would fault the GPU
-static const void* device_view_of_host(const void* p) {
-  void* d = nullptr;
-  if (hipHostGetDevicePointer(&d, const_cast<void*>(p), 0) != hipSuccess || d == nullptr) {
-    (void)hipGetLastError();
-    throw std::runtime_error("stream_copy: host operand is not device-mapped pinned memory");
-  }
-  return d;
-}
-
-void stream_copy(const void* src, void* dst, int64_t nbytes, int nblocks, bool nt, hipStream_t s, bool src_host,
-                 bool dst_host) {
-  const int64_t n16 = nbytes / 16;
-  if (n16 <= 0) return;
-  if (src_host) src = device_view_of_host(src);
-  if (dst_host) dst = const_cast<void*>(device_view_of_host(dst));
-  const int64_t need = (n16 + 255) / 256;
-  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(nblocks, need));
-  if (nt) hipLaunchKernelGGL(stream_copy_kernel<true>, dim3(g), dim3(256), 0, s, (const u32x4_t*)src, (u32x4_t*)dst, n16);
-  else hipLaunchKernelGGL(stream_copy_kernel<false>, dim3(g), dim3(256), 0, s, (const u32x4_t*)src, (u32x4_t*)dst, n16);
 }
 
 void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s) {

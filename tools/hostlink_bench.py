@@ -55,22 +55,6 @@ def main():
     t = timed(lambda: (h2d(), d2h()))
     out["duplex_total_GBps"] = round(2 * a.reps * nbytes / t / 1e9, 1)
 
-    import os
-    import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-    from gke_ray_train_amd import _native
-    C = _native.kernels()
-    kern = {}
-    for nb in (4, 8, 16, 32):
-        def kd2h(nb=nb):
-            with torch.cuda.stream(down):
-                for _ in range(a.reps):
-                    C.stream_copy(d_b, h_dst, nb, True)
-        kd2h()
-        t = timed(kd2h)
-        out[f"kernel_d2h_wg{nb}_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
-        kern[nb] = kd2h
-
     x = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     y = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     z = torch.empty(8192, 8192, device=dev, dtype=torch.bfloat16)
@@ -82,9 +66,7 @@ def main():
     gemms(5)
     tg = timed(gemms)
     out["gemm_alone_ms"] = round(tg * 1e3, 1)
-    arms = [("h2d", h2d), ("d2h", d2h), ("both", lambda: (h2d(), d2h()))]
-    arms += [(f"kernel_d2h_wg{nb}", f) for nb, f in kern.items()]
-    for name, fn in arms:
+    for name, fn in (("h2d", h2d), ("d2h", d2h), ("both", lambda: (h2d(), d2h()))):
         def run():
             fn()
             gemms()
