@@ -222,6 +222,7 @@ def plan_memory(cfg, world: int, parallel: str = "ddp", offload: bool = False, p
     hbm["grads"] = P * B
     if zero:
         hbm["grad_shard"] = P * B / world
+        hbm["param_shard"] = P * B / world  # the contiguous shard the sharded AdamW updates
         opt = 8.0 * P / world
     else:
         opt = 8.0 * P
