@@ -973,6 +973,56 @@ Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
   return y;
 }
 
+// Decode GEMV with the residual add / RMSNorm folded in (gemv.hip). sumsq: int64 [2, M, 64] fixed-point
+// accumulators (zero-initialised once; the producers keep them consistent), slot: 0 / 1.
+//   g given: y = bf16(x * rstd * g) W^T with rstd from sumsq[slot] (x = the residual stream h);
+//   res given: y = bf16(x W^T) + res, its sums of squares added into sumsq[slot], sumsq[1 - slot]
+//   zeroed for the next producer.
+Tensor gemv_fused(const Tensor& x, const Tensor& w, const Tensor& sumsq, int64_t slot, bool swiglu,
+                  const c10::optional<Tensor>& g, const c10::optional<Tensor>& res, double eps) {
+  check_cuda(x, "x");
+  check_contig(w, "w");
+  check_contig(sumsq, "sumsq");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == (swiglu ? 2 : 1) * w.size(1), "gemv_fused: x [M, K], w [N, K]");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "gemv_fused: bf16");
+  const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
+  TORCH_CHECK(M >= 1 && M <= 4 && K % 8 == 0 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemv_fused: 1..4 rows, K % 8");
+  TORCH_CHECK(N <= INT32_MAX && K <= INT32_MAX, "gemv_fused: dims");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
+              "gemv_fused: 16-byte alignment");
+  TORCH_CHECK(sumsq.scalar_type() == at::kLong && sumsq.numel() % 2 == 0 && sumsq.numel() / 2 >= M * 64 &&
+                  (slot == 0 || slot == 1),
+              "gemv_fused: sumsq int64 [2, >= M, 64], slot 0 / 1");
+  auto* acc = reinterpret_cast<unsigned long long*>(sumsq.data_ptr<int64_t>());
+  const int64_t stride = sumsq.numel() / 2;
+  grt::GemvFused f{};
+  f.x = x.data_ptr(), f.ldx = x.stride(0), f.w = w.data_ptr(), f.M = (int)M, f.N = (int)N, f.K = (int)K;
+  f.swiglu = swiglu, f.eps = (float)eps;
+  const bool normx = g.has_value() && g->defined();
+  const bool resnorm = res.has_value() && res->defined();
+  TORCH_CHECK(normx != resnorm, "gemv_fused: exactly one of g (normalise the input) / res (residual epilogue)");
+  if (normx) {
+    TORCH_CHECK(!swiglu, "gemv_fused: normx and swiglu are exclusive");
+    check_contig(*g, "g");
+    TORCH_CHECK(g->scalar_type() == at::kBFloat16 && g->numel() == K && reinterpret_cast<uintptr_t>(g->data_ptr()) % 16 == 0,
+                "gemv_fused: g bf16 [K], 16-byte aligned");
+    f.g = g->data_ptr(), f.sumsq_in = acc + slot * stride;
+  } else {
+    check_cuda(*res, "res");
+    TORCH_CHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == N && res->stride(1) == 1 &&
+                    res->scalar_type() == at::kBFloat16, "gemv_fused: res bf16 [M, N]");
+    f.res = res->data_ptr(), f.ldr = res->stride(0);
+    f.sumsq_out = acc + slot * stride, f.sumsq_zero = acc + (1 - slot) * stride;
+  }
+  c10::OptionalDeviceGuard dg(x.device());
+  Tensor y = at::empty({M, N}, x.options());
+  f.y = y.data_ptr(), f.ldy = N;
+  grt::gemv_fused_bf16(f, cur_stream(x));
+  return y;
+}
+
+int64_t gemv_workgroups(int64_t N) { return grt::gemv_workgroups((int)N); }
+
 // ------------------------------------------------------------------ embedding
 Tensor embedding_fwd(const Tensor& ids, const Tensor& w) {
   check_contig(ids, "ids");
@@ -1272,6 +1322,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_bwd_t", &swiglu_bwd_t);
   m.def("transpose_into", &transpose_into);
   m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
+  m.def("gemv_fused", &gemv_fused, py::arg("x"), py::arg("w"), py::arg("sumsq"), py::arg("slot"),
+        py::arg("swiglu") = false, py::arg("g") = py::none(), py::arg("res") = py::none(), py::arg("eps") = 1e-5);
+  m.def("gemv_workgroups", &gemv_workgroups);
   m.def("attn_decode", &attn_decode);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

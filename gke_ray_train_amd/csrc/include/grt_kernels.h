@@ -307,6 +307,30 @@ void transpose_bf16(const void* src, void* dst, int rows, int cols, hipStream_t 
 // swiglu: x is the fused [gate | up] output [M, 2K] and the GEMV input is silu(gate) * up
 void gemv_bf16(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int M, int N, int K, hipStream_t s,
                bool swiglu = false);
+// The decode step's residual adds / RMSNorms folded into the GEMVs (gemv.hip header):
+//   sumsq_in != null: the GEMV input is bf16(x * rsqrt(sum_j sumsq_in[m][j] * 2^-20 / K + eps) * g)
+//   (x = the residual stream h, sumsq_in [M][64] its fixed-point partial sums of squares);
+//   res != null: y = bf16(x W^T) + res (the next h); its sums of squares are added into sumsq_out
+//   [M][64] (zero at launch) and sumsq_zero [M][64] is zeroed for the next producer.
+struct GemvFused {
+  const void* x;
+  int64_t ldx;
+  const void* w;
+  void* y;
+  int64_t ldy;
+  int M, N, K;
+  bool swiglu;
+  const void* g;
+  float eps;
+  const unsigned long long* sumsq_in;
+  const void* res;
+  int64_t ldr;
+  unsigned long long* sumsq_out;
+  unsigned long long* sumsq_zero;
+};
+void gemv_fused_bf16(const GemvFused& f, hipStream_t s);
+int gemv_k_split(int N);
+int gemv_workgroups(int N);
 
 // ---------------- xGMI peer-to-peer collectives (ipc_comm.hip) ----------------
 constexpr int kIpcMaxRanks = 8;

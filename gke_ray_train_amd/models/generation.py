@@ -19,6 +19,7 @@ tokens instead of every token; the output is trimmed to HF's stopping point.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Union
 
 import torch
@@ -125,6 +126,62 @@ def _graph_layer_step(layer, h, residual, B, cos, sin, cache: KVCache, li: int, 
     return _mlp(layer.mlp, x), residual
 
 
+_GEMV_NORM = os.environ.get("GRT_GEMV_NORM", "1") != "0"
+
+
+def _plain_bf16_linear(lin) -> bool:
+    from ..ops import linear as _lin
+    w = getattr(lin, "weight", None)
+    return (isinstance(lin, _lin.Linear) and type(lin).forward is _lin.Linear.forward and lin.bias is None
+            and w.dtype == torch.bfloat16 and w.is_cuda and w.is_contiguous() and w.shape[1] % 8 == 0
+            and w.data_ptr() % 16 == 0)
+
+
+def _norm_fusable(model, B: int) -> bool:
+    """Every projection a plain bf16 Linear (no LoRA / NF4 wrappers, no bias) and 1-2 rows: the
+    decode step can run with its residual adds / RMSNorms inside the GEMVs (gemv.hip)."""
+    from ..ops import linear as _lin
+    if not (_GEMV_NORM and _lin._GEMV and B <= _lin.GEMV_MAX_ROWS and _native.kernels_available()):
+        return False
+    m = model.model
+    norms = [m.norm] + [n for ly in m.layers for n in (ly.input_layernorm, ly.post_attention_layernorm)]
+    lins = [model.lm_head] + [p for ly in m.layers for p in (ly.self_attn.qkv_proj, ly.self_attn.o_proj,
+                                                               ly.mlp.gate_up_proj, ly.mlp.down_proj)]
+    return (all(_plain_bf16_linear(p) for p in lins)
+            and all(n.weight.dtype == torch.bfloat16 and n.weight.is_contiguous() and n.weight.data_ptr() % 16 == 0
+                    for n in norms))
+
+
+class _NormWorkspace:
+    """Fixed-point sums of squares of the residual stream's rows (gemv.hip): two [B, 64] slots, the
+    producer GEMVs (o_proj, down_proj) alternate between them and each zeroes the other for the
+    next one. 2 producers per layer, so the slot sequence repeats every token (graph replay)."""
+
+    def __init__(self, B: int, device):
+        self.sumsq = torch.zeros(2, B, 64, dtype=torch.int64, device=device)
+
+
+def _fused_norm_layer_step(layer, h, first: bool, ws: _NormWorkspace, B, cos, sin, cache: KVCache, li: int,
+                           pos_b, lens):
+    """One-token layer step with the residual adds and RMSNorms inside the GEMVs: o_proj / down_proj
+    write h = y + residual and add sum(h^2) to a fixed-point accumulator, qkv / gate_up normalise
+    their input on the fly from (h, accumulator, norm weight). ``h`` IS the residual stream between
+    layers; slot 0 carries the post-attention norm's statistics, slot 1 the next input norm's."""
+    K = _native.kernels()
+    attn, mlp = layer.self_attn, layer.mlp
+    ln1, ln2 = layer.input_layernorm, layer.post_attention_layernorm
+    if first:  # layer 0: h is the embedding (no residual add, no producer GEMV summed its squares)
+        qkv = K.gemv(ops.rms_norm(h, ln1.weight, ln1.eps), attn.qkv_proj.weight)
+    else:
+        qkv = K.gemv_fused(h, attn.qkv_proj.weight, ws.sumsq, 1, g=ln1.weight, eps=ln1.eps)
+    hq, hkv, D = attn.hq, attn.hkv, attn.hd
+    q = K.rope_append(qkv, cos, sin, pos_b, hq, hkv, D, cos.shape[0], cache.k[li], cache.v[li], 1)
+    o = ops.flash_attention(q.view(B, 1, hq, D), cache.k[li], cache.v[li], causal=False, seqlens_k=lens)
+    h = K.gemv_fused(o.reshape(B, hq * D), attn.o_proj.weight, ws.sumsq, 0, res=h)
+    gu = K.gemv_fused(h, mlp.gate_up_proj.weight, ws.sumsq, 0, g=ln2.weight, eps=ln2.eps)
+    return K.gemv_fused(gu, mlp.down_proj.weight, ws.sumsq, 1, swiglu=True, res=h)
+
+
 class GraphDecoder:
     """Greedy / sampling decode with the per-token step captured in a HIP graph (see module doc).
 
@@ -146,6 +203,9 @@ class GraphDecoder:
         self.lens = torch.zeros(B, dtype=torch.int32, device=self.device)    # valid keys incl. new token
         self.graph = None
         self.logits = None
+        # residual adds / norms inside the GEMVs when every projection is a plain bf16 Linear
+        self.norm_ws = (_NormWorkspace(B, self.device)
+                        if self.device.type == "cuda" and _norm_fusable(model, B) else None)
 
     @torch.no_grad()
     def prefill(self, input_ids: torch.Tensor) -> torch.Tensor:
@@ -160,6 +220,17 @@ class GraphDecoder:
     def _step_body(self):
         m = self.model
         h = m.model.embed_tokens(self.ids).view(self.B, -1)
+        if self.norm_ws is not None:
+            for li, layer in enumerate(m.model.layers):
+                h = _fused_norm_layer_step(layer, h, li == 0, self.norm_ws, self.B, self.cos, self.sin,
+                                           self.cache, li, self.pos_b, self.lens)
+            fn = m.model.norm
+            logits = _native.kernels().gemv_fused(h, m.lm_head.weight, self.norm_ws.sumsq, 1, g=fn.weight,
+                                                  eps=fn.eps).float()
+            self.pos_b.add_(1)
+            self.pos_l.add_(1)
+            self.lens.add_(1)
+            return logits
         residual = None
         for li, layer in enumerate(m.model.layers):
             h, residual = _graph_layer_step(layer, h, residual, self.B, self.cos, self.sin, self.cache, li,

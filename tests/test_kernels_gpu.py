@@ -934,6 +934,86 @@ def test_gemv_swiglu_decode(M, N, K):
     _close(y, ref, 2e-2, 2e-2, "gemv_swiglu vs fp32")
 
 
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("swiglu", [False, True])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (4096, 14336), (37, 264)])
+def test_gemv_resnorm_epilogue(M, N, K, swiglu):
+    """Producer GEMV with the residual add and the next RMSNorm's statistics in its epilogue:
+    h == bf16(gemv(x, w)) + res bitwise (torch rounding); the fixed-point sum of squares (slot) ==
+    sum(h^2) and is bitwise reproducible; the other slot is zeroed for the next producer; a consumer
+    reading the slot normalises like rsqrt(mean(h^2) + eps)."""
+    C = _C()
+    g = torch.Generator(device=DEV).manual_seed(M * N + K + swiglu)
+    x = torch.randn(M, (2 if swiglu else 1) * K, device=DEV, dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16, generator=g) * 0.02
+    res = torch.randn(M, N, device=DEV, dtype=torch.bfloat16, generator=g)
+    sums = []
+    for slot in (0, 1, 0):
+        acc = torch.full((2, M, 64), 12345, dtype=torch.int64, device=DEV)
+        acc[slot] = 0
+        h = C.gemv_fused(x, w, acc, slot, swiglu=swiglu, res=res)
+        assert torch.equal(h, (C.gemv(x, w, swiglu).float() + res.float()).to(torch.bfloat16))
+        assert int(acc[1 - slot].abs().sum()) == 0
+        ref = h.double().pow(2).sum(-1)
+        torch.testing.assert_close(acc[slot].sum(-1).double() / 2 ** 20, ref, rtol=1e-5, atol=1e-5)
+        sums.append(acc[slot].clone())
+    assert torch.equal(sums[0], sums[1]) and torch.equal(sums[0], sums[2])
+    if N % 8:
+        return
+    # a consumer of h (normalise on the fly) against the norm math with the exact rstd
+    w2 = torch.randn(64, N, device=DEV, dtype=torch.bfloat16, generator=g) * 0.02
+    nw = (1 + 0.1 * torch.randn(N, device=DEV, generator=g)).to(torch.bfloat16)
+    y = C.gemv_fused(h, w2, torch.stack([torch.zeros_like(sums[0]), sums[0]]), 1, g=nw, eps=1e-5)
+    rstd = torch.rsqrt(h.float().pow(2).mean(-1) + 1e-5)
+    _close(y, (h.float() * rstd[:, None] * nw.float()) @ w2.float().t(), 2e-2, 2e-2, "normx after resnorm")
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (1000, 8192), (37, 264)])
+def test_gemv_normx_prologue(M, N, K):
+    """Consumer GEMV normalising its input on the fly from the fixed-point sum of squares: ==
+    rms_norm-rounded input + GEMV, and == fp32 math."""
+    C = _C()
+    g = torch.Generator(device=DEV).manual_seed(M * N + K)
+    h = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, generator=g)
+    nw = (1 + 0.1 * torch.randn(K, device=DEV, generator=g)).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16, generator=g) * 0.02
+    acc = torch.zeros(2, M, 64, dtype=torch.int64, device=DEV)
+    acc[0, :, 5] = torch.round(h.double().pow(2).sum(-1) * 2 ** 20).long()
+    y = C.gemv_fused(h, w, acc, 0, g=nw, eps=1e-5)
+    rstd = torch.rsqrt(h.float().pow(2).mean(-1) + 1e-5)
+    xn = (h.float() * rstd[:, None] * nw.float()).to(torch.bfloat16)
+    _close(y, C.gemv(xn, w), 1e-2, 1e-2, "gemv normx vs normalised input + gemv")
+    ref = (h.float() * rstd[:, None] * nw.float()) @ w.float().t()
+    _close(y, ref, 2e-2, 2e-2, "gemv normx vs fp32")
+
+
+def test_decode_fused_norm_matches_unfused():
+    """GraphDecoder with the residual adds / norms inside the GEMVs == the unfused decode
+    (GRT_GEMV_NORM=0 path): same greedy tokens, logits within bf16 rounding."""
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.models import generation as G
+    torch.manual_seed(0)
+    m = build_llama("llama-tiny-gqa", device=DEV, dtype=torch.bfloat16, seed=0).eval()
+    ids = torch.randint(0, m.config.vocab_size, (1, 12), device=DEV)
+    outs = []
+    for fused in (True, False):
+        G._GEMV_NORM = fused
+        try:
+            dec = G.GraphDecoder(m, 1, 32)
+            assert (dec.norm_ws is not None) == fused
+            lg = [dec.prefill(ids)]
+            nxt = lg[-1].argmax(-1)
+            for _ in range(6):
+                lg.append(dec.step(nxt).clone())
+                nxt = lg[-1].argmax(-1)
+            outs.append(torch.stack(lg))
+        finally:
+            G._GEMV_NORM = True
+    assert torch.equal(outs[0].argmax(-1), outs[1].argmax(-1))
+    _close(outs[0], outs[1], 2e-2, 2e-2, "fused vs unfused decode logits")
+
+
 @pytest.mark.parametrize("B,S,hq,hkv,L,start", [(1, 1, 32, 8, 64, 17), (2, 5, 8, 8, 40, 3), (3, 4, 4, 1, 10, 8)])
 def test_rope_append(B, S, hq, hkv, L, start):
     """Decode RoPE + KV-cache append (rope_append, elementwise.hip) == rope_fwd + cache slice writes;
