@@ -978,8 +978,12 @@ Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
 //   g given: y = bf16(x * rstd * g) W^T with rstd from sumsq[slot] (x = the residual stream h);
 //   res given: y = bf16(x W^T) + res, its sums of squares added into sumsq[slot], sumsq[1 - slot]
 //   zeroed for the next producer.
+//   cos given (qkv, head_dim 128): RoPE in the epilogue at position pos[m]; returns q [M, hq, 128],
+//   k / v written to cache slot pos[m] of kc / vc (rope_append semantics: bad positions write nothing).
 Tensor gemv_fused(const Tensor& x, const Tensor& w, const Tensor& sumsq, int64_t slot, bool swiglu,
-                  const c10::optional<Tensor>& g, const c10::optional<Tensor>& res, double eps) {
+                  const c10::optional<Tensor>& g, const c10::optional<Tensor>& res, double eps,
+                  const c10::optional<Tensor>& cos, const c10::optional<Tensor>& sin, const c10::optional<Tensor>& pos,
+                  const c10::optional<Tensor>& kc, const c10::optional<Tensor>& vc, int64_t hq, int64_t hkv) {
   check_cuda(x, "x");
   check_contig(w, "w");
   check_contig(sumsq, "sumsq");
@@ -1000,14 +1004,36 @@ Tensor gemv_fused(const Tensor& x, const Tensor& w, const Tensor& sumsq, int64_t
   f.swiglu = swiglu, f.eps = (float)eps;
   const bool normx = g.has_value() && g->defined();
   const bool resnorm = res.has_value() && res->defined();
-  TORCH_CHECK(normx != resnorm, "gemv_fused: exactly one of g (normalise the input) / res (residual epilogue)");
+  const bool rope = cos.has_value() && cos->defined();
+  TORCH_CHECK(!(normx && resnorm) && (normx || resnorm || rope),
+              "gemv_fused: g (normalise the input) or res (residual epilogue), and / or cos (RoPE epilogue)");
+  TORCH_CHECK(!(rope && (resnorm || swiglu)), "gemv_fused: the RoPE epilogue is for the qkv projection");
+  Tensor q;
+  if (rope) {
+    TORCH_CHECK(sin.has_value() && pos.has_value() && kc.has_value() && vc.has_value(), "gemv_fused: rope needs sin / pos / kc / vc");
+    check_rope(*cos, *sin, *pos, M, cos->numel() / 64, 128);
+    TORCH_CHECK(hq > 0 && hkv > 0 && N == (hq + 2 * hkv) * 128, "gemv_fused: rope N == (hq + 2 hkv) * 128");
+    for (const Tensor* c : {&*kc, &*vc}) {
+      check_cuda(*c, "cache");
+      TORCH_CHECK(c->dim() == 4 && c->size(0) == M && c->size(2) == hkv && c->size(3) == 128 && c->stride(3) == 1 &&
+                      c->scalar_type() == at::kBFloat16,
+                  "gemv_fused: cache bf16 [M, L, hkv, 128]");
+    }
+    TORCH_CHECK(vc->sizes() == kc->sizes(), "gemv_fused: kc / vc shapes");
+    q = at::empty({M, hq, 128}, x.options());
+    f.q_out = q.data_ptr(), f.kc = kc->data_ptr(), f.vc = vc->data_ptr();
+    f.c_bs = kc->stride(0), f.c_ss = kc->stride(1), f.c_hs = kc->stride(2);
+    f.v_bs = vc->stride(0), f.v_ss = vc->stride(1), f.v_hs = vc->stride(2);
+    f.cosb = cos->data_ptr<float>(), f.sinb = sin->data_ptr<float>(), f.pos = pos->data_ptr<int32_t>();
+    f.rope_S = (int)(cos->numel() / 64), f.cache_L = (int)kc->size(1), f.hq = (int)hq, f.hkv = (int)hkv;
+  }
   if (normx) {
     TORCH_CHECK(!swiglu, "gemv_fused: normx and swiglu are exclusive");
     check_contig(*g, "g");
     TORCH_CHECK(g->scalar_type() == at::kBFloat16 && g->numel() == K && reinterpret_cast<uintptr_t>(g->data_ptr()) % 16 == 0,
                 "gemv_fused: g bf16 [K], 16-byte aligned");
     f.g = g->data_ptr(), f.sumsq_in = acc + slot * stride;
-  } else {
+  } else if (resnorm) {
     check_cuda(*res, "res");
     TORCH_CHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == N && res->stride(1) == 1 &&
                     res->scalar_type() == at::kBFloat16, "gemv_fused: res bf16 [M, N]");
@@ -1015,8 +1041,8 @@ Tensor gemv_fused(const Tensor& x, const Tensor& w, const Tensor& sumsq, int64_t
     f.sumsq_out = acc + slot * stride, f.sumsq_zero = acc + (1 - slot) * stride;
   }
   c10::OptionalDeviceGuard dg(x.device());
-  Tensor y = at::empty({M, N}, x.options());
-  f.y = y.data_ptr(), f.ldy = N;
+  Tensor y = rope ? q : at::empty({M, N}, x.options());
+  f.y = rope ? nullptr : y.data_ptr(), f.ldy = N;
   grt::gemv_fused_bf16(f, cur_stream(x));
   return y;
 }
@@ -1323,7 +1349,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_into", &transpose_into);
   m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("gemv_fused", &gemv_fused, py::arg("x"), py::arg("w"), py::arg("sumsq"), py::arg("slot"),
-        py::arg("swiglu") = false, py::arg("g") = py::none(), py::arg("res") = py::none(), py::arg("eps") = 1e-5);
+        py::arg("swiglu") = false, py::arg("g") = py::none(), py::arg("res") = py::none(), py::arg("eps") = 1e-5,
+        py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("pos") = py::none(),
+        py::arg("kc") = py::none(), py::arg("vc") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0);
   m.def("gemv_workgroups", &gemv_workgroups);
   m.def("attn_decode", &attn_decode);
   m.def("embedding_fwd", &embedding_fwd);

@@ -327,6 +327,16 @@ struct GemvFused {
   int64_t ldr;
   unsigned long long* sumsq_out;
   unsigned long long* sumsq_zero;
+  // q_out != null (qkv projection, head_dim 128, N = (hq + 2 hkv) * 128): RoPE at position pos[m]
+  // in the epilogue; q -> q_out [M, hq, 128], k / v -> cache slot pos[m] of kc / vc [B, L, hkv, 128]
+  void* q_out;
+  void* kc;
+  void* vc;
+  int64_t c_bs, c_ss, c_hs, v_bs, v_ss, v_hs;
+  const float* cosb;
+  const float* sinb;
+  const int* pos;
+  int rope_S, cache_L, hq, hkv;
 };
 void gemv_fused_bf16(const GemvFused& f, hipStream_t s);
 int gemv_k_split(int N);

@@ -16,6 +16,8 @@
 //     64 64-bit fixed-point accumulators (2^-20 units: integer atomics are associative, so the
 //     sum — and the decode — stays bitwise reproducible; no fences, no counter). Workgroup 0 zeroes
 //     the other of two accumulator sets, the one the next producer adds into;
+//   * EPI_ROPE (qkv): each wave's 4 rows are two RoPE pairs of one head, so q / k are rotated in
+//     the epilogue and written straight to the attention input and the KV cache (no rope_append);
 //   * PRO_NORMX (qkv, gate_up, lm_head): every wave sums the 64 accumulators (one load, a wave
 //     reduction), rstd = rsqrt(sum / K + eps), and the K loop feeds bf16(h * rstd * g) to the FMAs
 //     (the separate norm kernel's rounding).
@@ -47,7 +49,7 @@ __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g))
 // input transform of x
 enum { PRO_NONE = 0, PRO_SWI = 1, PRO_NORMX = 2 };
 // output
-enum { EPI_NONE = 0, EPI_RESNORM = 1 };
+enum { EPI_NONE = 0, EPI_RESNORM = 1, EPI_ROPE = 2 };
 
 constexpr float kSumsqScale = 1048576.f;  // 2^20: fixed-point units of the sum-of-squares accumulator
 constexpr int kSumsqSlots = 64;           // accumulator addresses per row: workgroup b adds into b % 64
@@ -67,6 +69,16 @@ struct GemvArgs {
   int64_t ldr;
   unsigned long long* sumsq_out;   // [M][kSumsqSlots], zero at launch
   unsigned long long* sumsq_zero;  // [M][kSumsqSlots], zeroed here for the next producer
+  // EPI_ROPE (the qkv projection, head_dim 128): q rotated into q_out [M, hq, 128], k rotated and v
+  // written at cache slot pos[m] of kc / vc (row m = batch row m)
+  bf16* q_out;
+  bf16* kc;
+  bf16* vc;
+  int64_t c_bs, c_ss, c_hs, v_bs, v_ss, v_hs;
+  const float* cosb;  // [>= rope_S, 64]
+  const float* sinb;
+  const int* pos;     // [M]
+  int rope_S, cache_L, hq, hkv;
 };
 
 // KS waves of the workgroup split K for the same kR rows (KS = 4: 4x the workgroups and weight
@@ -82,6 +94,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(const GemvArgs a) {
   const int slot = wave / KS, kp = wave % KS;
   const int n0 = (blockIdx.x * (4 / KS) + slot) * kR;
   const int N = a.N, K = a.K;
+  // EPI_ROPE: the wave's 4 rows are the RoPE pairs (d, d + 64), (d + 1, d + 65) of one head, so the
+  // rotation happens in the epilogue: rows hh*128 + {d, d+1, d+64, d+65}, d = 2 * (group % 32)
+  const int hh = n0 / 128, d0 = 2 * ((n0 / kR) % 32);
+  auto row_of = [&](int r) { return EPI == EPI_ROPE ? hh * 128 + d0 + (r & 1) + 64 * (r >> 1) : n0 + r; };
   const bf16* __restrict__ x = a.x;
   float acc[M][kR];
 #pragma unroll
@@ -99,7 +115,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(const GemvArgs a) {
   float rstd[M];
   const u32x4* wr[kR];
 #pragma unroll
-  for (int r = 0; r < kR; ++r) wr[r] = reinterpret_cast<const u32x4*>(a.w + (int64_t)min(n0 + r, N - 1) * K);
+  for (int r = 0; r < kR; ++r) wr[r] = reinterpret_cast<const u32x4*>(a.w + (int64_t)min(row_of(r), N - 1) * K);
   auto kstep = [&](int k, auto first, bool valid) {
     u32x4 wv[kR];
 #pragma unroll
@@ -180,7 +196,36 @@ __global__ __launch_bounds__(256) void gemv_kernel(const GemvArgs a) {
         }
     }
   }
-  if constexpr (EPI == EPI_NONE) {
+  if constexpr (EPI == EPI_ROPE) {
+    if (lane == 0 && kp == 0) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        const int p = a.pos[m];
+        if (p < 0 || p >= a.rope_S || p >= a.cache_L) continue;  // like rope_append: no write
+        float y[kR];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) y[r] = static_cast<float>(static_cast<bf16>(acc[m][r]));  // the bf16 qkv
+        float o[kR];
+        bf16* dst;
+        if (hh < a.hq + a.hkv) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const float cs = a.cosb[(int64_t)p * 64 + d0 + i], sn = a.sinb[(int64_t)p * 64 + d0 + i];
+            o[i] = y[i] * cs - y[i + 2] * sn;
+            o[i + 2] = y[i + 2] * cs + y[i] * sn;
+          }
+          dst = hh < a.hq ? a.q_out + ((int64_t)m * a.hq + hh) * 128
+                          : a.kc + m * a.c_bs + (int64_t)p * a.c_ss + (int64_t)(hh - a.hq) * a.c_hs;
+        } else {
+#pragma unroll
+          for (int r = 0; r < kR; ++r) o[r] = y[r];
+          dst = a.vc + m * a.v_bs + (int64_t)p * a.v_ss + (int64_t)(hh - a.hq - a.hkv) * a.v_hs;
+        }
+#pragma unroll
+        for (int r = 0; r < kR; ++r) dst[d0 + (r & 1) + 64 * (r >> 1)] = static_cast<bf16>(o[r]);
+      }
+    }
+  } else if constexpr (EPI == EPI_NONE) {
     if (lane == 0 && kp == 0) {
 #pragma unroll
       for (int m = 0; m < M; ++m)
@@ -270,8 +315,14 @@ void gemv_fused_bf16(const GemvFused& f, hipStream_t s) {
   a.y = static_cast<bf16*>(f.y), a.ldy = f.ldy, a.N = f.N, a.K = f.K;
   a.g = static_cast<const bf16*>(f.g), a.eps = f.eps, a.sumsq_in = f.sumsq_in;
   a.res = static_cast<const bf16*>(f.res), a.ldr = f.ldr, a.sumsq_out = f.sumsq_out, a.sumsq_zero = f.sumsq_zero;
-  const bool normx = f.sumsq_in != nullptr, resnorm = f.res != nullptr;
-  if (normx && resnorm) launch_ks<PRO_NORMX, EPI_RESNORM>(a, f.M, s);
+  a.q_out = static_cast<bf16*>(f.q_out), a.kc = static_cast<bf16*>(f.kc), a.vc = static_cast<bf16*>(f.vc);
+  a.c_bs = f.c_bs, a.c_ss = f.c_ss, a.c_hs = f.c_hs, a.v_bs = f.v_bs, a.v_ss = f.v_ss, a.v_hs = f.v_hs;
+  a.cosb = f.cosb, a.sinb = f.sinb, a.pos = f.pos, a.rope_S = f.rope_S, a.cache_L = f.cache_L;
+  a.hq = f.hq, a.hkv = f.hkv;
+  const bool normx = f.sumsq_in != nullptr, resnorm = f.res != nullptr, rope = f.q_out != nullptr;
+  if (rope && normx) launch_ks<PRO_NORMX, EPI_ROPE>(a, f.M, s);
+  else if (rope) launch_ks<PRO_NONE, EPI_ROPE>(a, f.M, s);
+  else if (normx && resnorm) launch_ks<PRO_NORMX, EPI_RESNORM>(a, f.M, s);
   else if (normx) launch_ks<PRO_NORMX, EPI_NONE>(a, f.M, s);
   else if (resnorm && f.swiglu) launch_ks<PRO_SWI, EPI_RESNORM>(a, f.M, s);
   else if (resnorm) launch_ks<PRO_NONE, EPI_RESNORM>(a, f.M, s);

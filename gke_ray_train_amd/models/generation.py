@@ -147,6 +147,8 @@ def _norm_fusable(model, B: int) -> bool:
     norms = [m.norm] + [n for ly in m.layers for n in (ly.input_layernorm, ly.post_attention_layernorm)]
     lins = [model.lm_head] + [p for ly in m.layers for p in (ly.self_attn.qkv_proj, ly.self_attn.o_proj,
                                                                ly.mlp.gate_up_proj, ly.mlp.down_proj)]
+    if model.config.head_dim != 128:  # the RoPE epilogue / decode attention kernels
+        return False
     return (all(_plain_bf16_linear(p) for p in lins)
             and all(n.weight.dtype == torch.bfloat16 and n.weight.is_contiguous() and n.weight.data_ptr() % 16 == 0
                     for n in norms))
@@ -163,19 +165,21 @@ class _NormWorkspace:
 
 def _fused_norm_layer_step(layer, h, first: bool, ws: _NormWorkspace, B, cos, sin, cache: KVCache, li: int,
                            pos_b, lens):
-    """One-token layer step with the residual adds and RMSNorms inside the GEMVs: o_proj / down_proj
-    write h = y + residual and add sum(h^2) to a fixed-point accumulator, qkv / gate_up normalise
-    their input on the fly from (h, accumulator, norm weight). ``h`` IS the residual stream between
+    """One-token layer step with the residual adds, RMSNorms and RoPE inside the GEMVs: o_proj /
+    down_proj write h = y + residual and add sum(h^2) to a fixed-point accumulator, qkv / gate_up
+    normalise their input on the fly from (h, accumulator, norm weight), and the qkv epilogue
+    rotates q / k and appends k / v to the cache. ``h`` IS the residual stream between
     layers; slot 0 carries the post-attention norm's statistics, slot 1 the next input norm's."""
     K = _native.kernels()
     attn, mlp = layer.self_attn, layer.mlp
     ln1, ln2 = layer.input_layernorm, layer.post_attention_layernorm
-    if first:  # layer 0: h is the embedding (no residual add, no producer GEMV summed its squares)
-        qkv = K.gemv(ops.rms_norm(h, ln1.weight, ln1.eps), attn.qkv_proj.weight)
-    else:
-        qkv = K.gemv_fused(h, attn.qkv_proj.weight, ws.sumsq, 1, g=ln1.weight, eps=ln1.eps)
     hq, hkv, D = attn.hq, attn.hkv, attn.hd
-    q = K.rope_append(qkv, cos, sin, pos_b, hq, hkv, D, cos.shape[0], cache.k[li], cache.v[li], 1)
+    # the qkv GEMV's epilogue applies RoPE and appends k / v to the cache (no rope_append launch)
+    rope = dict(cos=cos, sin=sin, pos=pos_b, kc=cache.k[li], vc=cache.v[li], hq=hq, hkv=hkv)
+    if first:  # layer 0: h is the embedding (no residual add, no producer GEMV summed its squares)
+        q = K.gemv_fused(ops.rms_norm(h, ln1.weight, ln1.eps), attn.qkv_proj.weight, ws.sumsq, 1, **rope)
+    else:
+        q = K.gemv_fused(h, attn.qkv_proj.weight, ws.sumsq, 1, g=ln1.weight, eps=ln1.eps, **rope)
     o = ops.flash_attention(q.view(B, 1, hq, D), cache.k[li], cache.v[li], causal=False, seqlens_k=lens)
     h = K.gemv_fused(o.reshape(B, hq * D), attn.o_proj.weight, ws.sumsq, 0, res=h)
     gu = K.gemv_fused(h, mlp.gate_up_proj.weight, ws.sumsq, 0, g=ln2.weight, eps=ln2.eps)

@@ -988,6 +988,48 @@ def test_gemv_normx_prologue(M, N, K):
     _close(y, ref, 2e-2, 2e-2, "gemv normx vs fp32")
 
 
+@pytest.mark.parametrize("M,hq,hkv,normx", [(1, 32, 8, True), (2, 8, 8, False), (2, 4, 1, True)])
+def test_gemv_rope_epilogue(M, hq, hkv, normx):
+    """qkv GEMV with the RoPE + KV-cache append epilogue == GEMV + rope_append (q bitwise, cache
+    slots bitwise, untouched slots unchanged); an out-of-range position writes nothing."""
+    C, D, L = _C(), 128, 16
+    g = torch.Generator(device=DEV).manual_seed(M * hq + hkv)
+    K = 512
+    N = (hq + 2 * hkv) * D
+    h = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16, generator=g) * 0.05
+    nw = (1 + 0.1 * torch.randn(K, device=DEV, generator=g)).to(torch.bfloat16)
+    acc = torch.zeros(2, M, 64, dtype=torch.int64, device=DEV)
+    acc[1, :, 0] = torch.round(h.double().pow(2).sum(-1) * 2 ** 20).long()
+    ang = torch.arange(L, device=DEV, dtype=torch.float32)[:, None] * torch.rand(64, device=DEV, generator=g)
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    pos = torch.tensor([3, 11][:M], device=DEV, dtype=torch.int32)
+    if M == 2 and hq == 8:
+        pos[1] = L + 5  # past the cache / rope table: no write for that row
+    kc0 = torch.randn(M, L, hkv, D, device=DEV, dtype=torch.bfloat16, generator=g)
+    vc0 = torch.randn(M, L, hkv, D, device=DEV, dtype=torch.bfloat16, generator=g)
+    kc, vc, kr, vr = kc0.clone(), vc0.clone(), kc0.clone(), vc0.clone()
+    if normx:
+        q = C.gemv_fused(h, w, acc, 1, g=nw, eps=1e-5, cos=cos, sin=sin, pos=pos, kc=kc, vc=vc, hq=hq, hkv=hkv)
+        qkv = C.gemv_fused(h, w, acc, 1, g=nw, eps=1e-5)
+    else:
+        q = C.gemv_fused(h, w, acc, 1, cos=cos, sin=sin, pos=pos, kc=kc, vc=vc, hq=hq, hkv=hkv)
+        qkv = C.gemv(h, w)
+    qr = C.rope_append(qkv, cos, sin, pos, hq, hkv, D, L, kr, vr, 1)
+    ok = (pos < L).tolist()
+    for m in range(M):  # same bf16 qkv; the rotation's fp32 contraction may differ by an ulp
+        if ok[m]:
+            _close(q[m], qr[m].view(hq, D), 1e-2, 1e-2, "rope epilogue q")
+    _close(kc, kr, 1e-2, 1e-2, "rope epilogue k cache")
+    assert torch.equal(vc, vr)
+    assert not torch.equal(kc, kc0) and not torch.equal(vc, vc0)
+    for m in range(M):  # only the slot at pos[m] changed
+        keep = torch.ones(L, dtype=torch.bool)
+        if ok[m]:
+            keep[int(pos[m])] = False
+        assert torch.equal(kc[m, keep], kc0[m, keep]) and torch.equal(vc[m, keep], vc0[m, keep])
+
+
 def test_decode_fused_norm_matches_unfused():
     """GraphDecoder with the residual adds / norms inside the GEMVs == the unfused decode
     (GRT_GEMV_NORM=0 path): same greedy tokens, logits within bf16 rounding."""
