@@ -11,3 +11,4 @@ timeout -k 10 300 python bench.py > $OUT/bench2.log 2>&1; rc=$?; tail -1 $OUT/be
 bash scripts/gpu_prof.sh $OUT/prof --steps 6 --warmup 3; rc=$?; fatal $rc
 f=$(find $OUT/prof -name "*kernel_trace.csv" | head -1)
 python3 tools/prof_steps.py "$f" 9 > $OUT/step_breakdown.md 2>&1; head -40 $OUT/step_breakdown.md
+rm -rf $OUT/prof

@@ -96,5 +96,5 @@ def test_cross_entropy_sweep(rows, V, ignore):
     lr = torch.nn.functional.cross_entropy(hr @ wr.t(), lab, ignore_index=-100)
     lr.backward()
     if (lab != -100).any():
-        assert abs(float(loss) - float(lr)) < 2e-2 * max(1.0, abs(float(lr)))
+        assert abs(float(loss.detach()) - float(lr.detach())) < 2e-2 * max(1.0, abs(float(lr.detach())))
         assert _rel(h.grad, hr.grad) < 3e-2 and _rel(w.grad, wr.grad) < 3e-2
