@@ -6,7 +6,7 @@ read a norm's output, the on-the-fly normalisation against the add_rms_norm kern
 the projections that produce the residual stream, the residual-add + rstd epilogue. One JSON line
 per shape.
 
-    python tools/gemv_bench.py [--m 1] [--reps 50]
+    python tools/gemv_bench.py [--m 1] [--reps 50] [--flush]
 """
 import argparse
 import json
@@ -25,12 +25,17 @@ NORM_INPUT = ("qkv", "gate_up", "lm_head")  # the projections that consume a nor
 NORM_PRODUCER = ("o", "down_swiglu")         # ... and the ones whose output is the next residual
 
 
+FLUSH = None  # --flush: a 1 GiB read between timed calls evicts the weights from L2 / the MALL
+
+
 def med(fn, reps):
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
+        if FLUSH is not None:
+            FLUSH.sum()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         fn()
@@ -44,7 +49,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=1)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--flush", action="store_true",
+                    help="evict the weights between calls (the decode step reads 16 GB between two uses)")
     a = ap.parse_args()
+    global FLUSH
+    if a.flush:
+        FLUSH = torch.ones(2 ** 28, device="cuda")
     C = _native.kernels()
     dev = torch.device("cuda")
     ws = torch.zeros(C.sumsq_blocks(), device=dev)
