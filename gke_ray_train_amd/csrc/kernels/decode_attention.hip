@@ -44,6 +44,16 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(const AttnDecode
   const int per = ((len + p.NS - 1) / p.NS + 15) / 16 * 16;
   const int k0 = split * per, k1 = min(len, k0 + per);
 
+  const bf16* Kb = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs + c * 8;
+  const bf16* Vb = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs + c * 8;
+  // the K / V stream is pipelined one step ahead, and its first loads are issued before the query
+  // loads, so the two dependent round trips at the start overlap (most splits are 1-2 steps long)
+  int j = k0 + wave * 4 + grp;
+  u32x4 kraw{}, vraw{};
+  if (j < k1) {
+    kraw = *reinterpret_cast<const u32x4*>(Kb + (int64_t)j * p.k_ss);
+    vraw = *reinterpret_cast<const u32x4*>(Vb + (int64_t)j * p.v_ss);
+  }
   float q[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -60,12 +70,14 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(const AttnDecode
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[g][i] = 0.f;
   }
-  const bf16* Kb = (const bf16*)p.k + (int64_t)b * p.k_bs + (int64_t)hkv * p.k_hs + c * 8;
-  const bf16* Vb = (const bf16*)p.v + (int64_t)b * p.v_bs + (int64_t)hkv * p.v_hs + c * 8;
-  for (int j = k0 + wave * 4 + grp; j < k1; j += 16) {
+  for (; j < k1; j += 16) {
     float kf[8], vf[8];
-    cvt8(*reinterpret_cast<const u32x4*>(Kb + (int64_t)j * p.k_ss), kf);
-    cvt8(*reinterpret_cast<const u32x4*>(Vb + (int64_t)j * p.v_ss), vf);
+    cvt8(kraw, kf);
+    cvt8(vraw, vf);
+    if (j + 16 < k1) {
+      kraw = *reinterpret_cast<const u32x4*>(Kb + (int64_t)(j + 16) * p.k_ss);
+      vraw = *reinterpret_cast<const u32x4*>(Vb + (int64_t)(j + 16) * p.v_ss);
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       float s = 0.f;
