@@ -75,7 +75,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])  # 8: the full node's rank count (kIpcMaxRanks), peers on one card
 def test_ipc_allreduce_matches_host_sum(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
