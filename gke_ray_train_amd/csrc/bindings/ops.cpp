@@ -1047,8 +1047,6 @@ Tensor gemv_fused(const Tensor& x, const Tensor& w, const Tensor& sumsq, int64_t
   return y;
 }
 
-int64_t gemv_workgroups(int64_t N) { return grt::gemv_workgroups((int)N); }
-
 // ------------------------------------------------------------------ embedding
 Tensor embedding_fwd(const Tensor& ids, const Tensor& w) {
   check_contig(ids, "ids");
@@ -1352,7 +1350,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("swiglu") = false, py::arg("g") = py::none(), py::arg("res") = py::none(), py::arg("eps") = 1e-5,
         py::arg("cos") = py::none(), py::arg("sin") = py::none(), py::arg("pos") = py::none(),
         py::arg("kc") = py::none(), py::arg("vc") = py::none(), py::arg("hq") = 0, py::arg("hkv") = 0);
-  m.def("gemv_workgroups", &gemv_workgroups);
   m.def("attn_decode", &attn_decode);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);

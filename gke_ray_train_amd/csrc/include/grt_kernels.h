@@ -312,6 +312,7 @@ void gemv_bf16(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, 
 //   (x = the residual stream h, sumsq_in [M][64] its fixed-point partial sums of squares);
 //   res != null: y = bf16(x W^T) + res (the next h); its sums of squares are added into sumsq_out
 //   [M][64] (zero at launch) and sumsq_zero [M][64] is zeroed for the next producer.
+// gemv_workgroups(N): grid size of a GEMV with N output rows.
 struct GemvFused {
   const void* x;
   int64_t ldx;
