@@ -139,7 +139,7 @@ def test_lora_model_grads_kernels_vs_library(monkeypatch, p):
         loss.backward()
         ddp.finish_gradient_sync()
         grads = {i: b.float().clone() for i, b in enumerate(ddp.grad_buffers())}
-        res[on] = (float(loss), grads)
+        res[on] = (float(loss.detach()), grads)
         if on:
             assert any(getattr(lm, "_bt", None) is not None for lm in pm.lora_modules.values())
     (l1, g1), (l0, g0) = res[True], res[False]
