@@ -63,9 +63,10 @@ def test_ulysses_matches_full_sequence(world):
     from gke_ray_train_amd.models import build_llama
     m = build_llama("llama-tiny-gqa", device="cpu", dtype=torch.float32, seed=3)
     ids = _ids()
-    ref = m(ids, labels=ids)["loss"]
-    ref.backward()
-    assert abs(res[0][0] - float(ref)) < 1e-5 * max(1.0, abs(float(ref))), (res[0][0], float(ref))
+    loss = m(ids, labels=ids)["loss"]
+    loss.backward()
+    ref = float(loss.detach())
+    assert abs(res[0][0] - ref) < 1e-5 * max(1.0, abs(ref)), (res[0][0], ref)
     for n, p in m.named_parameters():
         g = torch.from_numpy(res[0][1][n])
         assert torch.allclose(g, p.grad, atol=2e-6, rtol=1e-4), f"{n}: {(g - p.grad).abs().max()}"
