@@ -1030,19 +1030,20 @@ def test_gemv_rope_epilogue(M, hq, hkv, normx):
         assert torch.equal(kc[m, keep], kc0[m, keep]) and torch.equal(vc[m, keep], vc0[m, keep])
 
 
-def test_decode_fused_norm_matches_unfused():
-    """GraphDecoder with the residual adds / norms inside the GEMVs == the unfused decode
-    (GRT_GEMV_NORM=0 path): same greedy tokens, logits within bf16 rounding."""
+@pytest.mark.parametrize("B", [1, 2])
+def test_decode_fused_norm_matches_unfused(B):
+    """GraphDecoder with the residual adds / norms / RoPE inside the GEMVs == the unfused decode
+    (GRT_GEMV_NORM=0 path): same greedy tokens, logits within bf16 rounding (1 and 2 rows)."""
     from gke_ray_train_amd.models import build_llama
     from gke_ray_train_amd.models import generation as G
     torch.manual_seed(0)
     m = build_llama("llama-tiny-gqa", device=DEV, dtype=torch.bfloat16, seed=0).eval()
-    ids = torch.randint(0, m.config.vocab_size, (1, 12), device=DEV)
+    ids = torch.randint(0, m.config.vocab_size, (B, 12), device=DEV)
     outs = []
     for fused in (True, False):
         G._GEMV_NORM = fused
         try:
-            dec = G.GraphDecoder(m, 1, 32)
+            dec = G.GraphDecoder(m, B, 32)
             assert (dec.norm_ws is not None) == fused
             lg = [dec.prefill(ids)]
             nxt = lg[-1].argmax(-1)
