@@ -953,7 +953,8 @@ void transpose_into(const Tensor& src, Tensor& dst) {
   grt::transpose_bf16(src.data_ptr(), dst.data_ptr(), (int)R, (int)Cc, cur_stream(src));
 }
 
-// y = x W^T for 1-4 rows; swiglu: x = [gate | up] [M, 2K] -> y = (silu(gate) * up) W^T
+// y = x W^T for 1-4 rows (1-16 rows when K % 256 == 0: 3+ rows run on MFMA); swiglu: x = [gate | up]
+// [M, 2K] -> y = (silu(gate) * up) W^T
 Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
   check_cuda(x, "x");
   check_contig(w, "w");
@@ -961,7 +962,8 @@ Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
               swiglu ? "gemv_swiglu: gu [M, 2K], w [N, K]" : "gemv: x [M, K], w [N, K]");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "gemv: bf16");
   const int64_t M = x.size(0), N = w.size(0), K = w.size(1);
-  TORCH_CHECK(M >= 1 && M <= 4, "gemv: 1..4 rows");
+  TORCH_CHECK((M >= 1 && M <= 4) || (!swiglu && grt::gemv_mfma_ok((int)M, (int)K)),
+              "gemv: 1..4 rows (5..16 without swiglu and with K % 256 == 0)");
   TORCH_CHECK(K % 8 == 0 && x.stride(1) == 1 && x.stride(0) % 8 == 0, "gemv: K and row stride multiples of 8");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0,
               "gemv: 16-byte alignment");

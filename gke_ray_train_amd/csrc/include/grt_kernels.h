@@ -307,6 +307,8 @@ void transpose_bf16(const void* src, void* dst, int rows, int cols, hipStream_t 
 // swiglu: x is the fused [gate | up] output [M, 2K] and the GEMV input is silu(gate) * up
 void gemv_bf16(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int M, int N, int K, hipStream_t s,
                bool swiglu = false);
+// 3 <= M <= 16 and K % 256 == 0 (no swiglu): gemv_bf16 runs the MFMA skinny kernel (M up to 16)
+bool gemv_mfma_ok(int M, int K);
 // The decode step's residual adds / RMSNorms folded into the GEMVs (gemv.hip header):
 //   sumsq_in != null: the GEMV input is bf16(x * rsqrt(sum_j sumsq_in[m][j] * 2^-20 / K + eps) * g)
 //   (x = the residual stream h, sumsq_in [M][64] its fixed-point partial sums of squares);

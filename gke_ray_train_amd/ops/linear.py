@@ -297,6 +297,14 @@ _GEMV = os.environ.get("GRT_GEMV", "1") != "0"
 # 285 vs 210 tok/s, batch 4 688 vs 793, batch 8 746 vs 1506 — profiles/r2_decode_batch_gemv.txt:
 # the activations, re-read by every wave, and the per-row FMAs outgrow the weight stream)
 GEMV_MAX_ROWS = int(os.environ.get("GRT_GEMV_MAX_ROWS", "2"))
+# 3-8 rows with K % 256 == 0: the MFMA skinny kernel (gemv.hip gemv_mfma_kernel; the kernel takes up
+# to 16). Llama-3.1-8B graph decode vs the library GEMM: batch 4 870 vs 795 tokens/s, batch 8 1564
+# vs 1539, batch 16 2536 vs 2729 (profiles/r5_decode.md) — so the library keeps 9+ rows
+GEMV_MFMA_MAX_ROWS = int(os.environ.get("GRT_GEMV_MFMA_MAX_ROWS", "8"))
+
+
+def _gemv_rows_ok(rows: int, K: int) -> bool:
+    return rows <= GEMV_MAX_ROWS or (rows <= GEMV_MFMA_MAX_ROWS and K % 256 == 0)
 
 
 def linear(x, weight, bias=None):
@@ -305,7 +313,7 @@ def linear(x, weight, bias=None):
     K = weight.shape[-1]
     if (_GEMV and x.is_cuda and not torch.is_grad_enabled() and x.dtype == torch.bfloat16
             and weight.dtype == torch.bfloat16 and weight.dim() == 2 and weight.is_contiguous()
-            and x.numel() // K <= GEMV_MAX_ROWS and K % 8 == 0 and x.shape[-1] == K):
+            and _gemv_rows_ok(x.numel() // K, K) and K % 8 == 0 and x.shape[-1] == K):
         # decode: 1-2 tokens per step are a weight stream -> HBM-bound GEMV kernel (gemv.hip)
         from .. import _native
         x2 = x.reshape(-1, K)

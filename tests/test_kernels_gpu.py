@@ -906,14 +906,26 @@ def test_gemv_decode(M, N, K):
     y = _C().gemv(x, w)
     ref = x.float() @ w.float().t()
     _close(y, ref, 2e-2, 2e-2, "gemv")
-    from gke_ray_train_amd.ops.linear import GEMV_MAX_ROWS
+    from gke_ray_train_amd.ops.linear import _gemv_rows_ok
     with torch.no_grad():
         y2 = linear(x.view(M, 1, K), w)
     assert y2.shape == (M, 1, N)
-    if M <= GEMV_MAX_ROWS:  # routed to the GEMV
+    if _gemv_rows_ok(M, K):  # routed to the GEMV (FMA for 1-2 rows, MFMA for 3-16)
         assert torch.equal(y2.view(M, N), y)
-    else:  # the library GEMM (faster from 3-4 rows on)
+    else:  # the library GEMM
         _close(y2.view(M, N), ref, 2e-2, 2e-2, "linear (library) at M rows")
+
+
+@pytest.mark.parametrize("M", [3, 5, 8, 16])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1000, 11008), (37, 512), (20000, 256)])
+def test_gemv_mfma_rows(M, N, K):
+    """Skinny MFMA GEMM for 3-16 decode rows (gemv.hip gemv_mfma_kernel, both wave counts, ragged N)
+    vs the fp32 product."""
+    g = torch.Generator(device=DEV).manual_seed(M * N + K)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16, generator=g) * 0.02
+    y = _C().gemv(x, w)
+    _close(y, x.float() @ w.float().t(), 2e-2, 2e-2, "gemv_mfma")
 
 
 @pytest.mark.parametrize("M", [1, 3])
