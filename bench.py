@@ -419,6 +419,9 @@ def run(a):
     if not cpu:
         torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if world > 1:  # a failed xGMI IPC collective (parallel/ipc.py) fails the run instead of timing it
+        from gke_ray_train_amd.parallel.ipc import check_all
+        check_all()
     if prof is not None:
         prof.__exit__(None, None, None)
         os.makedirs(a.profile_dir, exist_ok=True)

@@ -360,8 +360,15 @@ struct IpcPeers {
   int rank, world;
   uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
 };
-// signal buffer: [2 phases][kIpcMaxBlocks][kIpcMaxRanks] uint32
-constexpr int64_t kIpcSignalBytes = 2LL * kIpcMaxBlocks * kIpcMaxRanks * 4;
+// signal buffer: [2 phases][kIpcMaxBlocks][kIpcMaxRanks] uint32 flags, then one abort word that any
+// peer sets (system scope) when a wait of its own timed out, padded to 256 bytes.
+constexpr int kIpcAbortWord = 2 * kIpcMaxBlocks * kIpcMaxRanks;
+constexpr int64_t kIpcSignalBytes = 2LL * kIpcMaxBlocks * kIpcMaxRanks * 4 + 256;
+// error word bits: bit r (< kIpcMaxRanks) = a wait for rank r timed out here; kIpcErrAborted = a peer
+// announced a timeout; kIpcErrSkipped = a later call found the word set and did not run. Any set bit
+// makes every later call of the communicator write NaN to its output without waiting (fail-stop).
+constexpr uint32_t kIpcErrAborted = 1u << 30;
+constexpr uint32_t kIpcErrSkipped = 1u << 31;
 int ipc_blocks_for(int64_t nbytes, bool two_shot);
 // out = scale * sum over ranks of in (nbytes a multiple of 16, <= cap); in == out allowed.
 void ipc_allreduce(const IpcPeers& peers, uint32_t epoch, DType dt, const void* in, void* out, int64_t nbytes,

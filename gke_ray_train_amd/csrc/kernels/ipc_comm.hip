@@ -22,8 +22,15 @@
 // in call e+2, after it passed call e+1's start barrier, which needs our e+1 flag, which we set
 // after finishing every read of call e.
 //
-// Every wait is bounded by a wall-clock timeout (s_memrealtime, 100 MHz): a missing peer makes
-// the kernel record an error word and finish instead of spinning forever.
+// Every wait is bounded by a wall-clock timeout (s_memrealtime, 100 MHz). Failure is fail-stop, never
+// a silent wrong sum:
+//   * a timed-out wait records the peer in the local error word, sets the abort word of EVERY rank
+//     (so their pending and later calls stop waiting too) and the block writes NaN over its output;
+//   * every call first reads the local error word and its own abort word: if either is set it
+//     writes NaN over its whole output and returns without touching flags or peer memory;
+//   * the host raises on the error word at its next synchronisation point (IpcCommunicator.check,
+//     parallel/ipc.check_all from train.report / the SFT trainer / bench), and a NaN gradient or
+//     grad norm is what any step that consumed a poisoned result sees in the meantime.
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
@@ -55,13 +62,18 @@ __device__ __forceinline__ uint32_t* flag_ptr(uint32_t* base, int phase, int blo
   return base + ((phase * kIpcMaxBlocks + block) * kIpcMaxRanks + src);
 }
 
+__device__ __forceinline__ uint32_t* abort_ptr(uint32_t* base) { return base + kIpcAbortWord; }
+
 // Block-wide barrier across ranks for (phase, block). Producer side (MI355X_MICROARCH.md,
 // "Valid forms"): every storing wave drains its stores, workgroup barrier, then lane i < world
 // releases at SYSTEM scope (L2 write-back: the peer reads our HBM through the fabric), drains
 // again (compiler hazard: the release's wait can be dropped) and stores the flag into rank i's
 // signal array. Consumer side: one relaxed poll, one system-scope acquire, drain, barrier.
-__device__ void cross_rank_barrier(const IpcArgs& a, int phase) {
+// Returns false (block-uniform) when a wait timed out or a peer announced an abort: the caller
+// then poisons its output instead of reading peer buffers.
+__device__ bool cross_rank_barrier(const IpcArgs& a, int phase, int* s_fail) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (threadIdx.x == 0) *s_fail = 0;
   __syncthreads();
   const int b = blockIdx.x;
   if (threadIdx.x < (unsigned)a.world) {
@@ -71,13 +83,26 @@ __device__ void cross_rank_barrier(const IpcArgs& a, int phase) {
     __hip_atomic_store(flag_ptr(a.signal[peer], phase, b, a.rank), a.epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mine = flag_ptr(a.signal[a.rank], phase, b, peer);
+    uint32_t* my_abort = abort_ptr(a.signal[a.rank]);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (true) {
       const uint32_t v = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       if ((int32_t)(v - a.epoch) >= 0) break;
+      if (__hip_atomic_load(my_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+        // a peer gave up on this (or an earlier) call: stop waiting, fail this call here too
+        __hip_atomic_fetch_or(a.err, kIpcErrAborted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_fail = 1;  // benign race: every writer stores 1
+        break;
+      }
       if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
-        // a peer never arrived: record it and finish (garbage result, no hang)
+        // the peer never arrived: record it, tell every rank (their waits on us or on it end now)
         __hip_atomic_fetch_or(a.err, 1u << (peer & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int r = 0; r < a.world; ++r) {  // (release per store: the timeout path, never hot)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(abort_ptr(a.signal[r]), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        *s_fail = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -86,6 +111,30 @@ __device__ void cross_rank_barrier(const IpcArgs& a, int phase) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  return *s_fail == 0;
+}
+
+// Entry check of every call: a set local error word or abort word means an earlier call (here or
+// on a peer) failed; the call must not wait or read peers (their parities may be stale).
+__device__ bool comm_poisoned(const IpcArgs& a, int* s_fail) {
+  if (threadIdx.x == 0) {
+    const uint32_t e = __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ab = __hip_atomic_load(abort_ptr(a.signal[a.rank]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const bool bad = e != 0u || ab != 0u;
+    if (bad)
+      __hip_atomic_fetch_or(a.err, kIpcErrSkipped | (ab != 0u ? kIpcErrAborted : 0u), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+    *s_fail = bad ? 1 : 0;
+  }
+  __syncthreads();
+  return *s_fail != 0;
+}
+
+// NaN over chunks [c0, c1) of the output (fp32 quiet NaN / a pair of bf16 quiet NaNs per word)
+template <bool BF16>
+__device__ void poison_range(uint4* out, int64_t c0, int64_t c1) {
+  const uint32_t w = BF16 ? 0x7fc07fc0u : 0x7fc00000u;
+  for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) out[c] = make_uint4(w, w, w, w);
 }
 
 __device__ __forceinline__ float bf16_lo(uint32_t w) { return __uint_as_float(w << 16); }
@@ -143,9 +192,17 @@ __global__ __launch_bounds__(kThreads) void ipc_allreduce_kernel(const IpcArgs a
   const int64_t c0 = (int64_t)blockIdx.x * per;
   const int64_t c1 = c0 + per < nchunks ? c0 + per : nchunks;
   const int64_t par = (int64_t)(a.epoch & 1u) * a.cap;
+  __shared__ int s_fail;
+  if (comm_poisoned(a, &s_fail)) {
+    poison_range<BF16>(out, c0, c1);
+    return;
+  }
   uint4* mine = reinterpret_cast<uint4*>(static_cast<char*>(a.staging[a.rank]) + par);
   for (int64_t c = c0 + threadIdx.x; c < c1; c += blockDim.x) mine[c] = in[c];
-  cross_rank_barrier(a, 0);
+  if (!cross_rank_barrier(a, 0, &s_fail)) {
+    poison_range<BF16>(out, c0, c1);
+    return;
+  }
   if (!TWO_SHOT) {
     reduce_range<BF16>(a, a.staging, par, c0, c1, out, scale);
     return;
@@ -157,7 +214,10 @@ __global__ __launch_bounds__(kThreads) void ipc_allreduce_kernel(const IpcArgs a
   const int64_t s1 = s0 + sub < c1 ? s0 + sub : c1;
   uint4* res = reinterpret_cast<uint4*>(static_cast<char*>(a.result[a.rank]) + par);
   reduce_range<BF16>(a, a.staging, par, s0, s1, res, scale);
-  cross_rank_barrier(a, 1);
+  if (!cross_rank_barrier(a, 1, &s_fail)) {
+    poison_range<BF16>(out, c0, c1);
+    return;
+  }
   for (int r = 0; r < a.world; ++r) {
     const int64_t g0 = c0 + (int64_t)r * sub < c1 ? c0 + (int64_t)r * sub : c1;
     const int64_t g1 = g0 + sub < c1 ? g0 + sub : c1;
@@ -167,7 +227,11 @@ __global__ __launch_bounds__(kThreads) void ipc_allreduce_kernel(const IpcArgs a
 }
 
 // Barrier only (no payload): phase-0 flags of block 0.
-__global__ __launch_bounds__(64) void ipc_barrier_kernel(const IpcArgs a) { cross_rank_barrier(a, 0); }
+__global__ __launch_bounds__(64) void ipc_barrier_kernel(const IpcArgs a) {
+  __shared__ int s_fail;
+  if (comm_poisoned(a, &s_fail)) return;
+  cross_rank_barrier(a, 0, &s_fail);
+}
 
 IpcArgs make_args(const IpcPeers& p, uint32_t epoch) {
   IpcArgs a{};

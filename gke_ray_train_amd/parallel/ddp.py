@@ -245,6 +245,7 @@ class DistributedDataParallel(nn.Module):
         # norm weights) are all-reduced by them on a side stream instead of by RCCL. The decision
         # is a function of the bucket layout only, identical on every rank.
         self._ipc = None
+        self._ipc_tag = None
         self._ipc_limit = 0
         self._ipc_stream = None
         self.ipc_bucket_launches = 0  # buckets all-reduced over IPC so far (tests / logs)
@@ -256,7 +257,8 @@ class DistributedDataParallel(nn.Module):
                 # one communicator per engine: its epoch sequence is driven from this engine's
                 # side stream only (two engines sharing one would interleave calls across streams)
                 DistributedDataParallel._ipc_engines += 1
-                self._ipc = communicator(process_group, f"ddp-buckets-{DistributedDataParallel._ipc_engines}")
+                self._ipc_tag = f"ddp-buckets-{DistributedDataParallel._ipc_engines}"
+                self._ipc = communicator(process_group, self._ipc_tag)
                 if self._ipc is not None:
                     self._ipc_limit = route_limit(ipc_mode(), self._ipc.cap)
                     self._ipc_stream = torch.cuda.Stream(dev0)
@@ -575,3 +577,137 @@ class DistributedDataParallel(nn.Module):
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+    # ------------------------------------------------------------------ portable optimizer state
+    # The flat layout (bucket padding, ZeRO's align x world bucket alignment, the bucket size the
+    # planner picks for the world size) differs between world sizes, so the optimizer state of the
+    # flat parameters cannot be resumed elsewhere. The portable form is HF's optimizer.pt layout: one
+    # state entry per model parameter (index = position among the trainable named_parameters), in
+    # the parameter's shape, plus one param group per engine group (reference checkpoint layout:
+    # ray-jobs/fine_tune_llama_ray.py:313-319).
+    _OPT_KEYS = ("exp_avg", "exp_avg_sq", "master")
+
+    def _named_trainable(self):
+        seen, out = set(), []
+        for n, p in self.module.named_parameters():
+            if p.requires_grad and id(p) not in seen:
+                seen.add(id(p))
+                out.append((n, p))
+        return out
+
+    def _inner_opt(self, optimizer):
+        if hasattr(optimizer, "synchronize"):  # OverlappedOptimizer: pending chunk updates land first
+            optimizer.synchronize()
+        inner = getattr(optimizer, "opt", optimizer)
+        if len(inner.param_groups) != len(self.groups) or any(len(pg["params"]) != 1 for pg in inner.param_groups):
+            raise ValueError("portable optimizer state needs the optimizer built on optimizer_param_groups()")
+        return inner, [pg["params"][0] for pg in inner.param_groups]
+
+    def _gather_flat(self, g, t: torch.Tensor) -> Optional[torch.Tensor]:
+        """Rank 0: the full flat-length state of a group (ZeRO: gathered to host); None elsewhere.
+        ZeRO: every bucket's 1/world chunks are gathered to rank 0 (one collective per bucket)."""
+        if not self.zero:  # replicated: rank 0's own state (device views; the caller snapshots them)
+            return t.detach() if self.rank == 0 else None
+        if self.proxy:
+            raise NotImplementedError("proxy_world engines hold one rank's shard only")
+        W = self.world_size
+        full = torch.zeros(g.flat.numel(), dtype=t.dtype) if self.rank == 0 else None
+        dst = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
+        for b in g.buckets:
+            c = (b.end - b.start) // W
+            if c == 0:
+                continue
+            chunk = t[b.shard_off:b.shard_off + c].contiguous()
+            parts = [torch.empty_like(chunk) for _ in range(W)] if self.rank == 0 else None
+            dist.gather(chunk, parts, dst=dst, group=self.pg)
+            if self.rank == 0:
+                full[b.start:b.end].copy_(torch.cat(parts).to("cpu"))
+        return full
+
+    def portable_optimizer_state_dict(self, optimizer) -> Optional[dict]:
+        """Collective. On rank 0: the optimizer state per model parameter (HF ``optimizer.pt``
+        layout, host tensors in the parameters' shapes); None on the other ranks."""
+        inner, fps = self._inner_opt(optimizer)
+        named = self._named_trainable()
+        index = {id(p): i for i, (_, p) in enumerate(named)}
+        state: Dict[int, dict] = {}
+        groups_out = []
+        for gi, (g, fp) in enumerate(zip(self.groups, fps)):
+            st = inner.state.get(fp, {})
+            groups_out.append(dict({k: v for k, v in inner.param_groups[gi].items() if k != "params"},
+                                   params=sorted(index[id(p)] for p in g.params)))
+            for key in self._OPT_KEYS:
+                v = st.get(key)
+                if not isinstance(v, torch.Tensor):
+                    continue
+                full = self._gather_flat(g, v)
+                if full is not None:
+                    for p, o in zip(g.params, g.offsets):
+                        v = full[o:o + p.numel()].view(p.shape)
+                        # host views are cloned (torch.save would write the whole bucket storage per
+                        # view); device views are copied out by the caller's host snapshot
+                        state.setdefault(index[id(p)], {})[key] = v.clone() if v.device.type == "cpu" else v
+            if self.rank == 0 and isinstance(st.get("step"), torch.Tensor):
+                for p in g.params:
+                    state.setdefault(index[id(p)], {})["step"] = st["step"].detach().to("cpu", torch.float32).clone()
+        if self.rank != 0:
+            return None
+        return {"state": state, "param_groups": groups_out, "grt_param_names": [n for n, _ in named]}
+
+    def load_portable_optimizer_state_dict(self, optimizer, sd: dict):
+        """Every rank: rebuild this engine's flat (or ZeRO shard) optimizer state from a
+        :meth:`portable_optimizer_state_dict` written at ANY world size / sharding."""
+        inner, fps = self._inner_opt(optimizer)
+        named = self._named_trainable()
+        names = [n for n, _ in named]
+        if list(sd.get("grt_param_names", [])) != names:
+            raise ValueError("optimizer state was written for a different set of trainable parameters")
+        index = {id(p): i for i, (_, p) in enumerate(named)}
+        if len(sd["param_groups"]) != len(self.groups):
+            raise ValueError(f"optimizer state has {len(sd['param_groups'])} param groups, the engine {len(self.groups)}")
+        W, r = self.world_size, self.rank
+        for gi, (g, fp) in enumerate(zip(self.groups, fps)):
+            sg = sd["param_groups"][gi]
+            if sorted(sg["params"]) != sorted(index[id(p)] for p in g.params):
+                raise ValueError(f"param group {gi} holds different parameters than the engine's group {gi}")
+            inner.param_groups[gi].update({k: v for k, v in sg.items() if k != "params"})
+            first = sd["state"].get(index[id(g.params[0])], {})
+            st = inner.state[fp]
+            for key in self._OPT_KEYS:
+                if not isinstance(first.get(key), torch.Tensor):
+                    continue
+                n_out = fp.numel()
+                out = torch.zeros(n_out, dtype=torch.float32)
+                for b in g.buckets:
+                    if self.zero:
+                        c = (b.end - b.start) // W
+                        lo, hi, base = b.start + r * c, b.start + (r + 1) * c, b.shard_off
+                    else:
+                        lo, hi, base = b.start, b.end, b.start
+                    for p in b.params:
+                        o = self._flat_offset(g, p)
+                        a_, e_ = max(o, lo), min(o + p.numel(), hi)
+                        if a_ < e_:
+                            src = sd["state"][index[id(p)]][key].reshape(-1)
+                            out[base + a_ - lo:base + e_ - lo].copy_(src[a_ - o:e_ - o].float())
+                st[key] = inner._state_tensor(out, fp)
+            if "step" in first:
+                st["step"] = torch.as_tensor(first["step"]).detach().to("cpu", torch.float32).clone().reshape(())
+
+    @staticmethod
+    def _flat_offset(g, p) -> int:
+        off = getattr(g, "_offset_of", None)
+        if off is None:
+            off = g._offset_of = {id(q): o for q, o in zip(g.params, g.offsets)}
+        return off[id(p)]
+
+    def close(self):
+        """Collective (every rank): release this engine's IPC bucket communicator — its staging
+        buffers and peer mappings — once no further step will run on the engine."""
+        if self._ipc is not None:
+            from .ipc import release_communicator
+            if self._ipc_stream is not None:
+                torch.cuda.current_stream(self._ipc_stream.device).wait_stream(self._ipc_stream)
+            release_communicator(self.pg, self._ipc_tag)
+            self._ipc = None
+            self._ipc_limit = 0

@@ -23,10 +23,19 @@ Usage::
 Constraints: ranks of one node only (IPC), world <= 8, calls issued in the same order on every
 rank and ordered on the device (the current stream), message <= ``max_bytes`` and a multiple of
 16 bytes (``all_reduce`` pads through a scratch tensor when it is not).
+
+Failure is fail-stop (the reference's NCCL collectives abort the job on a dead peer,
+ray-jobs/pytorch_llm_ray.py:362-364): a wait that exceeds ``timeout_s`` (default: the
+NCCL process-group timeout, ``GRT_IPC_TIMEOUT_S``) marks the communicator failed on EVERY rank
+(abort word), every output of a failed call is NaN (so a grad norm / gradient consumed before the
+host notices is non-finite, never a plausible wrong sum), later calls return NaN immediately without
+waiting, and :func:`check_all` — called at every ``train.report``, SFT log / save and at the end of
+the bench's timed region — raises on the host.
 """
 from __future__ import annotations
 
 import os
+import weakref
 from typing import List, Optional
 
 import torch
@@ -35,11 +44,31 @@ import torch.distributed as dist
 from .. import _native
 
 REALTIME_HZ = 100_000_000  # s_memrealtime tick rate
+ERR_ABORTED = 1 << 30       # kIpcErrAborted (grt_kernels.h)
+ERR_SKIPPED = 1 << 31       # kIpcErrSkipped
+
+
+def default_timeout_s() -> float:
+    """``GRT_IPC_TIMEOUT_S``, else the NCCL process-group default (10 min): a peer that is slow for
+    a legitimate reason (rank 0 writing a checkpoint) must not fail the job sooner than RCCL would."""
+    env = os.environ.get("GRT_IPC_TIMEOUT_S")
+    if env:
+        return float(env)
+    try:
+        from torch.distributed.constants import default_pg_nccl_timeout
+        if default_pg_nccl_timeout is not None:
+            return float(default_pg_nccl_timeout.total_seconds())
+    except ImportError:
+        pass
+    return 600.0
+
+
+_live: "weakref.WeakSet[IpcCommunicator]" = weakref.WeakSet()
 
 
 class IpcCommunicator:
     def __init__(self, group=None, max_bytes: int = 8 << 20, device: Optional[torch.device] = None,
-                 timeout_s: float = 30.0, two_shot_bytes: Optional[int] = None):
+                 timeout_s: Optional[float] = None, two_shot_bytes: Optional[int] = None):
         if not (dist.is_available() and dist.is_initialized()):
             raise RuntimeError("IpcCommunicator needs an initialised process group")
         self.group = group
@@ -55,7 +84,8 @@ class IpcCommunicator:
         # two-shot pays once each GPU would otherwise read (W-1) x the message over the fabric
         self.two_shot_bytes = int(two_shot_bytes) if two_shot_bytes is not None else (
             512 << 10 if self.world > 2 else 1 << 62)
-        self.timeout_ticks = int(timeout_s * REALTIME_HZ)
+        self.timeout_s = float(default_timeout_s() if timeout_s is None else timeout_s)
+        self.timeout_ticks = int(self.timeout_s * REALTIME_HZ)
         self._C = C
         self.epoch = 0
         # own buffers: staging + result (2 parities each) in HBM, signals in fine-grained memory
@@ -100,14 +130,16 @@ class IpcCommunicator:
             self._release()
             raise RuntimeError(f"IPC communicator setup failed on rank(s) of the group"
                                f"{'' if failure is None else f' (here: {failure})'}")
+        _live.add(self)
 
     # ------------------------------------------------------------------ collectives
     def _next_epoch(self) -> int:
         self.epoch += 1
         return self.epoch & 0xFFFFFFFF
 
-    def all_reduce(self, t: torch.Tensor, average: bool = False) -> torch.Tensor:
-        """In-place SUM (or mean) of ``t`` over the group; fp32 / bf16 (fp32 accumulation)."""
+    def all_reduce(self, t: torch.Tensor, average: bool = False, two_shot: Optional[bool] = None) -> torch.Tensor:
+        """In-place SUM (or mean) of ``t`` over the group; fp32 / bf16 (fp32 accumulation).
+        ``two_shot`` forces the algorithm (self-test / tests); default: by size."""
         if t.dtype not in (torch.float32, torch.bfloat16):
             raise TypeError(f"ipc all_reduce supports fp32/bf16, got {t.dtype}")
         nbytes = t.numel() * t.element_size()
@@ -121,7 +153,8 @@ class IpcCommunicator:
             per16 = 16 // t.element_size()
             buf = torch.zeros((t.numel() + per16 - 1) // per16 * per16, dtype=t.dtype, device=t.device)
             buf[:t.numel()].copy_(t.reshape(-1))
-        two_shot = nbytes >= self.two_shot_bytes
+        if two_shot is None:
+            two_shot = nbytes >= self.two_shot_bytes
         self._C.ipc_allreduce(self.staging, self.result, self.signal, self.err, self.cap, self.rank,
                               self._next_epoch(), self.timeout_ticks, buf, buf, two_shot, scale)
         if not direct:
@@ -133,14 +166,32 @@ class IpcCommunicator:
         self._C.ipc_barrier(self.staging, self.result, self.signal, self.err, self.cap, self.rank,
                             self._next_epoch(), self.timeout_ticks)
 
+    @property
+    def failed(self) -> bool:
+        """Host flag set by :meth:`check` once the device error word was seen non-zero."""
+        return getattr(self, "_failed", False)
+
     def check(self):
-        """Synchronise and raise if any earlier call timed out waiting for a peer."""
-        e = int(self.err[0].item())
+        """Synchronise (the error word's device-to-host read) and raise if any earlier call failed:
+        a wait here timed out, a peer announced a timeout, or a call was skipped because of one."""
+        if self._C is None:
+            return
+        e = int(self.err[0].item()) & 0xFFFFFFFF
         if e:
-            peers = [i for i in range(32) if e >> i & 1]
-            raise RuntimeError(f"IPC collective timed out waiting for rank(s) {peers} (rank {self.rank})")
+            self._failed = True
+            peers = [i for i in range(8) if e >> i & 1]
+            what = []
+            if peers:
+                what.append(f"timed out waiting for rank(s) {peers}")
+            if e & ERR_ABORTED:
+                what.append("a peer rank aborted the communicator after its own timeout")
+            if e & ERR_SKIPPED:
+                what.append("later calls were skipped and returned NaN")
+            raise RuntimeError(f"IPC collective failed on rank {self.rank} (error word {e:#x}): "
+                               + "; ".join(what) + f" [timeout {self.timeout_s:g} s]")
 
     def _release(self):
+        _live.discard(self)
         for p in self._opened:
             self._C.ipc_close(p, self.dev_index)
         self._opened = []
@@ -157,16 +208,47 @@ class IpcCommunicator:
             dist.barrier(group=self.group)  # no peer kernel still reads our buffers
         self._release()
 
+    # (numel, dtype, two_shot): single and multi-block, one- and two-shot, both dtypes, up to the
+    # automatic routing limit; each case runs 3 times back to back (both staging parities, one reused)
+    SELF_TEST_CASES = ((4, torch.float32, False), (8 * 1024 + 4, torch.bfloat16, False),
+                       (40_000, torch.float32, False), (40_000, torch.float32, True),
+                       (300_000, torch.bfloat16, True), (524_288, torch.float32, True),
+                       (524_288, torch.float32, False))
+
     def self_test(self) -> bool:
-        """One 16-byte all-reduce with known inputs, checked on the host, agreed over the group:
-        True on every rank or False on every rank (the automatic path is then left unused)."""
-        x = torch.full((4,), float(self.rank + 1), dtype=torch.float32, device=self.device)
-        self.all_reduce(x)
-        torch.cuda.synchronize(self.device)
-        want = self.world * (self.world + 1) / 2
-        good = bool(torch.all(x == want).item()) and int(self.err[0].item()) == 0
-        ok = torch.tensor([1 if good else 0], dtype=torch.int32,
-                          device=self.device if dist.get_backend(self.group) == "nccl" else "cpu")
+        """Every SELF_TEST_CASES message is all-reduced 3 times over the IPC kernels and once over
+        the process group (RCCL / gloo) on the same integer-valued inputs (exact in fp32 and bf16,
+        so any reduction order gives the same bits) and compared element for element; the error
+        word must stay clean. The verdict is agreed over the group: True on every rank or False on
+        every rank (the automatic route is then left unused and RCCL carries everything)."""
+        good = True
+        self.self_test_error = None
+        dev_pg = self.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        try:
+            for i, (n, dt, two) in enumerate(self.SELF_TEST_CASES):
+                if n * torch.tensor([], dtype=dt).element_size() > self.cap:
+                    continue
+                g = torch.Generator().manual_seed(9173 + 31 * i + self.rank)
+                base = torch.randint(-8, 9, (n,), generator=g).to(dt)
+                ref = base.to(torch.float32, copy=True).to(dev_pg)  # fp32 on the wire (copy: never reduce base itself)
+                dist.all_reduce(ref, group=self.group)
+                ref = ref.to(self.device).to(dt)
+                for rep in range(3):
+                    x = base.to(self.device)
+                    self.all_reduce(x, two_shot=two)
+                    if not torch.equal(x, ref):
+                        good = False
+                        self.self_test_error = (f"case {i} ({n} x {dt}, two_shot={two}) call {rep}: "
+                                                f"{int((x != ref).sum())} elements differ from the process group's sum")
+            torch.cuda.synchronize(self.device)
+            e = int(self.err[0].item())
+            if e:
+                good = False
+                self.self_test_error = f"error word {e:#x}"
+        except Exception as ex:  # noqa: BLE001 -- a local failure must still reach the agreement below
+            good = False
+            self.self_test_error = repr(ex)
+        ok = torch.tensor([1 if good else 0], dtype=torch.int32, device=dev_pg)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
         return int(ok.item()) == 1
 
@@ -198,11 +280,60 @@ def routes(nbytes: int, dtype: torch.dtype, limit: int) -> bool:
 _comms: dict = {}
 
 
+def _group_key(group):
+    """Stable identity of a process group: its name (unique per creation in torch, never reused by
+    a later group the way ``id()`` of a destroyed one can be) plus its ranks."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return (None, ())
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    name = getattr(pg, "group_name", None)
+    try:
+        ranks = tuple(dist.get_process_group_ranks(pg))
+    except Exception:  # noqa: BLE001 -- older torch / fake groups
+        ranks = (dist.get_world_size(group),)
+    return (name if name is not None else id(pg), ranks)
+
+
+def check_all():
+    """Raise if any live communicator of this process has failed (one device-to-host read of each
+    error word: call it only where the host synchronises anyway — report, logging, checkpointing)."""
+    for c in list(_live):
+        c.check()
+
+
+def stage_errors() -> list:
+    """Asynchronous snapshot of every live communicator's error word (a non-blocking copy into
+    pinned host memory on the current stream); pair with :func:`raise_staged` once an event recorded
+    after it has completed — the check then costs no host-device synchronisation."""
+    out = []
+    for c in list(_live):
+        if c._C is None:
+            continue
+        h = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        h.copy_(c.err[:1], non_blocking=True)
+        out.append((c, h))
+    return out
+
+
+def raise_staged(staged: list):
+    for c, h in staged:
+        if int(h[0]) != 0:
+            c.check()
+
+
+def release_communicator(group=None, tag: str = "default"):
+    """Free the buffers / peer mappings of (group, tag) — collective (a barrier over the group)."""
+    key = (_group_key(group), tag)
+    comm = _comms.pop(key, None)
+    if comm is not None:
+        comm.close()
+
+
 def communicator(group=None, tag: str = "default", max_bytes: int = 8 << 20) -> Optional[IpcCommunicator]:
     """Communicator for (group, tag), created collectively on first use, or None when IPC is off,
     unavailable, or failed its set-up or self-test on any rank (then every rank uses RCCL). Each
     tag has its own buffers and epoch sequence, so a tag may be driven from its own stream."""
-    key = (id(group) if group is not None else None, tag)
+    key = (_group_key(group), tag)
     if key in _comms:
         return _comms[key]
     comm = None
@@ -212,6 +343,9 @@ def communicator(group=None, tag: str = "default", max_bytes: int = 8 << 20) -> 
         except RuntimeError:
             comm = None  # every rank raised the same way (agreed in __init__)
         if comm is not None and not comm.self_test():
+            import warnings
+            warnings.warn(f"IPC collectives disabled for tag {tag!r}: the self-test failed on some rank "
+                          f"(here: {comm.self_test_error or 'passed'}); RCCL carries every message")
             comm.close()
             comm = None
     _comms[key] = comm

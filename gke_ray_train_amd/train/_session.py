@@ -78,6 +78,10 @@ class _Session:
 
     def report(self, metrics: Dict[str, Any], checkpoint: Optional[Checkpoint] = None):
         _maybe_inject_fault(self.ctx.world_rank, self.index)
+        # a report is a synchronisation point of every rank: a failed xGMI IPC collective since the
+        # last one raises here (fail-stop, like an NCCL error) instead of being reported as a result
+        from ..parallel.ipc import check_all
+        check_all()
         staged = None
         if checkpoint is not None:
             # stage the files: the caller may delete its (temporary) directory right after report()

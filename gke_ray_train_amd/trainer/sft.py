@@ -613,6 +613,9 @@ class SFTTrainer:
                 mis = list(range(gi * accum, min(nb, (gi + 1) * accum)))
                 if not mis:
                     break
+                if step >= total:  # resumed at (or past) max_steps: nothing left to train
+                    done = True
+                    break
                 mi = mis[-1]
                 chunks = self._step_chunks(batches, mis, fuse)
                 if trace is not None:  # diagnosis only: synchronises every step
@@ -734,6 +737,9 @@ class SFTTrainer:
             host = vals
         meta = {"learning_rate": self.scheduler.get_last_lr()[0], "epoch": round(self.state["epoch"], 4),
                 "step": self.state["global_step"]}
+        if self.world > 1 and self.device.type == "cuda":  # IPC error words, read when the log is emitted
+            from ..parallel.ipc import stage_errors
+            meta["ipc_errs"] = stage_errors()
         self._pending_logs.append((self._now_marker(), host, meta, ntok, fpt))
 
     def _emit_logs(self, wait: bool = False):
@@ -745,6 +751,9 @@ class SFTTrainer:
                 elif not mark.query():
                     return
             self._pending_logs.pop(0)
+            if meta.get("ipc_errs"):  # a failed xGMI IPC collective fails the run here (fail-stop)
+                from ..parallel.ipc import raise_staged
+                raise_staged(meta["ipc_errs"])
             prev, ntok_prev = self._log_mark
             if isinstance(mark, float):
                 dt = max(mark - prev, 1e-9)
@@ -852,32 +861,45 @@ class SFTTrainer:
         tm = [time.time()]
         self._finish_save()
         self._settle()
+        if self.world > 1 and self.device.type == "cuda":  # a failed IPC collective fails the save
+            from ..parallel.ipc import check_all
+            check_all()
         tm.append(time.time())
         a = self.args
         d = os.path.join(a.output_dir, f"checkpoint-{step}")
         job = None
         err = None
         sharded_opt = bool(getattr(self.engine, "zero", False))
+        # optimizer.pt in HF's per-parameter layout at every world size and sharding: collective
+        # (ZeRO gathers each bucket's 1/world chunks to rank 0), so every rank calls it; the file
+        # then resumes at any world size (load_portable_optimizer_state_dict)
+        portable = hasattr(self.engine, "portable_optimizer_state_dict")
+        port_sd, port_err = None, None
+        if portable:
+            try:
+                port_sd = self.engine.portable_optimizer_state_dict(self.optimizer)
+            except Exception as e:  # noqa: BLE001 -- agreed below with the other ranks
+                port_err = e
         if self.rank == 0:
             try:
                 os.makedirs(d, exist_ok=True)
                 m = self._unwrapped()
                 is_adapter = hasattr(m, "adapter_state_dict") and hasattr(m, "lora_modules")
                 snap = self._snapshot if self.device.type == "cuda" and is_adapter else None
-                # ZeRO: rank 0 holds only its 1/world shard of the AdamW state, which must never sit
-                # under the HF full-state name optimizer.pt; every rank writes optimizer_rank<r>.pt
-                opt_sd = {} if sharded_opt else self.optimizer.state_dict()
+                if port_err is not None:
+                    raise port_err
+                opt_sd = port_sd if portable else self.optimizer.state_dict()
                 if snap is not None:  # ONE pinned snapshot of optimizer state (+ adapters)
                     host = snap.take({"o": opt_sd, "a": m.adapter_state_dict() if is_adapter else None})
                 else:
                     host = {"o": _to_host(opt_sd), "a": _to_host(m.adapter_state_dict()) if is_adapter else None}
                 tm.append(time.time())
-                files = {"scheduler.pt": self.scheduler.state_dict(), "training_args.bin": a.to_dict()}
-                if not sharded_opt:
-                    files["optimizer.pt"] = host["o"]
+                files = {"scheduler.pt": self.scheduler.state_dict(), "training_args.bin": a.to_dict(),
+                         "optimizer.pt": host["o"]}
                 st = dict(self.state, train_batch_size=a.per_device_train_batch_size, max_steps=a.max_steps,
                           logging_steps=a.logging_steps, save_steps=a.save_steps, eval_steps=a.eval_steps,
-                          grt_optimizer_layout={"zero": sharded_opt, "world": self.world})
+                          grt_optimizer_layout={"format": "per-parameter" if portable else "flat",
+                                                "zero": sharded_opt, "world": self.world})
                 st = json.loads(json.dumps(st))  # frozen copy: the live state keeps changing
                 adapter = None
                 if is_adapter:
@@ -903,10 +925,9 @@ class SFTTrainer:
         try:
             os.makedirs(d, exist_ok=True)
             torch.save(_rng_snapshot(), os.path.join(d, f"rng_state_{self.rank}.pth"))
-            if sharded_opt:  # ZeRO: each rank holds 1/world of the AdamW state
-                torch.save(_to_host(self.optimizer.state_dict()), os.path.join(d, f"optimizer_rank{self.rank}.pt"))
         except Exception as e:
             err = err or e
+        err = err or port_err
         # every rank reaches this exchange, so a failed snapshot raises everywhere (no hang)
         _rank_uniform_error(err, self.world, f"checkpoint {d}")
         # the async decision must be identical on every rank: _finish_save exchanges the outcome
@@ -970,7 +991,13 @@ class SFTTrainer:
             st = json.load(f)
         zero_now = bool(getattr(self.engine, "zero", False))
         layout = st.pop("grt_optimizer_layout", None)
-        if layout is not None:  # the optimizer layout must match: a shard is 1/world of the flat state
+        if layout is not None and layout.get("format") == "per-parameter":
+            # HF per-parameter layout: resumes at any world size / sharding
+            sd = torch.load(os.path.join(d, "optimizer.pt"), map_location="cpu", weights_only=True, mmap=True)
+            self.engine.load_portable_optimizer_state_dict(self.optimizer, sd)
+            del sd
+            return self._finish_load(d, st)
+        if layout is not None:  # legacy flat layout: must match (a shard is 1/world of the flat state)
             if bool(layout.get("zero")) != zero_now or (zero_now and int(layout.get("world", -1)) != self.world):
                 raise ValueError(
                     f"{d}: optimizer state was written {'ZeRO-sharded' if layout.get('zero') else 'unsharded'} "
@@ -985,6 +1012,9 @@ class SFTTrainer:
             raise FileNotFoundError(f"{d}: {os.path.basename(opt_f)} is missing (checkpoint written with a ZeRO-sharded "
                                     f"optimizer? its state is in optimizer_rank<r>.pt)")
         self.optimizer.load_state_dict(torch.load(opt_f, map_location=self.device, weights_only=True))
+        return self._finish_load(d, st)
+
+    def _finish_load(self, d: str, st: dict) -> int:
         self.scheduler.load_state_dict(torch.load(os.path.join(d, "scheduler.pt"), weights_only=True))
         self.state.update(st)
         rp = os.path.join(d, f"rng_state_{self.rank}.pth")

@@ -39,7 +39,7 @@ def _kernels(isa):
             out[cur] = []
             continue
         if cur is not None:
-            if "s_endpgm" in line:
+            if line.startswith(".Lfunc_end"):  # a kernel can hold several s_endpgm (early returns)
                 cur = None
                 continue
             t = line.strip()

@@ -281,3 +281,107 @@ def test_ddp_small_bucket_over_ipc(zero):
                 exp = full[name][r * c:(r + 1) * c]
                 got = torch.from_numpy(shard[:c])
                 assert torch.allclose(got, exp, atol=1e-5, rtol=1e-4), (name, r, (got - exp).abs().max())
+
+
+# ----------------------------------------------------------------------------- fail-stop
+def _late_peer_worker(rank, world, port, q):
+    """Rank 2 reaches the collective 6 s late against a 2 s IPC timeout. Every rank must end with a
+    NaN (never a plausible) result and raise at its next check; later calls fail at once."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GRT_IPC_ALLOW_GLOO="1",
+                      GRT_IPC_COLLECTIVES="auto", LOCAL_WORLD_SIZE=str(world), GRT_IPC_TIMEOUT_S="2")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {}
+    try:
+        import torch.nn as nn
+        from gke_ray_train_amd.parallel import ipc
+        from gke_ray_train_amd.parallel.ddp import DistributedDataParallel
+
+        class Net(nn.Module):
+            def __init__(self):
+                super().__init__()
+                self.fc1 = nn.Linear(256, 256, bias=False)
+                self.norm = nn.Module()
+                self.norm.weight = nn.Parameter(torch.ones(256))
+
+            def forward(self, x):
+                return (self.fc1(x) * self.norm.weight).square().mean()
+
+        torch.manual_seed(0)
+        net = Net().cuda()
+        ddp = DistributedDataParallel(net, broadcast_params=True)
+        assert ddp._ipc is not None and ddp._ipc.timeout_s == 2.0
+        # (1) a healthy step first: the IPC route works and check_all passes
+        x = torch.randn(8, 256, device="cuda")
+        dist.barrier()
+        ddp(x).backward()
+        ddp.finish_gradient_sync()
+        torch.cuda.synchronize()
+        ipc.check_all()
+        out["healthy_finite"] = bool(torch.isfinite(net.norm.weight.grad).all())
+        ddp.zero_grad()
+        # (2) rank 2 is late: the IPC-routed bucket (norm weight) of every rank comes out NaN
+        if rank == 2:
+            time.sleep(6.0)
+        ddp(x).backward()
+        ddp.finish_gradient_sync()
+        torch.cuda.synchronize()
+        out["late_nan"] = bool(torch.isnan(net.norm.weight.grad).all())
+        try:
+            ipc.check_all()
+            out["raised"] = None
+        except RuntimeError as e:
+            out["raised"] = str(e)
+        # (3) the communicator stays failed: the next call returns NaN without waiting
+        t0 = time.time()
+        y = torch.ones(64, device="cuda")
+        ddp._ipc.all_reduce(y)
+        torch.cuda.synchronize()
+        out["after_s"] = time.time() - t0
+        out["after_nan"] = bool(torch.isnan(y).all())
+        q.put((rank, out))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_late_peer_fails_every_rank_loudly():
+    res = _spawn(_late_peer_worker, 3, timeout=240)
+    for r in range(3):
+        o = res[r]
+        assert o["healthy_finite"], r
+        assert o["late_nan"], f"rank {r} consumed a non-NaN result of a timed-out all-reduce"
+        assert o["raised"] and "IPC collective failed" in o["raised"], (r, o["raised"])
+        assert o["after_nan"] and o["after_s"] < 1.5, (r, o["after_s"])
+    # the first rank to time out names the late rank and aborts the communicator for the others
+    # (whose waits then end early); the late rank learns of the abort on arrival
+    assert any("rank(s) [2]" in res[r]["raised"] for r in (0, 1)), [res[r]["raised"] for r in range(3)]
+    assert "aborted" in res[2]["raised"]
+
+
+def _self_test_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gke_ray_train_amd.parallel.ipc import IpcCommunicator
+        c = IpcCommunicator(max_bytes=8 << 20, timeout_s=20.0)
+        ok = c.self_test()
+        c.close()
+        q.put((rank, {"ok": ok}))
+    except Exception as e:
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_self_test_against_process_group(world):
+    """The set-up self-test (one- and two-shot, multi-block, 3 back-to-back calls per case, both
+    dtypes, exact integer data against the process group's own all-reduce) passes on a healthy node."""
+    res = _spawn(_self_test_worker, world)
+    assert all(res[r]["ok"] for r in range(world))
