@@ -137,11 +137,14 @@ def _plain_bf16_linear(lin) -> bool:
             and w.data_ptr() % 16 == 0)
 
 
+GEMV_FUSED_MAX_ROWS = 4  # gemv_fused's row limit (TORCH_CHECK in csrc/bindings/ops.cpp)
+
+
 def _norm_fusable(model, B: int) -> bool:
     """Every projection a plain bf16 Linear (no LoRA / NF4 wrappers, no bias) and 1-2 rows: the
     decode step can run with its residual adds / RMSNorms inside the GEMVs (gemv.hip)."""
     from ..ops import linear as _lin
-    if not (_GEMV_NORM and _lin._GEMV and B <= _lin.GEMV_MAX_ROWS and _native.kernels_available()):
+    if not (_GEMV_NORM and _lin._GEMV and B <= min(_lin.GEMV_MAX_ROWS, GEMV_FUSED_MAX_ROWS) and _native.kernels_available()):
         return False
     m = model.model
     norms = [m.norm] + [n for ly in m.layers for n in (ly.input_layernorm, ly.post_attention_layernorm)]

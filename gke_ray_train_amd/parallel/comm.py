@@ -44,17 +44,27 @@ def _prior(op: str, world: int) -> dict:
 
 
 def comm_model(op: str, world: int) -> dict:
-    """alpha (µs) / beta (GB/s of collective input) for ``op`` at ``world`` ranks: the calibration
-    file's entry for the nearest measured world size, else the prior."""
+    """alpha (µs) / beta (GB/s of collective input) for ``op`` at ``world`` ranks from the
+    calibration file — a single measurement (``{"world": W, op: {...}}``) or several
+    (``{"by_world": {"2": {...}, "8": {...}}}``). An entry measured at another world size is used
+    only after rescaling its algorithm bandwidth by the ring factor (bus bandwidth is what carries
+    over between world sizes); with no usable entry, the prior."""
     path = os.environ.get("GRT_COMM_CALIBRATION")
     if path and os.path.exists(path):
         import json
         with open(path) as f:
             cal = json.load(f)
-        ent = cal.get(op)
-        if ent and ent.get("beta_GBps", 0) > 0:
-            return {"alpha_us": float(ent["alpha_us"]), "beta_GBps": float(ent["beta_GBps"]),
-                    "source": path, "world": cal.get("world")}
+        tables = {int(k): v for k, v in cal.get("by_world", {}).items()}
+        if not tables and cal.get("world") is not None:
+            tables = {int(cal["world"]): cal}
+        usable = {w: t[op] for w, t in tables.items() if t.get(op, {}).get("beta_GBps", 0) > 0}
+        if usable:
+            w_cal = min(usable, key=lambda w: (abs(w - world), -w))
+            ent = usable[w_cal]
+            beta = float(ent["beta_GBps"])
+            if w_cal != world:  # algbw -> busbw at the measured size -> algbw at this size
+                beta *= _prior(op, world)["beta_GBps"] / _prior(op, w_cal)["beta_GBps"]
+            return {"alpha_us": float(ent["alpha_us"]), "beta_GBps": beta, "source": path, "world": w_cal}
     return _prior(op, world)
 
 

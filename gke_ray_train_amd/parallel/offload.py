@@ -282,6 +282,10 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
     def load_state_dict(self, sd):
         self.synchronize()
         super().load_state_dict(sd)
+        # slots uploaded ahead (prefetch()) hold the moments from before the load: drop them so the
+        # next step uploads the loaded ones (and nothing stale is written back over them)
+        self._landed.clear()
+        self._pending_down = []
         self._dev_m.clear()
         self._dev_v.clear()
         for st in self.state.values():

@@ -140,7 +140,19 @@ def test_bucket_plan_cost_model_and_calibration_file(tmp_path, monkeypatch):
     cal = json.loads(out.read_text())
     assert cal["world"] == 2 and cal["all_reduce"]["beta_GBps"] > 0 and cal["all_reduce"]["alpha_us"] >= 0
     monkeypatch.setenv("GRT_COMM_CALIBRATION", str(out))
-    m2 = comm_model("all_reduce", 8)
-    assert m2["source"] == str(out) and m2["beta_GBps"] == cal["all_reduce"]["beta_GBps"]
+    m2 = comm_model("all_reduce", 2)  # measured world: used as measured
+    assert m2["source"] == str(out) and m2["beta_GBps"] == cal["all_reduce"]["beta_GBps"] and m2["world"] == 2
+    # another world size: the measured bus bandwidth carries over, rescaled to algorithm bandwidth
+    m8 = comm_model("all_reduce", 8)
+    ring = (8 / (2 * 7)) / (2 / (2 * 1))
+    assert m8["world"] == 2 and abs(m8["beta_GBps"] - cal["all_reduce"]["beta_GBps"] * ring) < 1e-9
+    # a file holding several world sizes: the nearest one wins (per-world entries)
+    cal8 = dict(cal["by_world"]["2"], world=8, all_reduce=dict(cal["all_reduce"], beta_GBps=123.0))
+    multi = tmp_path / "multi.json"
+    multi.write_text(json.dumps({"by_world": {"2": cal["by_world"]["2"], "8": cal8}}))
+    monkeypatch.setenv("GRT_COMM_CALIBRATION", str(multi))
+    assert comm_model("all_reduce", 8)["beta_GBps"] == 123.0 and comm_model("all_reduce", 7)["world"] == 8
+    assert comm_model("all_reduce", 2)["beta_GBps"] == cal["all_reduce"]["beta_GBps"]
+    monkeypatch.setenv("GRT_COMM_CALIBRATION", str(out))
     b2 = plan_bucket_bytes(G, 8)
     assert 16 * 2 ** 20 <= b2 <= 2 ** 30

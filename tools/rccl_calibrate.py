@@ -105,9 +105,18 @@ def main(argv=None):
         res[op] = {"alpha_us": round(alpha * 1e6, 2), "beta_GBps": round(1.0 / inv_beta / 1e9, 2),
                    "busbw_GBps_at_max": round(nbytes[-1] / meds[-1] * scale / 1e9, 2),
                    "median_s": [round(t, 7) for t in meds]}
-    if R == 0:
+    if R == 0:  # one entry per world size (by_world); runs at other world sizes are kept
+        import os
+        out = {}
+        if os.path.exists(a.out):
+            with open(a.out) as f:
+                out = json.load(f)
+            if "by_world" not in out and out.get("world") is not None:
+                out = {"by_world": {str(out["world"]): out}}
+        out.setdefault("by_world", {})[str(W)] = res
+        out.update({k: v for k, v in res.items()})  # the latest run also at top level (older readers)
         with open(a.out, "w") as f:
-            json.dump(res, f, indent=1)
+            json.dump(out, f, indent=1)
         print(json.dumps({k: v for k, v in res.items() if k in ("world", "all_reduce", "reduce_scatter")}), flush=True)
     dist.destroy_process_group()
 
