@@ -163,6 +163,13 @@ def _baseline_metric() -> str:
         return "tokens/sec (whole node) Llama-2-7B fine-tune at 1/2/4/8 MI355X; samples/sec on Wikitext-2"
 
 
+def _link_plan(plan, a, step_s):
+    if a.parallel != "fsdp":
+        return None
+    from gke_ray_train_amd.parallel.offload import host_link_plan
+    return host_link_plan(plan, a.resident_fraction, step_s)
+
+
 def _bench_worker(cfg: dict):
     """TorchTrainer ``train_loop_per_worker``: the process group is already up (TrainWorker)."""
     run(argparse.Namespace(**cfg))
@@ -282,7 +289,7 @@ def run(a):
     a.resident_fraction = 0.0
     a.prefetch_slots = 0
     if a.offload and a.parallel == "fsdp":
-        from gke_ray_train_amd.parallel.offload import (PREFETCH_CAP_BYTES, prefetch_slots_for,
+        from gke_ray_train_amd.parallel.offload import (PREFETCH_CAP_BYTES, hbm_reserve_bytes, prefetch_slots_for,
                                                         resident_fraction_from_plan)
         if a.offload_resident == "auto":
             a.resident_fraction = resident_fraction_from_plan(plan, None)
@@ -290,7 +297,7 @@ def run(a):
             a.resident_fraction = float(a.offload_resident)
         moved = plan.host_per_rank.get("adam_moments_fp32", 0.0)
         streamed = (1.0 - a.resident_fraction) * moved
-        room = max(0.0, plan.hbm_capacity - plan.hbm_total - a.resident_fraction * moved - 8 * GiB)
+        room = max(0.0, plan.hbm_capacity - plan.hbm_total - a.resident_fraction * moved - hbm_reserve_bytes())
         budget = (min(streamed, PREFETCH_CAP_BYTES, room) if a.offload_prefetch_gib == "auto"
                   else float(a.offload_prefetch_gib) * GiB)
         a.prefetch_slots = prefetch_slots_for(budget, 1 << 26)
@@ -478,6 +485,8 @@ def run(a):
             "offload_units": len(getattr(opt, "segments", [])) if a.offload else None,
             "offload_prefetch_slots": getattr(opt, "prefetch_slots", None) if a.offload else None,
             "offload_resident_fraction": round(a.resident_fraction, 3) if a.offload else None,
+            # streamed moment bytes per step against the host link over the MEASURED step time
+            "offload_link": _link_plan(plan, a, elapsed / a.steps) if a.offload else None,
             "mfu_bf16_dense": round(mfu, 4),
             "hbm_plan_gib": round(plan.hbm_total / GiB, 1),
             "hbm_peak_gib": round(torch.cuda.max_memory_allocated(dev) / GiB, 1) if not cpu else None,

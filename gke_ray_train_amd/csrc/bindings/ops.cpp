@@ -953,6 +953,26 @@ void transpose_into(const Tensor& src, Tensor& dst) {
   grt::transpose_bf16(src.data_ptr(), dst.data_ptr(), (int)R, (int)Cc, cur_stream(src));
 }
 
+// dst <- src (same byte count, contiguous) on the GPU tensor's current stream by a DMA (SDMA)
+// engine, never by a blit kernel on the compute units: hipMemcpyDeviceToDeviceNoCU with the pointers
+// as they are (a pinned host tensor is addressed through its device mapping). The offloaded
+// optimizer's device -> host moment write-backs otherwise run as ROCclr __amd_rocclr_copyBuffer
+// kernels beside the step's compute (profiles/r5_offload70.md).
+void copy_sdma(Tensor& dst, const Tensor& src) {
+  TORCH_CHECK(dst.is_contiguous() && src.is_contiguous(), "copy_sdma: contiguous tensors");
+  const int64_t n = dst.numel() * dst.element_size();
+  TORCH_CHECK(n == src.numel() * src.element_size(), "copy_sdma: byte counts differ");
+  TORCH_CHECK(dst.is_cuda() || src.is_cuda(), "copy_sdma: one side must be a GPU tensor");
+  TORCH_CHECK((dst.is_cuda() || dst.is_pinned()) && (src.is_cuda() || src.is_pinned()),
+              "copy_sdma: host tensors must be pinned");
+  if (n == 0) return;
+  const Tensor& g = dst.is_cuda() ? dst : src;
+  c10::OptionalDeviceGuard guard(g.device());
+  const hipError_t e = hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), (size_t)n, hipMemcpyDeviceToDeviceNoCU,
+                                      cur_stream(g));
+  TORCH_CHECK(e == hipSuccess, "copy_sdma: hipMemcpyAsync: ", hipGetErrorString(e));
+}
+
 // y = x W^T for 1-4 rows (1-16 rows when K % 256 == 0: 3+ rows run on MFMA); swiglu: x = [gate | up]
 // [M, 2K] -> y = (silu(gate) * up) W^T
 Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
@@ -1347,6 +1367,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_fwd_t", &swiglu_fwd_t);
   m.def("swiglu_bwd_t", &swiglu_bwd_t);
   m.def("transpose_into", &transpose_into);
+  m.def("copy_sdma", &copy_sdma);
   m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("gemv_fused", &gemv_fused, py::arg("x"), py::arg("w"), py::arg("sumsq"), py::arg("slot"),
         py::arg("swiglu") = false, py::arg("g") = py::none(), py::arg("res") = py::none(), py::arg("eps") = 1e-5,

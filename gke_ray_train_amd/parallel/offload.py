@@ -301,11 +301,41 @@ def prefetch_slots_for(budget_bytes: float, chunk_elems: int) -> int:
     return max(0, int(budget_bytes // (8.0 * chunk_elems)))
 
 
-def resident_fraction_from_plan(plan_offload, plan_resident, margin_bytes: float = 8 * (1 << 30)) -> float:
+def hbm_reserve_bytes() -> float:
+    """HBM kept free by the automatic offload plan (``GRT_OFFLOAD_HBM_RESERVE_GIB``, default 8):
+    raise it to make ``auto`` stream moments and leave the room to activations / a bigger batch."""
+    return float(os.environ.get("GRT_OFFLOAD_HBM_RESERVE_GIB", "8")) * (1 << 30)
+
+
+def resident_fraction_from_plan(plan_offload, plan_resident=None, margin_bytes: Optional[float] = None) -> float:
     """Share of the offloaded moments that fits in HBM: capacity minus the offload plan's total
-    (which already holds the staging chunks) minus a margin, over the moments the offload moved."""
+    (which already holds the staging chunks) minus the reserve, over the moments the offload moved.
+    Every moment byte kept in HBM is one the host link does not carry twice per step, so the plan
+    keeps as many resident as the reserve allows; :func:`host_link_plan` says whether what is left
+    to stream fits under the step."""
     moved = plan_offload.host_per_rank.get("adam_moments_fp32", 0.0)
     if moved <= 0:
         return 1.0
-    room = plan_offload.hbm_capacity - plan_offload.hbm_total - margin_bytes
+    margin = hbm_reserve_bytes() if margin_bytes is None else float(margin_bytes)
+    room = plan_offload.hbm_capacity - plan_offload.hbm_total - margin
     return max(0.0, min(1.0, room / moved))
+
+
+# Host link of one MI355X (PCIe Gen5 x16), per direction, measured by tools/hostlink_bench.py:
+# SDMA uploads 57 GB/s; the device -> host write-backs run as ROCclr blit kernels at 30-57 GB/s
+# depending on the box (profiles/r5_offload70.md, profiles/r6_offload_link.md).
+HOST_LINK_GBPS = 57.0
+
+
+def host_link_plan(plan_offload, resident_fraction: float, step_s: float, link_GBps: Optional[float] = None) -> dict:
+    """Bytes the streamed share moves per step (each direction) against what the link carries in
+    ``step_s``: ``bound`` means the step will run at the link's pace, not the compute's."""
+    link = float(os.environ.get("GRT_HOST_LINK_GBPS", HOST_LINK_GBPS) if link_GBps is None else link_GBps)
+    moved = plan_offload.host_per_rank.get("adam_moments_fp32", 0.0)
+    streamed = max(0.0, 1.0 - float(resident_fraction)) * moved
+    link_s = streamed / (link * 1e9) if link > 0 else float("inf")
+    return {"streamed_gib_per_direction": round(streamed / (1 << 30), 2), "link_s": round(link_s, 3),
+            "step_s": round(step_s, 3), "link_bound": link_s > step_s,
+            # the resident share at which the streamed bytes just fit under the step
+            "resident_fraction_for_link": round(max(0.0, min(1.0, 1.0 - link * 1e9 * step_s / moved)), 3)
+            if moved > 0 else 1.0}

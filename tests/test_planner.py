@@ -156,3 +156,28 @@ def test_bucket_plan_cost_model_and_calibration_file(tmp_path, monkeypatch):
     monkeypatch.setenv("GRT_COMM_CALIBRATION", str(out))
     b2 = plan_bucket_bytes(G, 8)
     assert 16 * 2 ** 20 <= b2 <= 2 ** 30
+
+
+def test_offload_resident_share_reserve_and_host_link(monkeypatch):
+    """auto keeps every moment byte HBM can hold beside the configurable reserve; the link plan
+    says whether the streamed rest fits under a step (config #5, Llama-3-70B at 8 ranks)."""
+    from gke_ray_train_amd.parallel.offload import host_link_plan, resident_fraction_from_plan
+    cfg = get_config("llama3-70b")
+    plan = plan_memory(cfg, 8, "fsdp", offload=True, micro_batch=8, seq=1024, checkpointing=True,
+                       hbm_capacity=HBM, host_capacity=2000 * GiB)
+    moved = plan.host_per_rank["adam_moments_fp32"]
+    monkeypatch.delenv("GRT_OFFLOAD_HBM_RESERVE_GIB", raising=False)
+    assert resident_fraction_from_plan(plan) == 1.0  # 288 GB holds all of rank 0's moments
+    free = plan.hbm_capacity - plan.hbm_total
+    # a reserve that leaves room for only half of the moments -> auto streams the other half
+    monkeypatch.setenv("GRT_OFFLOAD_HBM_RESERVE_GIB", str((free - 0.5 * moved) / GiB))
+    f = resident_fraction_from_plan(plan)
+    assert abs(f - 0.5) < 1e-6
+    lp = host_link_plan(plan, f, step_s=3.5, link_GBps=57.0)
+    assert abs(lp["streamed_gib_per_direction"] - 0.5 * moved / GiB) < 0.01
+    assert lp["link_bound"] is False and lp["link_s"] < 3.5
+    slow = host_link_plan(plan, 0.0, step_s=1.0, link_GBps=57.0)  # everything streamed, short step
+    assert slow["link_bound"] is True and 0.0 < slow["resident_fraction_for_link"] < 1.0
+    # at that resident share the streamed bytes take exactly one step
+    edge = host_link_plan(plan, slow["resident_fraction_for_link"], step_s=1.0, link_GBps=57.0)
+    assert abs(edge["link_s"] - 1.0) < 0.01

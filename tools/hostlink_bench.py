@@ -4,7 +4,8 @@ chunks (torch ``copy_(non_blocking=True)`` on side streams, as parallel/offload.
 alone, both directions at once, and beside a GEMM loop on the compute stream (the GEMM's slowdown is
 what an overlapped copy costs the step). Under ``rocprofv3 --kernel-trace --memory-copy-trace`` the
 trace shows which engine each direction uses (SDMA copies vs ``__amd_rocclr_copyBuffer`` blit
-kernels on the CUs).
+kernels on the CUs). The ``*_sdma`` rows issue the same copies through the extension's
+``copy_sdma`` (hipMemcpyDeviceToDeviceNoCU: a DMA engine, never a kernel).
 
     python tools/hostlink_bench.py [--mib 512] [--reps 4]
 """
@@ -47,6 +48,25 @@ def main():
             for _ in range(a.reps):
                 h_dst.copy_(d_b, non_blocking=True)
 
+    C = None
+    try:
+        import os, sys
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from gke_ray_train_amd import _native
+        C = _native.kernels()
+    except Exception as e:  # noqa: BLE001
+        out["copy_sdma"] = f"unavailable: {e}"
+
+    def d2h_sdma():
+        with torch.cuda.stream(down):
+            for _ in range(a.reps):
+                C.copy_sdma(h_dst, d_b)
+
+    def h2d_sdma():
+        with torch.cuda.stream(up):
+            for _ in range(a.reps):
+                C.copy_sdma(d_a, h_src)
+
     h2d(), d2h()  # warm
     t = timed(h2d)
     out["h2d_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
@@ -54,6 +74,25 @@ def main():
     out["d2h_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
     t = timed(lambda: (h2d(), d2h()))
     out["duplex_total_GBps"] = round(2 * a.reps * nbytes / t / 1e9, 1)
+
+    if C is not None:
+        d_b.copy_(torch.arange(n, dtype=torch.float32, device=dev))
+        h_dst.zero_()
+        d2h_sdma()
+        torch.cuda.synchronize()
+        out["d2h_sdma_exact"] = bool(torch.equal(h_dst, d_b.cpu()))
+        h_src.copy_(torch.arange(n, dtype=torch.float32) * 3)
+        d_a.zero_()
+        h2d_sdma()
+        torch.cuda.synchronize()
+        out["h2d_sdma_exact"] = bool(torch.equal(d_a.cpu(), h_src))
+        d2h_sdma(), h2d_sdma()
+        t = timed(d2h_sdma)
+        out["d2h_sdma_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
+        t = timed(h2d_sdma)
+        out["h2d_sdma_GBps"] = round(a.reps * nbytes / t / 1e9, 1)
+        t = timed(lambda: (h2d_sdma(), d2h_sdma()))
+        out["duplex_sdma_total_GBps"] = round(2 * a.reps * nbytes / t / 1e9, 1)
 
     x = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
     y = torch.randn(8192, 8192, device=dev, dtype=torch.bfloat16)
@@ -66,7 +105,10 @@ def main():
     gemms(5)
     tg = timed(gemms)
     out["gemm_alone_ms"] = round(tg * 1e3, 1)
-    for name, fn in (("h2d", h2d), ("d2h", d2h), ("both", lambda: (h2d(), d2h()))):
+    modes = [("h2d", h2d), ("d2h", d2h), ("both", lambda: (h2d(), d2h()))]
+    if C is not None:
+        modes += [("d2h_sdma", d2h_sdma), ("both_sdma", lambda: (h2d(), d2h_sdma()))]
+    for name, fn in modes:
         def run():
             fn()
             gemms()
