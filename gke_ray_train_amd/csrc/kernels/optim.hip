@@ -73,17 +73,46 @@ __device__ __forceinline__ bf16 sr_bf16(float x, uint32_t r16) {
 
 // One AdamW element update with its fused multiply-adds spelled out, so every kernel variant (8- /
 // 4-wide, scalar tail, transposing) rounds identically whatever the compiler would contract.
+// FAST (default; GRT_ADAMW_FASTMATH=0 -> the IEEE forms): v_sqrt_f32 and v_rcp_f32 (1 ulp each)
+// instead of the correctly rounded sqrtf / division, whose expansions (denormal scaling, div_scale /
+// div_fmas / div_fixup) made up over a third of the kernel's ~57 VALU instructions per element. The
+// step is power-capped (1.39 kW on every sample of the headline step, profiles/r6_power.md), so the
+// update's instruction energy beside the forward costs step time even though the pass is HBM-bound.
+template <bool FAST>
 __device__ __forceinline__ float adam_elem(float p, float gf, float& m, float& v, float b1, float b2, float rbc2,
                                            float eps, float decay, float step) {
   m = fmaf(b1, m, (1.f - b1) * gf);
   v = fmaf(b2, v, (1.f - b2) * gf * gf);
-  const float denom = fmaf(sqrtf(v), rbc2, eps);
-  return fmaf(p, decay, -(step * m / denom));
+  if constexpr (FAST) {
+    const float denom = fmaf(__builtin_amdgcn_sqrtf(v), rbc2, eps);
+    return fmaf(-step * m, __builtin_amdgcn_rcpf(denom), p * decay);
+  } else {
+    const float denom = fmaf(sqrtf(v), rbc2, eps);
+    return fmaf(p, decay, -(step * m / denom));
+  }
+}
+
+// 16 random bits per element for stochastic rounding, 4 elements at a time (element base4 + k in
+// bits 16k .. 16k + 15), keyed by (step, flat element index): FAST = one 32-bit fmix per element
+// pair; otherwise one 64-bit splitmix per 4 elements.
+__device__ __forceinline__ uint32_t fmix32_o(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+template <bool FAST>
+__device__ __forceinline__ uint64_t sr_bits4(uint64_t srkey, uint64_t base4) {
+  if constexpr (FAST) {
+    const uint64_t pr = base4 >> 1;
+    const uint32_t k = (uint32_t)srkey ^ ((uint32_t)(pr >> 32) * 0x9E3779B1u);
+    return (uint64_t)fmix32_o(k ^ (uint32_t)pr) | ((uint64_t)fmix32_o(k ^ (uint32_t)(pr + 1)) << 32);
+  } else {
+    return hash_u64(srkey ^ (base4 >> 2));
+  }
 }
 
 // V elements per thread and iteration: 8 (16-byte loads of bf16 p / g, two float4 of m / v; needs
 // 16-byte aligned operands) or 4 (the fallback for 8-byte aligned bf16 slices).
-template <typename P, typename G, int V>
+template <typename P, typename G, int V, bool FAST>
 __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     float* __restrict__ master, int64_t n,
@@ -165,7 +194,7 @@ __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* 
       for (int k = 0; k < 4; ++k) {
         const int e = 4 * q + k;
         float mk = mv[q][k], vk = vv[q][k];
-        pf[e] = adam_elem(pf[e], gf[e], mk, vk, b1, b2, rbc2, eps, decay, step);
+        pf[e] = adam_elem<FAST>(pf[e], gf[e], mk, vk, b1, b2, rbc2, eps, decay, step);
         mv[q][k] = mk;
         vv[q][k] = vk;
       }
@@ -188,7 +217,7 @@ __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* 
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         if (sr) {
-          const uint64_t h = hash_u64(srkey ^ ((ioff + (uint64_t)(o + 4 * q)) >> 2));
+          const uint64_t h = sr_bits4<FAST>(srkey, (ioff + (uint64_t)(o + 4 * q)) & ~3ull);
 #pragma unroll
           for (int k = 0; k < 4; ++k) t[4 * q + k] = sr_bf16(pf[4 * q + k], (uint32_t)(h >> (16 * k)) & 0xffffu);
         } else {
@@ -222,12 +251,12 @@ __global__ __launch_bounds__(kNT) void adamw_kernel(P* __restrict__ p, const G* 
     float pf = master ? master[j] : to_f(p[j]);
     const float gf = to_f(g[j]) * gs;
     float mj = m[j], vj = v[j];
-    pf = adam_elem(pf, gf, mj, vj, b1, b2, rbc2, eps, decay, step);
+    pf = adam_elem<FAST>(pf, gf, mj, vj, b1, b2, rbc2, eps, decay, step);
     m[j] = mj;
     v[j] = vj;
     if (master) master[j] = pf;
     if constexpr (sizeof(P) == 2) {
-      p[j] = sr ? sr_bf16(pf, (uint32_t)(hash_u64(srkey ^ ((ioff + (uint64_t)j) >> 2)) >> (16 * ((ioff + j) & 3))) & 0xffffu)
+      p[j] = sr ? sr_bf16(pf, (uint32_t)(sr_bits4<FAST>(srkey, (ioff + (uint64_t)j) & ~3ull) >> (16 * ((ioff + j) & 3))) & 0xffffu)
                 : from_f<P>(pf);
     } else {
       p[j] = from_f<P>(pf);
@@ -248,6 +277,7 @@ __device__ __forceinline__ int ooff(int row, int ch) { return row * 256 + 16 * (
 
 // tile = 64 rows x 128 columns (cols % 128 == 0); the updated tile goes into the XOR-swizzled LDS
 // image of transpose.hip and is read back transposed with ds_read_b64_tr_b16.
+template <bool FAST>
 __global__ __launch_bounds__(kNT) void adamw_t_kernel(bf16* __restrict__ p, const bf16* __restrict__ g,
                                                       float* __restrict__ m, float* __restrict__ v,
                                                       bf16* __restrict__ pt, int64_t rows, int64_t cols,
@@ -291,13 +321,13 @@ __global__ __launch_bounds__(kNT) void adamw_t_kernel(bf16* __restrict__ p, cons
     bf16x8 out;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
-      const uint64_t hsh = hash_u64(srkey ^ ((ioff + (uint64_t)o + 4 * hh) >> 2));
+      const uint64_t hsh = sr_bits4<FAST>(srkey, (ioff + (uint64_t)o + 4 * hh) & ~3ull);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int e = 4 * hh + q;
         const float gf = to_f(gv[e]) * gs;
         float mq = mv[hh][q], vq = vv[hh][q];
-        const float pf = adam_elem(to_f(pv[e]), gf, mq, vq, b1, b2, rbc2, eps, decay, step);
+        const float pf = adam_elem<FAST>(to_f(pv[e]), gf, mq, vq, b1, b2, rbc2, eps, decay, step);
         mv[hh][q] = mq;
         vv[hh][q] = vq;
         out[e] = sr ? sr_bf16(pf, (uint32_t)(hsh >> (16 * q)) & 0xffffu) : from_f<bf16>(pf);
@@ -360,16 +390,31 @@ void clip_coef_finalize(const float* ws, int nparts, float max_norm, float presc
   hipLaunchKernelGGL(clip_finalize_kernel, dim3(1), dim3(kNT), 0, s, ws, nparts, max_norm, prescale, out);
 }
 
-template <typename P, typename G>
-void launch_adamw(dim3 grid, hipStream_t s, P* p, const G* g, float* m, float* v, float* master, int64_t n,
-                  const float* hyper, const float* gsp, uint64_t ioff) {
+// GRT_ADAMW_FASTMATH=0: the IEEE sqrt / division and the 64-bit stochastic-rounding hash (A/B switch)
+bool adamw_fastmath() {
+  static const bool f = [] { const char* e = std::getenv("GRT_ADAMW_FASTMATH"); return !(e && e[0] == '0'); }();
+  return f;
+}
+
+template <typename P, typename G, bool FAST>
+void launch_adamw_v(dim3 grid, hipStream_t s, P* p, const G* g, float* m, float* v, float* master, int64_t n,
+                    const float* hyper, const float* gsp, uint64_t ioff) {
   // GRT_ADAMW_V4=1: always the 4-wide variant (A/B switch)
   static const bool v4 = [] { const char* e = std::getenv("GRT_ADAMW_V4"); return e && e[0] == '1'; }();
   auto a16 = [](const void* q) { return q == nullptr || reinterpret_cast<uintptr_t>(q) % 16 == 0; };
   if (!v4 && a16(p) && a16(g) && a16(m) && a16(v) && a16(master))
-    hipLaunchKernelGGL((adamw_kernel<P, G, 8>), grid, dim3(kNT), 0, s, p, g, m, v, master, n, hyper, gsp, ioff);
+    hipLaunchKernelGGL((adamw_kernel<P, G, 8, FAST>), grid, dim3(kNT), 0, s, p, g, m, v, master, n, hyper, gsp, ioff);
   else
-    hipLaunchKernelGGL((adamw_kernel<P, G, 4>), grid, dim3(kNT), 0, s, p, g, m, v, master, n, hyper, gsp, ioff);
+    hipLaunchKernelGGL((adamw_kernel<P, G, 4, FAST>), grid, dim3(kNT), 0, s, p, g, m, v, master, n, hyper, gsp, ioff);
+}
+
+template <typename P, typename G>
+void launch_adamw(dim3 grid, hipStream_t s, P* p, const G* g, float* m, float* v, float* master, int64_t n,
+                  const float* hyper, const float* gsp, uint64_t ioff) {
+  if (adamw_fastmath())
+    launch_adamw_v<P, G, true>(grid, s, p, g, m, v, master, n, hyper, gsp, ioff);
+  else
+    launch_adamw_v<P, G, false>(grid, s, p, g, m, v, master, n, hyper, gsp, ioff);
 }
 
 void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v, float* master,
@@ -402,8 +447,12 @@ void adamw_step(DType pdt, DType gdt, void* p, const void* g, float* m, float* v
 void adamw_t_step(void* p, const void* g, float* m, float* v, void* pt, int64_t rows, int64_t cols,
                   const float* hyper, const float* gsp, hipStream_t s, int64_t ioff) {
   const dim3 grid((unsigned)((rows / 64) * (cols / 128)));
-  hipLaunchKernelGGL(adamw_t_kernel, grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, (bf16*)pt, rows,
-                     cols, hyper, gsp, (uint64_t)ioff);
+  if (adamw_fastmath())
+    hipLaunchKernelGGL(adamw_t_kernel<true>, grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, (bf16*)pt, rows,
+                       cols, hyper, gsp, (uint64_t)ioff);
+  else
+    hipLaunchKernelGGL(adamw_t_kernel<false>, grid, dim3(kNT), 0, s, (bf16*)p, (const bf16*)g, m, v, (bf16*)pt, rows,
+                       cols, hyper, gsp, (uint64_t)ioff);
 }
 
 void scale_inplace(DType dt, void* x, int64_t n, float a, const float* a_ptr, hipStream_t s) {
