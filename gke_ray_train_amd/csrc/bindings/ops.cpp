@@ -1339,6 +1339,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("sumsq_blocks", &sumsq_blocks);
+  m.def("lds_fill", [](int64_t pattern, int64_t device) {
+    c10::OptionalDeviceGuard g(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
+    grt::lds_fill((uint32_t)pattern, c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream());
+  }, "test support: fill every CU's LDS with a 32-bit pattern (stale-LDS-read detection)");
   m.def("sumsq", &sumsq);
   m.def("clip_finalize", &clip_finalize);
   m.def("adamw", &adamw, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("master"),

@@ -380,4 +380,7 @@ void ipc_get_handle(void* p, char out[kIpcHandleBytes]);
 void* ipc_open_handle(const char in[kIpcHandleBytes]);
 void ipc_close_handle(void* p);
 
+// test support (debug_lds.hip): every CU's LDS filled with `pattern` on stream s
+void lds_fill(uint32_t pattern, hipStream_t s);
+
 }  // namespace grt

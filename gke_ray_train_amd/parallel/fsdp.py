@@ -48,6 +48,9 @@ DEFAULT_UNITS = ("LlamaDecoderLayer", "EncoderLayer")
 _ALIGN = 64
 
 
+# GRT_FSDP_ZERO_FULL_GRAD=1: memset each unit's whole gradient buffer (A/B switch for the gap-only clear)
+_ZERO_FULL_GRAD = os.environ.get("GRT_FSDP_ZERO_FULL_GRAD", "0") == "1"
+
 class _BwdGather(torch.autograd.Function):
     """Identity on a unit's output; its backward fires right before the unit's backward kernels."""
 
@@ -412,7 +415,24 @@ class FullyShardedDataParallel(nn.Module):
     def _alloc_grads(self, u: _Unit):
         if u.grad_full is not None:
             return
-        g = self._acquire(u.total, zero=True)  # alignment gaps must not inject garbage into the reduction
+        # every parameter's slot is written whole by its first gradient of the step (GEMM beta = 0,
+        # copy, or the zero fill of finish_gradient_sync for unused ones), so only the alignment gaps
+        # between slots and the tail must be cleared (they must not inject garbage into the
+        # reduction): a few small ranges instead of a memset of the whole unit (37 x 55 us per
+        # Llama-2-7B step, profiles/r6_proxy8_steps.md)
+        g = self._acquire(u.total, zero=_ZERO_FULL_GRAD)
+        gaps = None if _ZERO_FULL_GRAD else getattr(u, "_grad_gaps", None)
+        if gaps is None and not _ZERO_FULL_GRAD:
+            gaps, end = [], 0
+            for o, n in sorted(zip(u.offsets, u.numels)):
+                if o > end:
+                    gaps.append((end, o))
+                end = max(end, o + n)
+            if end < u.total:
+                gaps.append((end, u.total))
+            u._grad_gaps = gaps
+        if gaps:
+            torch._foreach_zero_([g[a:b] for a, b in gaps])
         u.grad_full = g
         u.ready = 0
         for p, o, n, s in zip(u.params, u.offsets, u.numels, u.shapes):

@@ -235,6 +235,8 @@ def test_ddp_early_grad_norm_matches_full_norm(accum, bucket_mb):
         ref = clip_grad_norm_(ddp.grad_buffers(), 0.3)
         full = torch.sqrt(sum((b.float() ** 2).sum() for b in ddp.grad_buffers()))
         torch.cuda.synchronize()
+        bad = [n for n, p in m.named_parameters() if p.grad is not None and not torch.isfinite(p.grad).all()]
+        assert not bad, (step, "non-finite gradients", bad)
         assert abs(float(st.buf[0]) - float(full)) <= 1e-3 * float(full), (step, float(st.buf[0]), float(full))
         assert abs(float(st.buf[1]) - float(ref.buf[1])) <= 1e-3 * float(ref.buf[1])
         ddp.zero_grad()
