@@ -224,6 +224,10 @@ class IpcCommunicator:
         good = True
         self.self_test_error = None
         dev_pg = self.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        # a node whose peers cannot see each other's memory must fall back to RCCL in seconds, not
+        # after the data-plane timeout (GRT_IPC_SELFTEST_TIMEOUT_S, default 30 s)
+        saved = self.timeout_ticks
+        self.timeout_ticks = min(saved, int(float(os.environ.get("GRT_IPC_SELFTEST_TIMEOUT_S", "30")) * REALTIME_HZ))
         try:
             for i, (n, dt, two) in enumerate(self.SELF_TEST_CASES):
                 if n * torch.tensor([], dtype=dt).element_size() > self.cap:
@@ -248,6 +252,8 @@ class IpcCommunicator:
         except Exception as ex:  # noqa: BLE001 -- a local failure must still reach the agreement below
             good = False
             self.self_test_error = repr(ex)
+        finally:
+            self.timeout_ticks = saved
         ok = torch.tensor([1 if good else 0], dtype=torch.int32, device=dev_pg)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=self.group)
         return int(ok.item()) == 1
