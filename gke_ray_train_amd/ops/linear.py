@@ -102,11 +102,12 @@ def transpose_for_backward(w: torch.Tensor):
     stream (HIP transpose kernel, HBM-bound, overlapping the forward GEMMs) and return (W^T, event)
     for the backward's TN input-gradient GEMM; None where it does not apply (FSDP-managed or
     unaligned weights, non-bf16)."""
-    if not (_TRANSPOSED_DGRAD and (_TRANSPOSED_DGRAD_TRAINABLE or getattr(w, "_grt_fwd_transpose", False))
+    fsdp_t = getattr(w, "_grt_fsdp_fwd_transpose", False)  # FSDP: W^T of the gathered weight
+    if not (_TRANSPOSED_DGRAD and (_TRANSPOSED_DGRAD_TRAINABLE or getattr(w, "_grt_fwd_transpose", False) or fsdp_t)
             and w.is_cuda and w.dtype == torch.bfloat16
             and w.dim() == 2
             and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0 and getattr(w, "_grt_slot", None) is not None
-            and getattr(w, "_grt_unit", None) is None and w.is_contiguous()):
+            and (getattr(w, "_grt_unit", None) is None or fsdp_t) and w.is_contiguous()):
         return None
     from .. import _native
     buf = getattr(w, "_grt_wt_buf", None)
@@ -119,6 +120,8 @@ def transpose_for_backward(w: torch.Tensor):
         _native.kernels().transpose_into(w.detach(), buf)
         ev = torch.cuda.Event()
         ev.record(side)
+    if fsdp_t:  # the gathered weight's buffer goes back to FSDP's pool after the unit's forward:
+        w._grt_wt_pending = ev  # FSDP's _unbind orders that release after this read
     return buf, ev
 
 

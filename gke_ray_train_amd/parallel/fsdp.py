@@ -220,6 +220,7 @@ class FullyShardedDataParallel(nn.Module):
         self._order: List[_Unit] = []
         for u in self.units:
             self._attach_slots(u)
+        self._enable_forward_transposes()
         for u in self.units:
             if u.module is not module:
                 u.module.register_forward_pre_hook(self._make_pre_fwd(u))
@@ -233,6 +234,26 @@ class FullyShardedDataParallel(nn.Module):
         self._grad_zero_by_optimizer = False
         self._grads_consumed = False  # set by an optimizer that zeroed the gradients itself (offload.py)
         self._gstream = None
+
+    def _enable_forward_transposes(self):
+        """Projection weights get W^T written on a side stream at forward time (right after the unit's
+        all-gather, ops/linear.transpose_for_backward), kept until the backward's input-gradient
+        GEMM, which then runs in the TN form instead of the NN form (13-15 % faster on the Llama
+        shapes; the NN kernels were 80 ms of the proxy-8 step, profiles/r6_proxy8_steps.md). The
+        copies persist across steps (one buffer per weight), i.e. one full bf16 copy of the
+        projection weights per rank, so only when that fits ``GRT_FSDP_FWD_TRANSPOSE_MAX_GIB``
+        (default 24: Llama-2-7B / 3-8B yes, 70B no); ``GRT_FSDP_FWD_TRANSPOSE=0`` turns it off."""
+        mode = os.environ.get("GRT_FSDP_FWD_TRANSPOSE", "auto")
+        if mode == "0" or self.device.type != "cuda":
+            return
+        from ..ops.linear import Linear as _DirectLinear
+        ws = [m.weight for u in self.units if u.module is not self.module for m in u.module.modules()
+              if isinstance(m, _DirectLinear) and m.weight.requires_grad and m.weight.dtype == torch.bfloat16]
+        nbytes = sum(w.numel() * w.element_size() for w in ws)
+        if mode == "auto" and nbytes > float(os.environ.get("GRT_FSDP_FWD_TRANSPOSE_MAX_GIB", "24")) * (1 << 30):
+            return
+        for w in ws:
+            w._grt_fsdp_fwd_transpose = True
 
     # ================================================================ optimizer hand-off
     def set_update_events(self, events):
@@ -306,6 +327,14 @@ class FullyShardedDataParallel(nn.Module):
     def _unbind(self, u: _Unit):
         if not self.comm:
             return
+        if self.device.type == "cuda":  # side-stream W^T reads of this gather (ops/linear.py) finish
+            cur = None  # before the buffer can be handed to the next all-gather
+            for p in u.params:
+                ev = getattr(p, "_grt_wt_pending", None)
+                if ev is not None:
+                    cur = cur or torch.cuda.current_stream(self.device)
+                    cur.wait_event(ev)
+                    p._grt_wt_pending = None
         if u.full is not None and u.full is not u.shard:
             self._release(u.full)
         u.full = None
