@@ -41,6 +41,41 @@ from ..ops.optim import FusedAdamW, GradClipState, bump_param_generation
 from .ddp import DistributedDataParallel, forward_wait_modules
 
 
+def fine_forward_wait_modules(module: nn.Module, unit_types, param_ids: set) -> Dict[nn.Module, List[int]]:
+    """``forward_wait_modules`` at projection granularity: inside a transformer layer each
+    ``ops.linear.Linear`` projection waits only for its OWN weight's update (its forward pre-hook),
+    and the layer's other parameters (norm weights, read directly by the layer's forward) are
+    waited for at the layer's entry. The next step's first layer then starts once its norm and QKV
+    weights are updated instead of its whole update (the step-boundary stall of
+    profiles/r6_proxy8_steps.md: embedding + whole layer-0 update ahead of the first norm).
+    Opt-in (GRT_OVERLAP_FINE=1): measured 287.8 vs 287.5 ms per headline step against the layer
+    granularity (3 interleaved rounds, scripts/r6/fine_ab.sh) — the earlier start of layer 0 is
+    cancelled by 4x the chunk launches / events. Returned in forward order."""
+    coarse = forward_wait_modules(module, unit_types, param_ids)
+    if os.environ.get("GRT_OVERLAP_FINE", "0") != "1":
+        return coarse
+    from ..ops.linear import Linear as _DirectLinear
+    out: Dict[nn.Module, List[int]] = {}
+    for m, ids in coarse.items():
+        if type(m).__name__ not in unit_types:
+            out[m] = ids
+            continue
+        mine = set(ids)
+        lins = []
+        for sm in m.modules():
+            if isinstance(sm, _DirectLinear):
+                own = [id(p) for p in sm.parameters(recurse=False) if id(p) in mine]
+                if own:
+                    lins.append((sm, own))
+        taken = {i for _, own in lins for i in own}
+        rest = [i for i in ids if i not in taken]
+        if rest:
+            out[m] = rest  # the layer's entry: its norm weights
+        for sm, own in lins:  # registration order = the layer's forward order
+            out[sm] = own
+    return out
+
+
 class OverlappedOptimizer:
     def __init__(self, engine: DistributedDataParallel, optimizer: FusedAdamW, max_blocks: Optional[int] = None):
         if engine.zero:
@@ -55,7 +90,7 @@ class OverlappedOptimizer:
         for gi, g in enumerate(engine.groups):
             for p, off in zip(g.params, g.offsets):
                 flat_ids[id(p)] = (gi, off, p.numel())
-        waits = forward_wait_modules(engine.module, engine.UNIT_TYPES, set(flat_ids))
+        waits = fine_forward_wait_modules(engine.module, engine.UNIT_TYPES, set(flat_ids))
         # chunk = one module's parameters = one contiguous range per flat group (params of a module
         # are consecutive in registration order, hence in the reversed flat layout)
         self.chunks: List[Tuple[nn.Module, List[Tuple[int, int, int]]]] = []

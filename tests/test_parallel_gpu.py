@@ -1,6 +1,8 @@
 """GPU checks for the data-parallel engines on one MI355X: FSDP (world 1, meta init, HIP kernels,
 direct-grad GEMM slots) produces the same update as DDP; OffloadedAdamW (pinned host moments
 streamed through the HIP AdamW kernel) matches the resident FusedAdamW bit-for-bit."""
+import os
+
 import pytest
 import torch
 
@@ -102,7 +104,9 @@ def test_overlapped_optimizer_matches_serial(transpose, monkeypatch):
         opt = FusedAdamW(ddp.optimizer_param_groups(0.01), lr=1e-3)
         if overlap:
             opt = OverlappedOptimizer(ddp, opt)
-            assert len(opt.chunks) == m.config.num_hidden_layers + 3  # embed, layers, norm, head
+            # embed, layers (GRT_OVERLAP_FINE=1: per layer its norms + 4 projections), final norm, head
+            per = 5 if os.environ.get("GRT_OVERLAP_FINE", "0") == "1" else 1
+            assert len(opt.chunks) == per * m.config.num_hidden_layers + 3
             assert bool(opt._wt) == (transpose == "1")
         g = torch.Generator(device="cuda").manual_seed(9)
         losses = []
