@@ -196,12 +196,17 @@ struct AttnParams {
   // optional (bf16 forward, D = 128): the output also written transposed, o_t[(hq D + d) * ot_ld + token]
   // ([Hq D, tokens]) for the o projection's TN weight gradient
   void* o_t; int64_t ot_ld;
+  // set by the launchers (attn_set_skip_dead, GRT_ATTN_SKIP, default 1): in the causal band a wave
+  // whose rows mask every key of a tile skips that tile's math (forward kernel; it still
+  // takes part in the tile's barrier and LDS-DMA)
+  int skip_dead;
 };
 void attn_set_schedule(int s);
 int attn_get_schedule();
 void attn_set_dkdv_form(int f);  // 1 = 4-wave dK / dV kernel, 2 = wave-pair kernel (default)
 int attn_get_dkdv_form();
 void attn_set_dma_fast(int on);  // 1 = hoisted DMA addressing (default), 0 = per-tile clamped addressing
+void attn_set_skip_dead(int on);  // 1 = skip fully masked causal tiles per wave (default), 0 = compute them
 void attn_fwd(const AttnParams& p, hipStream_t s);
 struct AttnBwdParams {
   AttnParams f;

@@ -223,6 +223,9 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
   }
   const int klim = p.causal ? min(sk - 1, myq + off) : sk - 1;   // keys <= klim are kept
   const int kmask = p.causal ? min(sk, qw0 + off + 1) : sk;      // tiles reaching past need the mask
+  // the wave's last kept key: tiles past it are masked for all 32 rows (the causal band of a
+  // 128-row block, 3 - w tiles for wave w) and skip their math (p.skip_dead)
+  const int klast = p.skip_dead && p.causal ? min(sk - 1, qw0 + 31 + off) : INT_MAX;
 
   int kend = sk;
   if (p.causal) kend = min(kend, q0 + F3M + off);
@@ -365,9 +368,20 @@ __global__ __launch_bounds__(F3NT, 2) void attn_fwd_kernel(const AttnParams p) {
       if constexpr (I & 1) step(t0 + I, std::integral_constant<int, I % NS>{}, sB, sA);
       else step(t0 + I, std::integral_constant<int, I % NS>{}, sA, sB);
     };
+    // tiles past klast are masked for every row of this wave: their exponentials would be 0 and
+    // their P V products add nothing, so the wave's math stops at ntl and it only keeps the later
+    // tiles' barriers and its share of their DMA (the drain below). A separate loop rather than an
+    // early exit inside the step: a branch out of the pipelined body spilled 239 VGPRs.
+    const int ntl = klast == INT_MAX ? nt : min(nt, max(0, klast / F3N + 1));
     int t = 0;
-    for (; t + UNR <= nt; t += UNR) static_for([&](auto i_c) { step_i(t, i_c); }, std::make_integer_sequence<int, UNR>{});
-    static_for([&](auto i_c) { if (t + decltype(i_c)::value < nt) step_i(t, i_c); }, std::make_integer_sequence<int, UNR - 1>{});
+    for (; t + UNR <= ntl; t += UNR) static_for([&](auto i_c) { step_i(t, i_c); }, std::make_integer_sequence<int, UNR>{});
+    static_for([&](auto i_c) { if (t + decltype(i_c)::value < ntl) step_i(t, i_c); }, std::make_integer_sequence<int, UNR - 1>{});
+    for (t = ntl; t < nt; ++t) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t + 1 < nt) wait_dma(min(nt, t + NS - 1) - (t + 2));
+      __builtin_amdgcn_s_barrier();
+      if (t + NS - 1 < nt) dma_tile(t + NS - 1, (uint32_t)(((t + NS - 1) % NS) * F3SLOT));
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -1313,6 +1327,14 @@ int dkdv_form() {
   }
   return g_dkdv;
 }
+int g_skip_dead = -1;
+int skip_dead_now() {
+  if (g_skip_dead < 0) {
+    const char* e = getenv("GRT_ATTN_SKIP");
+    g_skip_dead = e && atoi(e) == 0 ? 0 : 1;
+  }
+  return g_skip_dead;
+}
 int g_dma_fast = -1;
 int dma_fast_now() {
   if (g_dma_fast < 0) {
@@ -1357,6 +1379,7 @@ void attn_set_schedule(int s) { g_sched = s; }
 void attn_set_dkdv_form(int f) { g_dkdv = f == 1 ? 1 : 2; }
 int attn_get_dkdv_form() { return dkdv_form(); }
 void attn_set_dma_fast(int on) { g_dma_fast = on ? 1 : 0; }
+void attn_set_skip_dead(int on) { g_skip_dead = on ? 1 : 0; }
 int attn_get_schedule() { return sched_now(); }
 
 // Padding-free packing (cu_seqlens): the grid is sized for the longest sequence, so a shorter one's
@@ -1367,6 +1390,7 @@ static int sched_for(const AttnParams& p, int bit) { return p.cu_seqlens ? 0 : (
 void attn_fwd(const AttnParams& p0, hipStream_t s) {
   AttnParams p = p0;
   p.dma_fast = dma_fast_for(p, 0);
+  p.skip_dead = skip_dead_now();
   const int nqb = (p.Sq + F3M - 1) / F3M;
   p.sched = pair_if_fills(sched_for(p, 0), nqb, p.B * p.Hq, 2);
   const dim3 grid(q_grid(p.sched, nqb, p.B * p.Hq));
@@ -1383,6 +1407,7 @@ int64_t attn_bwd_workspace_floats(int B, int Hq, int Sq, int Dh) {
 void attn_bwd(const AttnBwdParams& p0, hipStream_t s) {
   AttnBwdParams p = p0;
   p.f.dma_fast = dma_fast_for(p.f, p.do_ss);
+  p.f.skip_dead = skip_dead_now();
   const int64_t rows = (int64_t)p.f.B * p.f.Hq * sq_pad(p.f.Sq);
   hipLaunchKernelGGL(attn_bwd_pre_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, p);
   const int nkb = (p.f.Sk + K2N - 1) / K2N;

@@ -25,6 +25,28 @@ class RayTrainReportCallback:
 
 
 def prepare_trainer(trainer):
-    """Ray's prepare_trainer validates the HF Trainer for Ray; the SFT trainer is already
-    distributed-aware, so this is the identity."""
+    """Ready an SFT trainer to run as one worker of a Train job (Ray's ``prepare_trainer`` role).
+
+    * Checks that the trainer's distributed view (rank / world it sharded data and optimizer
+      state for) matches the Train session's context. A trainer built before the process group
+      was initialised would otherwise train as world 1 on every rank, silently replicating the
+      job N times; that raises here instead.
+    * Attaches a ``RayTrainReportCallback`` when none is attached, so every checkpoint and the
+      final metrics reach ``train.report`` and ``result.metrics`` / ``result.checkpoint`` are
+      filled (the reference imports both names and uses neither, so its result is empty:
+      ray-jobs/fine_tune_llama_ray.py:8).
+
+    Returns the same trainer object.
+    """
+    from ..train import get_context
+    ctx = get_context()
+    want = (ctx.get_world_rank(), ctx.get_world_size())
+    have = (getattr(trainer, "rank", 0), getattr(trainer, "world", 1))
+    if have != want:
+        raise RuntimeError(f"trainer was built for rank {have[0]} of {have[1]} but this Train worker is "
+                           f"rank {want[0]} of {want[1]}; construct the trainer inside the training "
+                           f"function, after the process group is initialised")
+    cbs = getattr(trainer, "callbacks", None)
+    if cbs is not None and not any(isinstance(cb, RayTrainReportCallback) for cb in cbs):
+        cbs.append(RayTrainReportCallback())
     return trainer

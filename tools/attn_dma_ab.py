@@ -8,7 +8,10 @@ Per shape both modes must give bit-identical O / lse / dQ / dK / dV (only addres
 forward and backward are timed in interleaved rounds (median). Shapes: the Llama-2-7B headline
 (B8 S1024 H32), a GQA shape, and a padding-free pack of odd-length sequences (the clamped tail
 tiles) at the reference SFT job's Llama-3.1-8B heads.
-usage: python tools/attn_dma_ab.py [--rounds 7] [--iters 10]
+
+``--flag skip_dead`` A/Bs AttnParams::skip_dead instead (attn_set_skip_dead: a wave skips the causal
+tiles its rows mask entirely, forward kernel), under the same bitwise-equality gate.
+usage: python tools/attn_dma_ab.py [--rounds 7] [--iters 10] [--flag dma_fast|skip_dead]
 """
 import argparse
 import json
@@ -22,6 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gke_ray_train_amd import _native  # noqa: E402
 
 C = _native.kernels()
+SET, FLAG = C.attn_set_dma_fast, "dma"
 
 
 def ev_time(fn, n):
@@ -47,7 +51,7 @@ def run(tag, B, S, Hq, Hkv, lens, rounds, iters):
     fwd = lambda: C.attn_fwd(q, k, v, None, scale, True, None, 0.0, 0, **kw)  # noqa: E731
     res, fw, bw = {}, {0: [], 1: []}, {0: [], 1: []}
     for m in (0, 1):
-        C.attn_set_dma_fast(m)
+        SET(m)
         o, lse = fwd()
         res[m] = (o, lse) + tuple(C.attn_bwd(do, q, k, v, o, lse, None, None, None, scale, True, None, 0.0, 0, **kw))
     torch.cuda.synchronize()
@@ -57,15 +61,15 @@ def run(tag, B, S, Hq, Hkv, lens, rounds, iters):
     o, lse = res[1][:2]
     for _ in range(rounds):
         for m in (0, 1):
-            C.attn_set_dma_fast(m)
+            SET(m)
             fw[m].append(ev_time(fwd, iters))
             bw[m].append(ev_time(lambda: C.attn_bwd(do, q, k, v, o, lse, None, None, None, scale, True, None,
                                                     0.0, 0, **kw), iters))
-    C.attn_set_dma_fast(1)
+    SET(1)
     row = {"shape": tag, "bitwise_equal_o_lse_dq_dk_dv": same}
     for m in (0, 1):
-        row[f"fwd_us_dma{m}"] = round(statistics.median(fw[m]), 1)
-        row[f"bwd_us_dma{m}"] = round(statistics.median(bw[m]), 1)
+        row[f"fwd_us_{FLAG}{m}"] = round(statistics.median(fw[m]), 1)
+        row[f"bwd_us_{FLAG}{m}"] = round(statistics.median(bw[m]), 1)
     print(json.dumps(row), flush=True)
     return all(same)
 
@@ -74,7 +78,9 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--flag", choices=("dma_fast", "skip_dead"), default="dma_fast")
     a = ap.parse_args()
+    SET, FLAG = getattr(C, f"attn_set_{a.flag}"), ("dma" if a.flag == "dma_fast" else "skip")
     ok = run("B8 S1024 Hq32 Hkv32 causal", 8, 1024, 32, 32, None, a.rounds, a.iters)
     ok &= run("B2 S2048 Hq32 Hkv8 causal", 2, 2048, 32, 8, None, a.rounds, a.iters)
     lens = [700, 1023, 517, 1301, 933, 1100, 429]
