@@ -314,6 +314,10 @@ def _late_peer_worker(rank, world, port, q):
         assert ddp._ipc is not None and ddp._ipc.timeout_s == 2.0
         # (1) a healthy step first: the IPC route works and check_all passes
         x = torch.randn(8, 256, device="cuda")
+        with ddp.no_sync():  # library handles / first-call set-up outside the 2 s IPC window
+            ddp(x).backward()
+        torch.cuda.synchronize()
+        ddp.zero_grad()
         dist.barrier()
         ddp(x).backward()
         ddp.finish_gradient_sync()
