@@ -68,6 +68,8 @@ def parse():
                          "(shuffle -> map_batches -> per-rank streaming shard -> iter_torch_batches, produced "
                          "in a separate process through the shared-memory ring); static: on-device batches")
     ap.add_argument("--profile-dir", default="", help="write a torch.profiler trace here")
+    ap.add_argument("--heartbeat", type=float, default=0.0,
+                    help="rank 0 prints its current phase to stderr every N seconds outside the timed region (long builds)")
     ap.add_argument("--metrics-jsonl", default="", help="per-step metrics (phase breakdown, MFU, HBM) -> JSONL; "
                     "adds one host sync per step, so it is off for the headline number")
     ap.add_argument("--device", default="cuda")
@@ -219,6 +221,31 @@ def main():
     run(a)
 
 
+class _Progress:
+    """Phase lines on stderr (rank 0) outside the timed region; with ``--heartbeat N`` also the current
+    phase every N seconds from a daemon thread, for long runs (a 70B offload build) under a runner that
+    treats a silent process as hung. Nothing is printed between the timing barriers."""
+
+    def __init__(self, enabled: bool, every: float):
+        import threading
+        self.enabled, self.name, self.t0, self.quiet = enabled, "start", time.perf_counter(), False
+        self._stop = threading.Event()
+        if enabled and every > 0:
+            def beat():
+                while not self._stop.wait(every):
+                    if not self.quiet:
+                        print(f"bench.py: [{time.perf_counter() - self.t0:.0f} s] {self.name}", file=sys.stderr, flush=True)
+            threading.Thread(target=beat, daemon=True).start()
+
+    def phase(self, name: str):
+        self.name = name
+        if self.enabled:
+            print(f"bench.py: [{time.perf_counter() - self.t0:.0f} s] {name}", file=sys.stderr, flush=True)
+
+    def stop(self):
+        self._stop.set()
+
+
 def run(a):
     if a.ipc:
         os.environ["GRT_IPC_COLLECTIVES"] = "1"
@@ -313,8 +340,12 @@ def run(a):
         print(f"bench.py: memory preflight failed for {cfg.name} {a.parallel} world={world}: "
               + "; ".join(plan.problems()), file=sys.stderr, flush=True)
         sys.exit(3)
+    t_build = time.perf_counter()
+    progress = _Progress(rank == 0, a.heartbeat)
+    progress.phase(f"building {cfg.name} ({a.parallel}, world {world})")
     model, eng, call, opt = build(a, cfg, dev, dtype, world)
     model.train()
+    progress.phase(f"model and optimizer built in {time.perf_counter() - t_build:.1f} s; warm-up")
 
     mb = a.micro_batch or a.batch
     assert a.batch % mb == 0
@@ -402,6 +433,7 @@ def run(a):
         loss = step()
     if not fsdp:
         eng.wait_params()
+    progress.phase(f"{a.warmup} warm-up steps issued; timing {a.steps} steps")
     if not cpu:
         torch.cuda.synchronize()
     if world > 1:
@@ -414,6 +446,7 @@ def run(a):
         stacks = os.environ.get("GRT_PROFILE_STACKS", "0") == "1"  # attribute kernels to Python call sites
         prof = profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=stacks, with_stack=stacks)
         prof.__enter__()
+    progress.quiet = True  # no heartbeat lines inside the timed region
     t0 = time.perf_counter()
     for i in range(a.steps):
         loss = timed_step(i)
@@ -426,6 +459,7 @@ def run(a):
     if not cpu:
         torch.cuda.synchronize()
     t1 = time.perf_counter()
+    progress.stop()
     if world > 1:  # a failed xGMI IPC collective (parallel/ipc.py) fails the run instead of timing it
         from gke_ray_train_amd.parallel.ipc import check_all
         check_all()

@@ -85,16 +85,18 @@ def build_kernels(force=False, jobs=8, verbose=False) -> Path:
                    "-munsafe-fp-atomics", *_check_flags(), *inc, "-c", str(src), "-o", str(obj)]
             tasks.append(cmd)
     pyinc = sysconfig.get_paths()["include"]
-    bind_src = CSRC / "bindings" / "ops.cpp"
-    bind_obj = BUILD / "ops_bind.o"
-    objs.append(bind_obj)
-    if force or _newer(bind_obj, [bind_src, *hdrs]):
-        cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
-               "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-               "-I", str(tdir / "include"), "-I", str(tdir / "include" / "torch" / "csrc" / "api" / "include"),
-               "-I", pyinc, "-I", str(ROCM / "include"), *inc, "-Wno-deprecated-declarations",
-               "-c", str(bind_src), "-o", str(bind_obj)]
-        tasks.append(cmd)
+    # host sources: the pybind module (ops.cpp) and the host-side runtime pieces it binds (the
+    # HSA SDMA copier), compiled by g++ against the HIP / HSA / torch headers
+    for bind_src in sorted((CSRC / "bindings").glob("*.cpp")):
+        bind_obj = BUILD / ("ops_bind.o" if bind_src.stem == "ops" else bind_src.stem + "_host.o")
+        objs.append(bind_obj)
+        if force or _newer(bind_obj, [bind_src, *hdrs]):
+            cmd = ["g++", "-O2", "-fPIC", "-std=c++17", "-pthread", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+                   "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                   "-I", str(tdir / "include"), "-I", str(tdir / "include" / "torch" / "csrc" / "api" / "include"),
+                   "-I", pyinc, "-I", str(ROCM / "include"), *inc, "-Wno-deprecated-declarations",
+                   "-c", str(bind_src), "-o", str(bind_obj)]
+            tasks.append(cmd)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         for out in ex.map(_run, tasks):
             if verbose and out.strip():
@@ -104,7 +106,7 @@ def build_kernels(force=False, jobs=8, verbose=False) -> Path:
         lib = tdir / "lib"
         cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(so),
                "-L", str(lib), "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
-               f"-Wl,-rpath,{lib}"]
+               f"-Wl,-rpath,{lib}", "-L", str(ROCM / "lib"), "-lhsa-runtime64"]
         _run(cmd)
     return so
 

@@ -12,6 +12,7 @@
 #include <c10/core/DeviceGuard.h>
 
 #include "grt_kernels.h"
+#include "grt_sdma.h"
 
 namespace {
 
@@ -973,6 +974,31 @@ void copy_sdma(Tensor& dst, const Tensor& src) {
   TORCH_CHECK(e == hipSuccess, "copy_sdma: hipMemcpyAsync: ", hipGetErrorString(e));
 }
 
+// dst (pinned host) <- src (device) on an SDMA engine, ordered on src's current stream through the
+// HSA runtime (csrc/bindings/sdma_copy.cpp): the HIP route above still lands on a blit kernel for a
+// device -> host copy on this image (profiles/r6_offload_link.md).
+void sdma_d2h(Tensor& dst, const Tensor& src) {
+  TORCH_CHECK(dst.is_contiguous() && src.is_contiguous(), "sdma_d2h: contiguous tensors");
+  TORCH_CHECK(src.is_cuda() && !dst.is_cuda() && dst.is_pinned(), "sdma_d2h: device source, pinned host destination");
+  const int64_t n = dst.numel() * dst.element_size();
+  TORCH_CHECK(n == src.numel() * src.element_size(), "sdma_d2h: byte counts differ");
+  c10::OptionalDeviceGuard guard(src.device());
+  grt::sdma_d2h(dst.data_ptr(), src.data_ptr(), (size_t)n, src.get_device(), cur_stream(src));
+}
+
+py::dict sdma_stats(int64_t device) {
+  const grt::SdmaStats st = grt::sdma_stats((int)device);
+  py::dict d;
+  d["copies"] = st.copies;
+  d["bytes"] = st.bytes;
+  d["busy_s"] = st.busy_ns * 1e-9;
+  d["error"] = st.error;
+  d["engine"] = st.engine;
+  d["engines_available"] = st.engines_available;
+  d["engines_preferred"] = st.engines_preferred;
+  return d;
+}
+
 // y = x W^T for 1-4 rows (1-16 rows when K % 256 == 0: 3+ rows run on MFMA); swiglu: x = [gate | up]
 // [M, 2K] -> y = (silu(gate) * up) W^T
 Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
@@ -1374,6 +1400,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_bwd_t", &swiglu_bwd_t);
   m.def("transpose_into", &transpose_into);
   m.def("copy_sdma", &copy_sdma);
+  m.def("sdma_d2h", &sdma_d2h, "pinned host <- device on an SDMA engine, ordered on the source's current stream");
+  m.def("sdma_stats", &sdma_stats, "copies / bytes / worker busy seconds / first error of the SDMA copier");
+  m.def("sdma_clear_error", [](int64_t device) { grt::sdma_clear_error((int)device); });
   m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);
   m.def("gemv_fused", &gemv_fused, py::arg("x"), py::arg("w"), py::arg("sumsq"), py::arg("slot"),
         py::arg("swiglu") = false, py::arg("g") = py::none(), py::arg("res") = py::none(), py::arg("eps") = 1e-5,

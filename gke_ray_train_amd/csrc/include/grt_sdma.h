@@ -1,0 +1,23 @@
+// Device -> pinned-host copies on the SDMA engines, ordered with HIP streams (csrc/bindings/sdma_copy.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace grt {
+
+struct SdmaStats {
+  uint64_t copies = 0, bytes = 0, busy_ns = 0;  // busy_ns: worker time from copy issue to completion
+  uint32_t engine = 0, engines_available = 0, engines_preferred = 0;  // hsa_amd_sdma_engine_id_t masks (0: runtime-assigned)
+  std::string error;                          // first failure since the last clear ("" = none)
+};
+
+// Copy `bytes` from device memory `src` to pinned host memory `dst` after the work already on
+// stream `s`; work enqueued on `s` afterwards runs after the copy has landed.
+void sdma_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t s);
+SdmaStats sdma_stats(int device);
+void sdma_clear_error(int device);
+
+}  // namespace grt

@@ -30,7 +30,12 @@ MI355X design:
   next uploads, so both directions of the owned chunks use the backward window and the forward
   window carries only the ring chunks' traffic.
   A slot is reused only after the download of its previous chunk (event per slot), which also
-  orders every upload after the previous step's download of the same host range.
+  orders every upload after the previous step's download of the same host range;
+* WRITE-BACK ENGINE (``GRT_OFFLOAD_D2H``): ``sdma`` (default) hands each write-back to an SDMA
+  engine of its own through the HSA runtime (``sdma_d2h``, csrc/bindings/sdma_copy.cpp), ordered on
+  the download stream like a stream copy, so no write-back occupies the CUs; a failed SDMA copy
+  raises at the next ``step()`` / ``synchronize()``. ``blit`` copies with ``Tensor.copy_``, which
+  ROCclr runs as blit kernels on the CUs (profiles/r6_offload_link.md).
 """
 from __future__ import annotations
 
@@ -83,6 +88,10 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         self._landed: Dict[int, torch.cuda.Event] = {}  # chunk index -> upload done (prefetched)
         self._pending_down: List[tuple] = []  # (chunk index, update done) of deferred write-backs
         self.defer_writeback = os.environ.get("GRT_OFFLOAD_DEFER_WRITEBACK", "1") != "0"
+        mode = os.environ.get("GRT_OFFLOAD_D2H", "sdma")
+        if mode not in ("blit", "sdma"):
+            raise ValueError(f"GRT_OFFLOAD_D2H={mode!r}: expected 'blit' or 'sdma'")
+        self.d2h_engine = mode if fsdp.device.type == "cuda" else "blit"
         fsdp._grad_zero_by_optimizer = True
         if self.prefetch_slots > 0:
             fsdp.add_forward_tail_hook(self.prefetch)
@@ -113,6 +122,7 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         up, upd, down = self._streams
         comp = torch.cuda.current_stream(dev)
         fs.wait_updates()  # the previous step's updates all landed (normally long done)
+        self._check_d2h()
         self._flush_downloads()  # no forward tail since the last step (prefetch() did not run)
         hbs, work = [], []
         for gi, group in enumerate(self.param_groups):
@@ -193,8 +203,13 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         sst = self.state[self.param_groups[0]["params"][0]]
         with torch.cuda.stream(down):
             down.wait_event(done)
-            sst["exp_avg"][s:e].copy_(mb[:e - s], non_blocking=True)
-            sst["exp_avg_sq"][s:e].copy_(vb[:e - s], non_blocking=True)
+            if self.d2h_engine == "sdma":
+                C = _native.kernels()
+                C.sdma_d2h(sst["exp_avg"][s:e], mb[:e - s])
+                C.sdma_d2h(sst["exp_avg_sq"][s:e], vb[:e - s])
+            else:
+                sst["exp_avg"][s:e].copy_(mb[:e - s], non_blocking=True)
+                sst["exp_avg_sq"][s:e].copy_(vb[:e - s], non_blocking=True)
             free = torch.cuda.Event()
             free.record(down)
         self._slot_free[slot] = free
@@ -255,6 +270,19 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         if self._streams is not None:
             self._flush_downloads()
             torch.cuda.current_stream(self.fsdp.device).wait_stream(self._streams[2])
+            self._check_d2h()
+
+    def _check_d2h(self):
+        """Raise if an SDMA write-back failed or timed out since the last check (its host range
+        then holds stale moments; the copy released the stream instead of hanging it)."""
+        if self.d2h_engine != "sdma" or self._streams is None:
+            return
+        C = _native.kernels()
+        dev = self.fsdp.device.index if self.fsdp.device.index is not None else torch.cuda.current_device()
+        err = C.sdma_stats(dev)["error"]
+        if err:
+            C.sdma_clear_error(dev)
+            raise RuntimeError(f"offloaded AdamW: SDMA moment write-back failed: {err}")
 
     def state_dict(self):
         """Moments of resident units are copied into the host tensors, so the layout is the plain

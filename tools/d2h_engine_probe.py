@@ -3,7 +3,8 @@
 ``rocprofv3 --kernel-trace --memory-copy-trace``: SDMA copies appear as MEMORY_COPY_DEVICE_TO_HOST,
 blit copies as ``__amd_rocclr_copyBuffer`` kernels. Variants (argv[1]): ``torch`` (copy_ into a
 hipHostMalloc'ed pin_memory tensor), ``nocu`` (copy_sdma = hipMemcpyDeviceToDeviceNoCU),
-``registered`` (copy_ into a hipHostRegister'ed plain host tensor). Prints GB/s."""
+``registered`` (copy_ into a hipHostRegister'ed plain host tensor), ``hsa`` (``sdma_d2h``: the HSA
+runtime's async copy on an SDMA engine, stream-ordered by csrc/bindings/sdma_copy.cpp). Prints GB/s."""
 import os
 import sys
 import time
@@ -24,10 +25,10 @@ def main(mode, mib=256, reps=4):
     else:
         h = torch.empty(n, dtype=torch.float32).pin_memory()
     s = torch.cuda.Stream()
-    if mode == "nocu":
+    if mode in ("nocu", "hsa"):
         from gke_ray_train_amd import _native
         C = _native.kernels()
-        fn = lambda: C.copy_sdma(h, d)  # noqa: E731
+        fn = (lambda: C.copy_sdma(h, d)) if mode == "nocu" else (lambda: C.sdma_d2h(h, d))
     else:
         fn = lambda: h.copy_(d, non_blocking=True)  # noqa: E731
     with torch.cuda.stream(s):
