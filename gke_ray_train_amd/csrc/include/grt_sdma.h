@@ -16,6 +16,9 @@ struct SdmaStats {
 
 // Copy `bytes` from device memory `src` to pinned host memory `dst` after the work already on
 // stream `s`; work enqueued on `s` afterwards runs after the copy has landed.
+// The copies of one device run one at a time in submission order. Submit from ONE stream per device
+// (the offloaded AdamW's download stream), or from streams that never wait on each other: a copy
+// whose producer waits on another stream's later copy would wait forever behind it.
 void sdma_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t s);
 SdmaStats sdma_stats(int device);
 void sdma_clear_error(int device);
