@@ -1390,7 +1390,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_get_dkdv_form", &grt::attn_get_dkdv_form);
   m.def("attn_set_dma_fast", &grt::attn_set_dma_fast, "1 = hoisted LDS-DMA addressing (default), 0 = clamped per tile");
   m.def("attn_set_skip_dead", &grt::attn_set_skip_dead,
-        "1 = a wave skips the causal tiles its rows mask entirely (default), 0 = computes them");
+        "1 = forward / dK-dV waves skip the causal tiles they mask entirely (default), 0 = compute them");
   m.def("nf4_quantize", &nf4_quantize);
   m.def("nf4_dequantize", &nf4_dequantize);
   m.def("nf4_dequantize_t", &nf4_dequantize_t);

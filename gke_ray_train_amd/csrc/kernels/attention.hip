@@ -899,6 +899,9 @@ __global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdPa
   const int total = (k0 < sk) ? nqt * grp : 0;
   const int qlim = mykey < sk ? (p.causal ? mykey - off : INT_MIN) : INT_MAX;
   const int qmask = (k0 + K3N > sk) ? INT_MAX : (p.causal ? kw0 + 31 - off : INT_MIN);
+  // query tiles ending at or before dead_q hold no query at or past this pair's first key: every
+  // (query, key) of theirs is masked (causal), and with keys past sk the tile is masked anyway
+  const int dead_q = p.skip_dead && p.causal && !DROP ? kw0 - off : INT_MIN;
 
   // LDS-DMA of a tile: wave w fills image rows 4w .. 4w+3 of Q and of dO (one 1-KiB piece each)
   // and its own copy of the tile's 32 lse2 and 32 delta values (3 instructions per wave and tile)
@@ -980,7 +983,12 @@ __global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdPa
       advance(dma_h, dma_q);
     }
     const char* qi = smem + SL * K3SLOT;
+    // causal tiles whose queries all precede this pair's first key (the first `pr` tiles of each
+    // head's sweep): p = dS = 0 there, so both roles skip their math (p.skip_dead; energy only: the
+    // workgroup's barrier cadence is set by the other pairs)
+    const bool dead_c = cur_q + K3M <= dead_q, dead_p = prv_q + K3M <= dead_q;
     if constexpr (SW) {
+     if (!dead_c) {
       const float* st = reinterpret_cast<const float*>(qi + 2 * K3IMG + w * 1024);
       f32x16 s = f32x16{};
       if (cur_q < qmask) {  // wave-uniform: the tile touches the diagonal / key padding
@@ -1019,15 +1027,18 @@ __global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdPa
           acc[db] = mfma32(a, stp ? pb1 : pb0, acc[db]);
         }
       }
+     }
     } else {  // the previous tile first: its dP is the only one live (register budget of 2 waves/SIMD)
-      if (t > 0) finish(t - 1, smem + ((SL + K3NS - 1) % K3NS) * K3SLOT);
+      if (t > 0 && !dead_p) finish(t - 1, smem + ((SL + K3NS - 1) % K3NS) * K3SLOT);
       __builtin_amdgcn_sched_barrier(0);
-      bf16x8 fd[D / 16];
+      if (!dead_c) {
+        bf16x8 fd[D / 16];
 #pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) fd[ks] = lds_row_read(qi + K3IMG, l32, 2 * ks + h);
-      dpc = f32x16{};
+        for (int ks = 0; ks < D / 16; ++ks) fd[ks] = lds_row_read(qi + K3IMG, l32, 2 * ks + h);
+        dpc = f32x16{};
 #pragma unroll
-      for (int ks = 0; ks < D / 16; ++ks) dpc = mfma32(fd[ks], kv[ks], dpc);
+        for (int ks = 0; ks < D / 16; ++ks) dpc = mfma32(fd[ks], kv[ks], dpc);
+      }
     }
     prv_h = cur_h;
     prv_q = cur_q;
@@ -1060,7 +1071,9 @@ __global__ __launch_bounds__(K3NT, 1) void attn_bwd_dkdv2_kernel(const AttnBwdPa
     // the dP-wave's last tile: its P is published at this barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if constexpr (!SW) finish(total - 1, smem + ((total - 1) % K3NS) * K3SLOT);
+    if constexpr (!SW) {
+      if (prv_q + K3M > dead_q) finish(total - 1, smem + ((total - 1) % K3NS) * K3SLOT);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
