@@ -197,7 +197,7 @@ struct AttnParams {
   // ([Hq D, tokens]) for the o projection's TN weight gradient
   void* o_t; int64_t ot_ld;
   // set by the launchers (attn_set_skip_dead, GRT_ATTN_SKIP, default 1): in the causal band a wave
-  // whose rows mask every key of a tile skips that tile's math (forward and wave-pair dK / dV kernels; it still
+  // whose rows mask every key of a tile skips that tile's math (forward, dQ and wave-pair dK / dV kernels; it still
   // takes part in the tile's barrier and LDS-DMA)
   int skip_dead;
 };

@@ -1188,6 +1188,7 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
   const int klim = p.causal ? min(sk - 1, myq + off) : sk - 1;
   // first key past which a tile needs the mask for some lane of this wave
   const int kmask = p.causal ? min(sk, qw0 + off + 1) : sk;
+  const int klast = p.skip_dead && p.causal && !DROP ? min(sk - 1, qw0 + 31 + off) : INT_MAX;  // see the forward
 
   int kend = sk;
   if (p.causal) kend = min(kend, q0 + Q2M + off);
@@ -1254,6 +1255,7 @@ __global__ __launch_bounds__(Q2NT, 2) void attn_bwd_dq_kernel(const AttnBwdParam
     if (t + 1 < nt) wait_dma(min(nt, t + Q2NSLOT - 1) - (t + 2));
     __builtin_amdgcn_s_barrier();
     if (t + Q2NSLOT - 1 < nt) dma_tile(t + Q2NSLOT - 1, (uint32_t)(((SL + Q2NSLOT - 1) % Q2NSLOT) * Q2SLOT));
+    if (t * Q2N > klast) return;  // tile t (and every later one) masked for the whole wave: p = dS = 0
 
     sdp(t + 1, std::integral_constant<int, (SL + 1) % Q2NSLOT>{}, s_n, dp_n);  // past the end: dropped
 

@@ -1,6 +1,6 @@
 # dead-tile skip in the wave-pair dK/dV kernel: attention GPU tests (incl. wave-pair vs 4-wave bitwise),
 # stale-LDS tests, isolated A/B, interleaved headline A/B
-O=gpurun_out/r6skip2; mkdir -p $O
+O=gpurun_out/r6skip3; mkdir -p $O
 timeout -k 10 400 python3 -u -m pytest tests/test_kernels_gpu.py tests/test_lds_poison_gpu.py -x -q -k "attn or attention or dkdv" --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 timeout -k 10 300 python3 tools/attn_dma_ab.py --flag skip_dead --rounds 7 --iters 10 > $O/ab.jsonl 2> $O/ab.err || { cat $O/ab.jsonl; tail -20 $O/ab.err; exit 1; }

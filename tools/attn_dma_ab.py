@@ -10,7 +10,7 @@ forward and backward are timed in interleaved rounds (median). Shapes: the Llama
 tiles) at the reference SFT job's Llama-3.1-8B heads.
 
 ``--flag skip_dead`` A/Bs AttnParams::skip_dead instead (attn_set_skip_dead: a wave skips the causal
-tiles its rows mask entirely, forward and wave-pair dK / dV kernels), under the same bitwise-equality gate.
+tiles its rows mask entirely: forward, dQ and wave-pair dK / dV kernels), under the same bitwise-equality gate.
 usage: python tools/attn_dma_ab.py [--rounds 7] [--iters 10] [--flag dma_fast|skip_dead]
 """
 import argparse
