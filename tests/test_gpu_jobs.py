@@ -203,3 +203,42 @@ def test_sft_full_ft_overlapped_engine_matches_plain_path(tmp_path, monkeypatch)
         d = (runs[0][1][k] - v).abs().max().item()
         assert d < 3e-2 * max(1.0, v.abs().max().item()), (k, d)
     assert runs[0][2].metrics["train_tokens_per_second"] > 0
+
+
+def test_sft_full_ft_resume_on_gpu_matches_uninterrupted(tmp_path, monkeypatch):
+    """Full fine-tuning on the overlapped engine, resumed from checkpoint-3 (per-parameter
+    optimizer.pt loaded through load_portable_optimizer_state_dict into the device state) in a fresh
+    trainer: steps 4-6 end at the parameters of the uninterrupted 6-step run to bf16 rounding (the
+    stochastic-rounding bits and the first post-resume dX GEMM, NN until an update of this process
+    registers W^T, differ), and far closer than a resume that drops the optimizer state (control)."""
+    from gke_ray_train_amd.models import build_llama
+    from gke_ray_train_amd.parallel import DistributedDataParallel
+    from gke_ray_train_amd.trainer import SFTConfig, SFTTrainer
+    rows = [{"text": "select a, b from t%d where c > %d order by b" % (i, 3 * i)} for i in range(48)]
+
+    def make(out):
+        torch.manual_seed(0)
+        m = build_llama("llama-tiny-gqa", device="cuda", dtype=torch.bfloat16, seed=3)
+        tr = SFTTrainer(m, SFTConfig(output_dir=str(out), per_device_train_batch_size=2, gradient_accumulation_steps=2,
+                                     learning_rate=1e-3, max_steps=6, logging_steps=2, save_steps=3,
+                                     save_strategy="steps", max_seq_length=64, optim="adamw_torch",
+                                     report_to="none", seed=1), train_dataset=rows)
+        return m, tr
+
+    ma, ta = make(tmp_path / "a")
+    ta.train()
+    torch.cuda.synchronize()
+    ref = {k: v.float().clone() for k, v in ma.state_dict().items()}
+
+    def resumed(out):
+        m, tr = make(out)
+        tr.train(resume_from_checkpoint=str(tmp_path / "a" / "checkpoint-3"))
+        torch.cuda.synchronize()
+        assert tr.state["global_step"] == 6
+        return max((v.float() - ref[k]).abs().max().item() / max(1e-3, ref[k].abs().max().item())
+                   for k, v in m.state_dict().items())
+
+    worst = resumed(tmp_path / "b")
+    monkeypatch.setattr(DistributedDataParallel, "load_portable_optimizer_state_dict", lambda self, opt, sd: None)
+    worst_dropped = resumed(tmp_path / "c")
+    assert worst <= 1e-2 and worst_dropped >= 4 * worst, (worst, worst_dropped)
