@@ -31,11 +31,11 @@ MI355X design:
   window carries only the ring chunks' traffic.
   A slot is reused only after the download of its previous chunk (event per slot), which also
   orders every upload after the previous step's download of the same host range;
-* WRITE-BACK ENGINE (``GRT_OFFLOAD_D2H``): ``sdma`` (default) hands each write-back to an SDMA
-  engine of its own through the HSA runtime (``sdma_d2h``, csrc/bindings/sdma_copy.cpp), ordered on
-  the download stream like a stream copy, so no write-back occupies the CUs; a failed SDMA copy
-  raises at the next ``step()`` / ``synchronize()``. ``blit`` copies with ``Tensor.copy_``, which
-  ROCclr runs as blit kernels on the CUs (profiles/r6_offload_link.md).
+* WRITE-BACK ENGINE (``GRT_OFFLOAD_D2H``): ``blit`` (default) copies with ``Tensor.copy_``, which
+  ROCclr runs as blit kernels on the CUs; ``sdma`` hands each write-back to an SDMA engine of its own
+  through the HSA runtime (``sdma_d2h``, csrc/bindings/sdma_copy.cpp), ordered on the download
+  stream like a stream copy, so no write-back occupies the CUs; a failed SDMA copy raises at the next
+  ``step()`` / ``synchronize()`` (profiles/r6_offload_link.md).
 """
 from __future__ import annotations
 
@@ -88,7 +88,7 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         self._landed: Dict[int, torch.cuda.Event] = {}  # chunk index -> upload done (prefetched)
         self._pending_down: List[tuple] = []  # (chunk index, update done) of deferred write-backs
         self.defer_writeback = os.environ.get("GRT_OFFLOAD_DEFER_WRITEBACK", "1") != "0"
-        mode = os.environ.get("GRT_OFFLOAD_D2H", "sdma")
+        mode = os.environ.get("GRT_OFFLOAD_D2H", "blit")
         if mode not in ("blit", "sdma"):
             raise ValueError(f"GRT_OFFLOAD_D2H={mode!r}: expected 'blit' or 'sdma'")
         self.d2h_engine = mode if fsdp.device.type == "cuda" else "blit"
