@@ -49,8 +49,15 @@ def load_counters(path):
 def main(d):
     tr = glob.glob(os.path.join(d, "**", "trace_kernel_trace.csv"), recursive=True)
     dur = defaultdict(list)
-    for r in csv.DictReader(open(tr[0])):
-        dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e9)
+    if tr:
+        for r in csv.DictReader(open(tr[0])):
+            dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e9)
+    else:  # no separate kernel trace: the (serialised) dispatch times of the first counter pass
+        seen = set()
+        for r in csv.DictReader(open(glob.glob(os.path.join(d, "**", "sq_counter_collection.csv"), recursive=True)[0])):
+            if r["Dispatch_Id"] not in seen:
+                seen.add(r["Dispatch_Id"])
+                dur[r["Kernel_Name"]].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e9)
     ctr = {}
     for tag in ("sq", "fetch", "write"):
         f = glob.glob(os.path.join(d, "**", f"{tag}_counter_collection.csv"), recursive=True)
