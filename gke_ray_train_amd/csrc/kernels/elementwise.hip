@@ -261,6 +261,65 @@ __global__ __launch_bounds__(kNT) void rope_kernel(const T* __restrict__ src_q, 
   }
 }
 
+// D = 128 (every Llama head): one thread per 8-pair group with 32-bit index math and compile-time
+// group count (the generic kernel's 64-bit div / mod per item were the bulk of its VALU), one group
+// per thread on a full grid so every thread's six loads are in flight together.
+template <typename T, bool FWD>
+__global__ __launch_bounds__(kNT) void rope128_kernel(const T* __restrict__ src_q, const T* __restrict__ src_k,
+                                                      int64_t src_ld_q, int64_t src_ld_k,
+                                                      T* __restrict__ dst_q, T* __restrict__ dst_k,
+                                                      int64_t dst_ld_q, int64_t dst_ld_k,
+                                                      const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                      const int32_t* __restrict__ pos, uint32_t total, int S,
+                                                      int hq, int hkv) {
+  constexpr int D = 128, half = 64;
+  const uint32_t i = blockIdx.x * kNT + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t heads = (uint32_t)(hq + hkv);
+  const uint32_t th = i >> 3, t = th / heads, h = th - t * heads;
+  const int c = (int)(i & 7) * 8;
+  const int p = pos ? pos[t] : (int)(t % (uint32_t)S);
+  const T* src = h < (uint32_t)hq ? src_q + (int64_t)t * src_ld_q + (int64_t)h * D
+                                  : src_k + (int64_t)t * src_ld_k + (int64_t)(h - hq) * D;
+  T* dst = h < (uint32_t)hq ? dst_q + (int64_t)t * dst_ld_q + (int64_t)h * D
+                            : dst_k + (int64_t)t * dst_ld_k + (int64_t)(h - hq) * D;
+  float x1[8], x2[8], cs[8], sn[8], o1[8], o2[8];
+  if constexpr (Vec16<T>::N == 8) {
+    load16(src + c, x1);
+    load16(src + half + c, x2);
+  } else {
+    load16(src + c, x1); load16(src + c + 4, x1 + 4);
+    load16(src + half + c, x2); load16(src + half + c + 4, x2 + 4);
+  }
+  const float* cr = cosb + (int64_t)p * half + c;
+  const float* sr = sinb + (int64_t)p * half + c;
+  load16(cr, cs); load16(cr + 4, cs + 4);
+  load16(sr, sn); load16(sr + 4, sn + 4);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float s2 = FWD ? sn[k] : -sn[k];
+    o1[k] = x1[k] * cs[k] - x2[k] * s2;
+    o2[k] = x2[k] * cs[k] + x1[k] * s2;
+  }
+  if constexpr (Vec16<T>::N == 8) {
+    store16(dst + c, o1);
+    store16(dst + half + c, o2);
+  } else {
+    store16(dst + c, o1); store16(dst + c + 4, o1 + 4);
+    store16(dst + half + c, o2); store16(dst + half + c + 4, o2 + 4);
+  }
+}
+
+// GRT_ROPE128=0 / rope_set_fast(0): the generic kernel for D = 128 as well (A/B switch)
+int g_rope128 = -1;
+inline bool rope128_on() {
+  if (g_rope128 < 0) {
+    const char* e = getenv("GRT_ROPE128");
+    g_rope128 = e && e[0] == '0' ? 0 : 1;
+  }
+  return g_rope128 != 0;
+}
+
 // ------------------------- decode: RoPE + KV-cache append ------------------
 // The cached-decode step's q / k rotation and the cache writes in one launch: token t (batch row
 // t / tpr) at position pos[t] has its q heads rotated into q_out and its rotated k heads and raw v
@@ -473,10 +532,19 @@ void gelu_bwd(DType dt, const void* x, const void* dy, void* dx, int64_t n, hipS
   GRT_DISPATCH(dt, K, 0);
 #undef K
 }
+void rope_set_fast(int on) { g_rope128 = on ? 1 : 0; }
 void rope_fwd(DType dt, const void* qkv, int64_t ld, void* q_out, void* k_out, const float* cos,
               const float* sin, const int32_t* pos, int64_t T_, int S, int hq, int hkv, int D,
               hipStream_t s) {
   const int64_t work = T_ * (hq + hkv) * (D / 16);
+  if (D == 128 && work < INT32_MAX && rope128_on()) {
+#define K(TY, ...) hipLaunchKernelGGL((rope128_kernel<TY, true>), dim3((unsigned)((work + kNT - 1) / kNT)), dim3(kNT), 0, s, \
+      (const TY*)qkv, (const TY*)qkv + (int64_t)hq * D, ld, ld, (TY*)q_out, (TY*)k_out, (int64_t)hq * D, \
+      (int64_t)hkv * D, cos, sin, pos, (uint32_t)work, S, hq, hkv)
+    GRT_DISPATCH(dt, K, 0);
+#undef K
+    return;
+  }
 #define K(TY, ...) hipLaunchKernelGGL((rope_kernel<TY, true>), dim3(grid_for(work)), dim3(kNT), 0, s, \
       (const TY*)qkv, (const TY*)qkv + (int64_t)hq * D, ld, ld, (TY*)q_out, (TY*)k_out, (int64_t)hq * D, \
       (int64_t)hkv * D, cos, sin, pos, T_, S, hq, hkv, D)
@@ -495,6 +563,14 @@ void rope_bwd(DType dt, const void* dq, const void* dk, void* dqkv, int64_t ld, 
               const float* sin, const int32_t* pos, int64_t T_, int S, int hq, int hkv, int D,
               hipStream_t s) {
   const int64_t work = T_ * (hq + hkv) * (D / 16);
+  if (D == 128 && work < INT32_MAX && rope128_on()) {
+#define K(TY, ...) hipLaunchKernelGGL((rope128_kernel<TY, false>), dim3((unsigned)((work + kNT - 1) / kNT)), dim3(kNT), 0, s, \
+      (const TY*)dq, (const TY*)dk, (int64_t)hq * D, (int64_t)hkv * D, (TY*)dqkv, (TY*)dqkv + (int64_t)hq * D, \
+      ld, ld, cos, sin, pos, (uint32_t)work, S, hq, hkv)
+    GRT_DISPATCH(dt, K, 0);
+#undef K
+    return;
+  }
 #define K(TY, ...) hipLaunchKernelGGL((rope_kernel<TY, false>), dim3(grid_for(work)), dim3(kNT), 0, s, \
       (const TY*)dq, (const TY*)dk, (int64_t)hq * D, (int64_t)hkv * D, (TY*)dqkv, (TY*)dqkv + (int64_t)hq * D, \
       ld, ld, cos, sin, pos, T_, S, hq, hkv, D)

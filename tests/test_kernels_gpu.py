@@ -235,6 +235,36 @@ def test_rope():
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("T,S,hq,hkv,packed", [(8192, 1024, 32, 32, False), (600, 300, 32, 8, True), (37, 37, 4, 2, False)])
+def test_rope_d128_kernel_matches_generic(dtype, T, S, hq, hkv, packed):
+    """The D = 128 RoPE kernel (32-bit indexing, one 8-pair group per thread) gives the generic
+    kernel's q / k and backward dqkv bit for bit, with and without per-token positions."""
+    from gke_ray_train_amd.ops import _ref
+    C = _C()
+    D = 128
+    g = torch.Generator(device=DEV).manual_seed(T + hq)
+    qkv = torch.randn(T, (hq + 2 * hkv) * D, device=DEV, dtype=dtype, generator=g)
+    cos, sin = _ref.rope_tables(S, D, 10000.0, device=DEV)
+    cos, sin = cos.float().contiguous(), sin.float().contiguous()
+    pos = torch.cat([torch.arange(S, device=DEV), torch.arange(T - S, device=DEV)]).int() if packed else None
+    dq = torch.randn(T, hq * D, device=DEV, dtype=dtype, generator=g)
+    dk = torch.randn(T, hkv * D, device=DEV, dtype=dtype, generator=g)
+    out = []
+    try:
+        for fast in (1, 0):
+            C.rope_set_fast(fast)
+            q, k = C.rope_fwd(qkv, cos, sin, pos, hq, hkv, D, S)
+            dqkv = torch.full_like(qkv, float("nan"))
+            C.rope_bwd(dq, dk, dqkv, cos, sin, pos, hq, hkv, D, S)
+            torch.cuda.synchronize()
+            out.append((q, k, dqkv[:, :(hq + hkv) * D].clone()))
+    finally:
+        C.rope_set_fast(1)
+    for name, a, b in zip(("q", "k", "dqk"), *out):
+        assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("V", [32000, 283])
 def test_cross_entropy(dtype, V):
     from gke_ray_train_amd import ops
