@@ -1389,7 +1389,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_set_dkdv_form", &grt::attn_set_dkdv_form, "dK / dV kernel: 1 = 4-wave, 2 = wave-pair (default)");
   m.def("attn_get_dkdv_form", &grt::attn_get_dkdv_form);
   m.def("attn_set_dma_fast", &grt::attn_set_dma_fast, "1 = hoisted LDS-DMA addressing (default), 0 = clamped per tile");
-  m.def("rope_set_fast", &grt::rope_set_fast, "1 = the D = 128 RoPE kernel (default), 0 = the generic kernel");
+  m.def("ew_set_fast", &grt::ew_set_fast, "1 = single-pass RoPE (D = 128) / SwiGLU kernels (default), 0 = grid-stride kernels");
   m.def("attn_set_skip_dead", &grt::attn_set_skip_dead,
         "1 = forward / dK-dV waves skip the causal tiles they mask entirely (default), 0 = compute them");
   m.def("nf4_quantize", &nf4_quantize);

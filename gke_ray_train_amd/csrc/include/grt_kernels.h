@@ -45,7 +45,7 @@ void gelu_bwd(DType dt, const void* x, const void* dy, void* dx, int64_t n, hipS
 // RoPE (rotate-half convention). qkv: [T, (hq + 2*hkv) * D] fused projection output with row
 // stride `ld`; writes q_out [T, hq, D], k_out [T, hkv, D] contiguous. cos/sin: [S, D/2] fp32,
 // position of token t is pos[t] (int32) or t % S when pos == nullptr.
-void rope_set_fast(int on);  // 1 = D = 128 RoPE kernel with 32-bit indexing (default), 0 = generic kernel
+void ew_set_fast(int on);  // 1 = single-pass 32-bit-index RoPE (D = 128) / SwiGLU kernels (default), 0 = grid-stride kernels
 void rope_fwd(DType dt, const void* qkv, int64_t ld, void* q_out, void* k_out, const float* cos,
               const float* sin, const int32_t* pos, int64_t T, int S, int hq, int hkv, int D,
               hipStream_t s);

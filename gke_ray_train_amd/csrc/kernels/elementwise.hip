@@ -26,6 +26,20 @@ inline unsigned grid_for(int64_t work) {
   return (unsigned)g;
 }
 
+// Single-pass forms of the row-indexed elementwise kernels (RoPE at D = 128, plain SwiGLU): one work
+// item per thread on a full grid with 32-bit index math, instead of a capped grid-stride loop whose
+// 64-bit div / mod per item dominated the kernels' VALU. GRT_EW_FAST=0 / ew_set_fast(0) selects the
+// grid-stride kernels (A/B switch); both give bitwise the same results.
+int g_ew_fast = -1;
+inline bool ew_fast() {
+  if (g_ew_fast < 0) {
+    const char* e = getenv("GRT_EW_FAST");
+    g_ew_fast = e && e[0] == '0' ? 0 : 1;
+  }
+  return g_ew_fast != 0;
+}
+inline unsigned grid_full(int64_t work) { return (unsigned)((work + kNT - 1) / kNT); }
+
 // ------------------------------- SwiGLU -------------------------------------
 // gu: [rows, 2F] = [gate | up]; out = silu(gate) * up
 template <typename T>
@@ -69,6 +83,45 @@ __global__ __launch_bounds__(kNT) void swiglu_bwd_kernel(const T* __restrict__ g
     store16(dgu + r * 2 * f + c, dg);
     store16(dgu + r * 2 * f + f + c, du);
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void swiglu_fwd1_kernel(const T* __restrict__ gu, T* __restrict__ out, uint32_t total,
+                                                          int f, int64_t ldo) {
+  constexpr int V = Vec16<T>::N;
+  const uint32_t i = blockIdx.x * kNT + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t vpr = (uint32_t)(f / V), r = i / vpr;
+  const int c = (int)(i - r * vpr) * V;
+  float g[V], u[V], o[V];
+  load16(gu + (int64_t)r * 2 * f + c, g);
+  load16(gu + (int64_t)r * 2 * f + f + c, u);
+#pragma unroll
+  for (int k = 0; k < V; ++k) o[k] = g[k] * sigmoidf_(g[k]) * u[k];
+  store16(out + (int64_t)r * ldo + c, o);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void swiglu_bwd1_kernel(const T* __restrict__ gu, const T* __restrict__ dout,
+                                                          T* __restrict__ dgu, uint32_t total, int f) {
+  constexpr int V = Vec16<T>::N;
+  const uint32_t i = blockIdx.x * kNT + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t vpr = (uint32_t)(f / V), r = i / vpr;
+  const int c = (int)(i - r * vpr) * V;
+  float g[V], u[V], d[V], dg[V], du[V];
+  load16(gu + (int64_t)r * 2 * f + c, g);
+  load16(gu + (int64_t)r * 2 * f + f + c, u);
+  load16(dout + (int64_t)r * f + c, d);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {  // same arithmetic as swiglu_bwd_kernel
+    const float sg = sigmoidf_(g[k]);
+    const float silu = g[k] * sg;
+    du[k] = d[k] * silu;
+    dg[k] = d[k] * u[k] * sg * (1.f + g[k] * (1.f - sg));
+  }
+  store16(dgu + (int64_t)r * 2 * f + c, dg);
+  store16(dgu + (int64_t)r * 2 * f + f + c, du);
 }
 
 // ---------------- SwiGLU with the transposed copy for the weight gradient ---------------------
@@ -310,15 +363,6 @@ __global__ __launch_bounds__(kNT) void rope128_kernel(const T* __restrict__ src_
   }
 }
 
-// GRT_ROPE128=0 / rope_set_fast(0): the generic kernel for D = 128 as well (A/B switch)
-int g_rope128 = -1;
-inline bool rope128_on() {
-  if (g_rope128 < 0) {
-    const char* e = getenv("GRT_ROPE128");
-    g_rope128 = e && e[0] == '0' ? 0 : 1;
-  }
-  return g_rope128 != 0;
-}
 
 // ------------------------- decode: RoPE + KV-cache append ------------------
 // The cached-decode step's q / k rotation and the cache writes in one launch: token t (batch row
@@ -500,11 +544,25 @@ __global__ __launch_bounds__(kNT) void dropout_bwd_kernel(const T* __restrict__ 
 
 void swiglu_fwd(DType dt, const void* gu, void* out, int64_t rows, int f, hipStream_t s, int64_t ldo) {
   if (ldo <= 0) ldo = f;
+  if (ew_fast() && rows * f / 4 < INT32_MAX) {
+#define K(T, ...) hipLaunchKernelGGL(swiglu_fwd1_kernel<T>, dim3(grid_full(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, \
+      (const T*)gu, (T*)out, (uint32_t)(rows * f / Vec16<T>::N), f, ldo)
+    GRT_DISPATCH(dt, K, 0);
+#undef K
+    return;
+  }
 #define K(T, ...) hipLaunchKernelGGL(swiglu_fwd_kernel<T>, dim3(grid_for(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)gu, (T*)out, rows, f, ldo)
   GRT_DISPATCH(dt, K, 0);
 #undef K
 }
 void swiglu_bwd(DType dt, const void* gu, const void* dout, void* dgu, int64_t rows, int f, hipStream_t s) {
+  if (ew_fast() && rows * f / 4 < INT32_MAX) {
+#define K(T, ...) hipLaunchKernelGGL(swiglu_bwd1_kernel<T>, dim3(grid_full(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, \
+      (const T*)gu, (const T*)dout, (T*)dgu, (uint32_t)(rows * f / Vec16<T>::N), f)
+    GRT_DISPATCH(dt, K, 0);
+#undef K
+    return;
+  }
 #define K(T, ...) hipLaunchKernelGGL(swiglu_bwd_kernel<T>, dim3(grid_for(rows * f / Vec16<T>::N)), dim3(kNT), 0, s, (const T*)gu, (const T*)dout, (T*)dgu, rows, f)
   GRT_DISPATCH(dt, K, 0);
 #undef K
@@ -532,12 +590,12 @@ void gelu_bwd(DType dt, const void* x, const void* dy, void* dx, int64_t n, hipS
   GRT_DISPATCH(dt, K, 0);
 #undef K
 }
-void rope_set_fast(int on) { g_rope128 = on ? 1 : 0; }
+void ew_set_fast(int on) { g_ew_fast = on ? 1 : 0; }
 void rope_fwd(DType dt, const void* qkv, int64_t ld, void* q_out, void* k_out, const float* cos,
               const float* sin, const int32_t* pos, int64_t T_, int S, int hq, int hkv, int D,
               hipStream_t s) {
   const int64_t work = T_ * (hq + hkv) * (D / 16);
-  if (D == 128 && work < INT32_MAX && rope128_on()) {
+  if (D == 128 && work < INT32_MAX && ew_fast()) {
 #define K(TY, ...) hipLaunchKernelGGL((rope128_kernel<TY, true>), dim3((unsigned)((work + kNT - 1) / kNT)), dim3(kNT), 0, s, \
       (const TY*)qkv, (const TY*)qkv + (int64_t)hq * D, ld, ld, (TY*)q_out, (TY*)k_out, (int64_t)hq * D, \
       (int64_t)hkv * D, cos, sin, pos, (uint32_t)work, S, hq, hkv)
@@ -563,7 +621,7 @@ void rope_bwd(DType dt, const void* dq, const void* dk, void* dqkv, int64_t ld, 
               const float* sin, const int32_t* pos, int64_t T_, int S, int hq, int hkv, int D,
               hipStream_t s) {
   const int64_t work = T_ * (hq + hkv) * (D / 16);
-  if (D == 128 && work < INT32_MAX && rope128_on()) {
+  if (D == 128 && work < INT32_MAX && ew_fast()) {
 #define K(TY, ...) hipLaunchKernelGGL((rope128_kernel<TY, false>), dim3((unsigned)((work + kNT - 1) / kNT)), dim3(kNT), 0, s, \
       (const TY*)dq, (const TY*)dk, (int64_t)hq * D, (int64_t)hkv * D, (TY*)dqkv, (TY*)dqkv + (int64_t)hq * D, \
       ld, ld, cos, sin, pos, (uint32_t)work, S, hq, hkv)

@@ -12,7 +12,7 @@ qkv = torch.randn(T, (hq + 2 * hkv) * D, device="cuda", dtype=torch.bfloat16)
 cos, sin = _ref.rope_tables(S, D, 10000.0, device="cuda")
 cos, sin = cos.float().contiguous(), sin.float().contiguous()
 def t(fast, n=50):
-    C.rope_set_fast(fast)
+    C.ew_set_fast(fast)
     for _ in range(5): C.rope_fwd(qkv, cos, sin, None, hq, hkv, D, S)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -29,7 +29,7 @@ PY
 cat $O/time.log
 for i in 1 2 3; do
   for f in 1 0; do
-    GRT_ROPE128=$f timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $O/b$f.$i.json 2> $O/b$f.$i.err || exit 1
-    echo "rope128=$f round $i: $(python3 -c "import json;d=json.load(open('$O/b$f.$i.json'));print(d['value'], d['ms_per_step'], d['loss'])")"
+    GRT_EW_FAST=$f timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > $O/b$f.$i.json 2> $O/b$f.$i.err || exit 1
+    echo "ew_fast=$f round $i: $(python3 -c "import json;d=json.load(open('$O/b$f.$i.json'));print(d['value'], d['ms_per_step'], d['loss'])")"
   done
 done

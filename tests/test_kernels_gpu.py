@@ -104,6 +104,28 @@ def test_layernorm(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,f,pad", [(6656, 14336, 0), (33, 688, 0), (257, 1024, 64)])
+def test_swiglu_single_pass_kernels_match_grid_stride(dtype, rows, f, pad):
+    """The single-pass SwiGLU kernels (32-bit indexing, one vector per thread) give the grid-stride
+    kernels' forward (incl. a padded LoRA-tail row buffer) and backward bit for bit."""
+    C = _C()
+    g = torch.Generator(device=DEV).manual_seed(rows + f)
+    gu = torch.randn(rows, 2 * f, device=DEV, dtype=dtype, generator=g)
+    dout = torch.randn(rows, f, device=DEV, dtype=dtype, generator=g)
+    out = []
+    try:
+        for fast in (1, 0):
+            C.ew_set_fast(fast)
+            y = C.swiglu_fwd(gu, pad)
+            dgu = C.swiglu_bwd(gu, dout)
+            torch.cuda.synchronize()
+            out.append((y[:, :f].clone(), dgu))
+    finally:
+        C.ew_set_fast(1)
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_swiglu_gelu(dtype):
     from gke_ray_train_amd import ops
     torch.manual_seed(2)
@@ -252,14 +274,14 @@ def test_rope_d128_kernel_matches_generic(dtype, T, S, hq, hkv, packed):
     out = []
     try:
         for fast in (1, 0):
-            C.rope_set_fast(fast)
+            C.ew_set_fast(fast)
             q, k = C.rope_fwd(qkv, cos, sin, pos, hq, hkv, D, S)
             dqkv = torch.full_like(qkv, float("nan"))
             C.rope_bwd(dq, dk, dqkv, cos, sin, pos, hq, hkv, D, S)
             torch.cuda.synchronize()
             out.append((q, k, dqkv[:, :(hq + hkv) * D].clone()))
     finally:
-        C.rope_set_fast(1)
+        C.ew_set_fast(1)
     for name, a, b in zip(("q", "k", "dqk"), *out):
         assert torch.equal(a, b), name
 
