@@ -249,7 +249,11 @@ class FullyShardedDataParallel(nn.Module):
         from ..ops.linear import Linear as _DirectLinear
         ws = [m.weight for u in self.units if u.module is not self.module for m in u.module.modules()
               if isinstance(m, _DirectLinear) and m.weight.requires_grad and m.weight.dtype == torch.bfloat16]
-        nbytes = sum(w.numel() * w.element_size() for w in ws)
+        # the units' recorded full sizes: after sharding a module's weight tensor no longer has them
+        # (a 70B model measured as "fits" and kept 130 GiB of W^T copies, profiles/r6_offload_link.md)
+        full = {id(p): n for u in self.units for p, n in zip(u.params, u.numels)}
+        nbytes = sum(full.get(id(w), w.numel()) * w.element_size() for w in ws)
+        self.fwd_transpose_bytes = nbytes
         if mode == "auto" and nbytes > float(os.environ.get("GRT_FSDP_FWD_TRANSPOSE_MAX_GIB", "24")) * (1 << 30):
             return
         for w in ws:

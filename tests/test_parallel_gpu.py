@@ -351,3 +351,24 @@ def test_overlapped_offload_optimizer_resume_continues_identically(resident, pre
     torch.cuda.synchronize()
     assert torch.equal(f1.shard_store, f2.shard_store)
     assert torch.equal(f1.rep_flat, f2.rep_flat)
+
+
+def test_fsdp_forward_transpose_budget_uses_full_weight_sizes(monkeypatch):
+    """FSDP's forward-time W^T copies persist (one full bf16 copy of the projection weights), so they
+    are enabled only under GRT_FSDP_FWD_TRANSPOSE_MAX_GIB measured on the FULL weight sizes: the
+    sharded module tensors no longer carry them (a 70B run once kept 130 GiB of copies)."""
+    from gke_ray_train_amd.models.llama import LlamaForCausalLM, get_config
+    from gke_ray_train_amd.ops.linear import Linear
+    from gke_ray_train_amd.parallel.fsdp import FullyShardedDataParallel
+    cfg = get_config("llama-tiny-gqa")
+    expect = None
+    for limit, on in (("24", True), ("0.0001", False)):
+        monkeypatch.setenv("GRT_FSDP_FWD_TRANSPOSE_MAX_GIB", limit)
+        torch.manual_seed(0)
+        m = LlamaForCausalLM(cfg, device="meta", dtype=torch.bfloat16)
+        full = sum(mod.weight.numel() * 2 for blk in m.model.layers for mod in blk.modules() if isinstance(mod, Linear))
+        f = FullyShardedDataParallel(m, param_init_fn=lambda mod: None, device="cuda", proxy_world=4)
+        assert f.fwd_transpose_bytes == full, (f.fwd_transpose_bytes, full)
+        flags = [getattr(mod.weight, "_grt_fsdp_fwd_transpose", False) for blk in m.model.layers
+                 for mod in blk.modules() if isinstance(mod, Linear)]
+        assert flags and all(x == on for x in flags), (limit, flags)
