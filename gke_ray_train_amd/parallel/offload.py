@@ -321,7 +321,10 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
             st.pop("dev_v", None)
 
 
-PREFETCH_CAP_BYTES = 32 * (1 << 30)
+# largest automatic prefetch ring (bench --offload-prefetch-gib auto; the HBM room beside the plan
+# and the reserve bounds it further). Full-depth 70B, proxy rank 0 of 8, moments streamed: 32 / 48 /
+# 64 GiB ring = 0.80 / 0.82 / 0.91 x of the resident step (profiles/r6_offload_link.md)
+PREFETCH_CAP_BYTES = 64 * (1 << 30)
 
 
 def prefetch_slots_for(budget_bytes: float, chunk_elems: int) -> int:
