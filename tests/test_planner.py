@@ -110,7 +110,8 @@ def test_proxy_host_ram_counts_one_rank_and_reports_the_node():
 def test_offload_prefetch_ring_sizing():
     from gke_ray_train_amd.parallel.offload import PREFETCH_CAP_BYTES, prefetch_slots_for
     chunk = 1 << 26  # 64 Mi elements: m + v = 512 MiB per slot
-    assert prefetch_slots_for(PREFETCH_CAP_BYTES, chunk) == 64
+    assert prefetch_slots_for(PREFETCH_CAP_BYTES, chunk) == 128  # the 64 GiB automatic cap
+    assert prefetch_slots_for(32 * (1 << 30), chunk) == 64
     assert prefetch_slots_for(511 * (1 << 20), chunk) == 0
     assert prefetch_slots_for(0, chunk) == 0
 
