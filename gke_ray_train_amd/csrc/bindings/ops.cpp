@@ -977,13 +977,14 @@ void copy_sdma(Tensor& dst, const Tensor& src) {
 // dst (pinned host) <- src (device) on an SDMA engine, ordered on src's current stream through the
 // HSA runtime (csrc/bindings/sdma_copy.cpp): the HIP route above still lands on a blit kernel for a
 // device -> host copy on this image (profiles/r6_offload_link.md).
-void sdma_d2h(Tensor& dst, const Tensor& src) {
+void sdma_d2h(Tensor& dst, const Tensor& src, int64_t producer_stream) {
   TORCH_CHECK(dst.is_contiguous() && src.is_contiguous(), "sdma_d2h: contiguous tensors");
   TORCH_CHECK(src.is_cuda() && !dst.is_cuda() && dst.is_pinned(), "sdma_d2h: device source, pinned host destination");
   const int64_t n = dst.numel() * dst.element_size();
   TORCH_CHECK(n == src.numel() * src.element_size(), "sdma_d2h: byte counts differ");
   c10::OptionalDeviceGuard guard(src.device());
-  grt::sdma_d2h(dst.data_ptr(), src.data_ptr(), (size_t)n, src.get_device(), cur_stream(src));
+  grt::sdma_d2h(dst.data_ptr(), src.data_ptr(), (size_t)n, src.get_device(), cur_stream(src),
+                reinterpret_cast<hipStream_t>(producer_stream));
 }
 
 py::dict sdma_stats(int64_t device) {
@@ -1401,7 +1402,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("swiglu_bwd_t", &swiglu_bwd_t);
   m.def("transpose_into", &transpose_into);
   m.def("copy_sdma", &copy_sdma);
-  m.def("sdma_d2h", &sdma_d2h, "pinned host <- device on an SDMA engine, ordered on the source's current stream");
+  m.def("sdma_d2h", &sdma_d2h, py::arg("dst"), py::arg("src"), py::arg("producer_stream") = 0,
+        "pinned host <- device on an SDMA engine, ordered on the source's current stream; producer_stream "
+        "(a raw stream handle): the stream whose work so far wrote src");
   m.def("sdma_stats", &sdma_stats, "copies / bytes / worker busy seconds / first error of the SDMA copier");
   m.def("sdma_clear_error", [](int64_t device) { grt::sdma_clear_error((int)device); });
   m.def("gemv", &gemv, py::arg("x"), py::arg("w"), py::arg("swiglu") = false);

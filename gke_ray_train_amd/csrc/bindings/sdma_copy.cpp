@@ -13,10 +13,11 @@
 //   job's sequence number there. Work enqueued on the stream afterwards — or on any stream that
 //   waits for an event recorded there afterwards — therefore runs after the copy has landed, as
 //   with a stream-ordered copy.
-//   worker: hipEventSynchronize(ready) -> hsa_amd_memory_async_copy(dst, cpu, src, gpu) with a
-//   completion signal -> bounded wait -> store seq (release). A failed or timed-out copy still
-//   stores seq (the stream must not hang) and leaves a sticky error (sdma_stats()['error'], raised by
-//   the offloaded optimizer at its next step / synchronize).
+//   worker: hipEventSynchronize(ready) -> hsa_amd_memory_async_copy_on_engine
+//   (dst, cpu, src, gpu) with a completion signal -> wait bounded at 10 s + 1 s per GB -> store seq
+//   (release). A failed or timed-out copy still stores seq (the stream must not hang) and leaves a
+//   sticky error (sdma_stats()['error'], raised by the offloaded optimizer at its next step /
+//   synchronize); every later copy then releases its stream at once instead of queueing behind it.
 // Coherence: the event marker after the producer releases to system scope (L2 written back), so
 // the SDMA engine reads the producer's data from memory; the host destination is read by later
 // SDMA host -> device copies or by the CPU after a stream synchronisation.
@@ -75,7 +76,7 @@ class Copier {
     worker_.detach();  // lives as long as the process (no teardown ordering against the HIP runtime)
   }
 
-  void d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  void d2h(void* dst, const void* src, size_t bytes, hipStream_t s, hipStream_t producer) {
     std::lock_guard<std::mutex> g(submit_mu_);  // sequence numbers follow submission order
     if (!gpu_known_) {
       hsa_amd_pointer_info_t info{};
@@ -87,8 +88,12 @@ class Copier {
       gpu_known_ = true;
       pick_engine();
     }
+    // the producer event is recorded on the producer's own stream when one is given: an event recorded
+    // on `s` behind a cross-stream wait let copies read moments their update had not yet written
+    // (full GPU suite with GRT_OFFLOAD_D2H=sdma, gpurun_out/r6sdma3)
     hipEvent_t ev;
-    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, s) != hipSuccess)
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(ev, producer ? producer : s) != hipSuccess)
       throw std::runtime_error("sdma_d2h: event record failed");
     const uint32_t seq = ++next_seq_;
     if (trace_) fprintf(stderr, "sdma: submit seq=%u bytes=%zu\n", seq, bytes);
@@ -117,6 +122,7 @@ class Copier {
   void clear_error() {
     std::lock_guard<std::mutex> g(err_mu_);
     err_.clear();
+    failed_ = false;
   }
 
  private:
@@ -141,6 +147,7 @@ class Copier {
   void fail(const std::string& m) {
     std::lock_guard<std::mutex> g(err_mu_);
     if (err_.empty()) err_ = m;
+    failed_ = true;
   }
 
   void run() {
@@ -154,10 +161,15 @@ class Copier {
         q_.pop_front();
       }
       const auto tq = std::chrono::steady_clock::now();
+      // the producer. (Polling hipEventQuery from this thread instead let copies start before their
+      // producer finished: the parity test read stale moments, gpurun_out/r6sdma3.)
       const hipError_t e = hipEventSynchronize(j.ready);
       (void)hipEventDestroy(j.ready);
       const auto t0 = std::chrono::steady_clock::now();
-      if (e != hipSuccess) {
+      if (failed_) {
+        // an earlier copy failed: release the stream at once (the error is already recorded and the
+        // host raises at its next check) instead of stalling every later copy behind a stuck engine
+      } else if (e != hipSuccess) {
         fail(std::string("producer event failed: ") + hipGetErrorString(e));
       } else {
         hsa_signal_store_screlease(sig_, 1);
@@ -168,10 +180,11 @@ class Copier {
         if (st != HSA_STATUS_SUCCESS) {
           fail("hsa_amd_memory_async_copy returned " + std::to_string((int)st));
         } else {
-          // bounded: a copy that does not finish in 120 s releases the stream with an error
-          const hsa_signal_value_t v = hsa_signal_wait_scacquire(sig_, HSA_SIGNAL_CONDITION_LT, 1,
-                                                                 120ull * 1000000000ull, HSA_WAIT_STATE_BLOCKED);
-          if (v != 0) fail(v < 0 ? "SDMA copy reported an error" : "SDMA copy timed out (120 s)");
+          // bounded: 10 s + 1 s per GB (the link moves ~56 GB/s) releases the stream with an error
+          const uint64_t limit_ns = 10000000000ull + (uint64_t)j.bytes;
+          const hsa_signal_value_t v = hsa_signal_wait_scacquire(sig_, HSA_SIGNAL_CONDITION_LT, 1, limit_ns,
+                                                                 HSA_WAIT_STATE_BLOCKED);
+          if (v != 0) fail(v < 0 ? "SDMA copy reported an error" : "SDMA copy timed out");
         }
       }
       const auto t1 = std::chrono::steady_clock::now();
@@ -200,6 +213,7 @@ class Copier {
   std::thread worker_;
   std::atomic<uint64_t> copies_{0}, bytes_{0}, busy_ns_{0};
   std::string err_;
+  std::atomic<bool> failed_{false};  // set by fail(): later copies release their streams at once
 };
 
 constexpr int kMaxDev = 64;
@@ -215,9 +229,9 @@ Copier& copier(int dev) {
 
 }  // namespace
 
-void sdma_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t s) {
+void sdma_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t s, hipStream_t producer) {
   if (bytes == 0) return;
-  copier(device).d2h(dst, src, bytes, s);
+  copier(device).d2h(dst, src, bytes, s, producer);
 }
 
 SdmaStats sdma_stats(int device) { return copier(device).stats(); }

@@ -19,7 +19,11 @@ struct SdmaStats {
 // The copies of one device run one at a time in submission order. Submit from ONE stream per device
 // (the offloaded AdamW's download stream), or from streams that never wait on each other: a copy
 // whose producer waits on another stream's later copy would wait forever behind it.
-void sdma_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t s);
+// `dst` must stay allocated until the stream has passed the copy: unlike a stream copy, the copy is
+// not recorded with torch's caching host allocator.
+// `producer` (optional): the stream whose work so far produced `src`; the copy waits for it directly
+// (recorded there) rather than for an event recorded on `s` behind a cross-stream wait.
+void sdma_d2h(void* dst, const void* src, size_t bytes, int device, hipStream_t s, hipStream_t producer = nullptr);
 SdmaStats sdma_stats(int device);
 void sdma_clear_error(int device);
 

@@ -204,9 +204,11 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
         with torch.cuda.stream(down):
             down.wait_event(done)
             if self.d2h_engine == "sdma":
+                # the copy waits for the update stream itself (the producer of mb / vb)
                 C = _native.kernels()
-                C.sdma_d2h(sst["exp_avg"][s:e], mb[:e - s])
-                C.sdma_d2h(sst["exp_avg_sq"][s:e], vb[:e - s])
+                upd = self._streams[1].cuda_stream
+                C.sdma_d2h(sst["exp_avg"][s:e], mb[:e - s], upd)
+                C.sdma_d2h(sst["exp_avg_sq"][s:e], vb[:e - s], upd)
             else:
                 sst["exp_avg"][s:e].copy_(mb[:e - s], non_blocking=True)
                 sst["exp_avg_sq"][s:e].copy_(vb[:e - s], non_blocking=True)
@@ -309,6 +311,10 @@ class OverlappedOffloadAdamW(OffloadedAdamW):
 
     def load_state_dict(self, sd):
         self.synchronize()
+        # the host waits for every in-flight write-back: the load replaces the host moment tensors,
+        # and a device -> host copy landing after that (into memory the host allocator may already
+        # have handed out again: SDMA copies are not tracked by it) would corrupt it
+        torch.cuda.synchronize(self.fsdp.device)
         super().load_state_dict(sd)
         # slots uploaded ahead (prefetch()) hold the moments from before the load: drop them so the
         # next step uploads the loaded ones (and nothing stale is written back over them)
