@@ -27,13 +27,31 @@ constexpr int kNT = 256;
 constexpr int kSumBlocks = 1024;
 
 template <typename T>
-__global__ __launch_bounds__(kNT) void sumsq_kernel(const T* __restrict__ x, int64_t n, float* __restrict__ out) {
+__global__ __launch_bounds__(kNT) void sumsq_kernel(const T* __restrict__ x, int64_t n, float* __restrict__ out,
+                                                   bool sumsq_unroll) {
   __shared__ float red[kNT / kWave];
   constexpr int V = Vec16<T>::N;
   const int64_t nv = n / V;
   float acc = 0.f;
   const int64_t stride = (int64_t)gridDim.x * kNT;
-  for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < nv; i += stride) {
+  int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x;
+  // 4 independent 16-byte loads in flight per lane (one per iteration left each wave waiting a full
+  // HBM latency per 1 KiB, GRT_SUMSQ_UNROLL=0 keeps that loop for the A/B)
+  static constexpr int U = 4;
+  if (sumsq_unroll) {
+    float acc4[U] = {0.f, 0.f, 0.f, 0.f};
+    for (; i + (U - 1) * stride < nv; i += U * stride) {
+      float a[U][V];
+#pragma unroll
+      for (int u = 0; u < U; ++u) load16(x + (i + u * stride) * V, a[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < V; ++k) acc4[u] += a[u][k] * a[u][k];
+    }
+    acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+  }
+  for (; i < nv; i += stride) {
     float a[V];
     load16(x + i * V, a);
 #pragma unroll
@@ -378,11 +396,12 @@ unsigned grid_for(int64_t work) {
 int optim_sumsq_blocks() { return kSumBlocks; }
 
 void sumsq_accumulate(DType dt, const void* x, int64_t n, float* ws, int slot, hipStream_t s) {
+  static const bool unroll = [] { const char* e = std::getenv("GRT_SUMSQ_UNROLL"); return !(e && e[0] == '0'); }();
   float* out = ws + (int64_t)slot * kSumBlocks;
   if (dt == DType::BF16)
-    hipLaunchKernelGGL(sumsq_kernel<bf16>, dim3(kSumBlocks), dim3(kNT), 0, s, (const bf16*)x, n, out);
+    hipLaunchKernelGGL(sumsq_kernel<bf16>, dim3(kSumBlocks), dim3(kNT), 0, s, (const bf16*)x, n, out, unroll);
   else
-    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(kSumBlocks), dim3(kNT), 0, s, (const float*)x, n, out);
+    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(kSumBlocks), dim3(kNT), 0, s, (const float*)x, n, out, unroll);
 }
 
 void clip_coef_finalize(const float* ws, int nparts, float max_norm, float prescale, float* out,

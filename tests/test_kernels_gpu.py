@@ -1416,3 +1416,20 @@ def test_attn_bwd_writes_transposed_dqkv(B, S, hq, hkv, rope, form, varlen):
     assert torch.equal(outs[0][0], outs[1][0])
     assert not torch.isnan(outs[1][0].float()).any()
     assert torch.equal(outs[1][1], outs[1][0].t().contiguous())
+
+
+@pytest.mark.parametrize("dt,n", [(torch.bfloat16, 40_000_013), (torch.bfloat16, 3 * 1024 * 256 * 8 + 5),
+                                  (torch.float32, 9_000_011)])
+def test_sumsq_unrolled_matches_float64(dt, n):
+    """Grad-norm partial sums over sizes that run the 4-load unrolled loop on every lane, on some
+    lanes only (3 grid strides + a tail) and through the scalar remainder."""
+    from gke_ray_train_amd import _native
+    K = _native.kernels()
+    torch.manual_seed(11)
+    x = torch.randn(n, device=DEV, dtype=dt)
+    ws = torch.zeros(2 * K.sumsq_blocks(), device=DEV, dtype=torch.float32)
+    K.sumsq(x, ws, 1)
+    got = ws[K.sumsq_blocks():].double().sum().item()
+    ref = x.double().square().sum().item()
+    assert abs(got - ref) < 1e-5 * ref, (got, ref)
+    assert float(ws[:K.sumsq_blocks()].abs().sum()) == 0.0
