@@ -26,20 +26,21 @@ namespace {
 constexpr int kNT = 256;
 constexpr int kSumBlocks = 1024;
 
-template <typename T>
-__global__ __launch_bounds__(kNT) void sumsq_kernel(const T* __restrict__ x, int64_t n, float* __restrict__ out,
-                                                   bool sumsq_unroll) {
+template <typename T, int U>
+__global__ __launch_bounds__(kNT) void sumsq_kernel(const T* __restrict__ x, int64_t n, float* __restrict__ out) {
   __shared__ float red[kNT / kWave];
   constexpr int V = Vec16<T>::N;
   const int64_t nv = n / V;
   float acc = 0.f;
   const int64_t stride = (int64_t)gridDim.x * kNT;
   int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x;
-  // 4 independent 16-byte loads in flight per lane (one per iteration left each wave waiting a full
-  // HBM latency per 1 KiB, GRT_SUMSQ_UNROLL=0 keeps that loop for the A/B)
-  static constexpr int U = 4;
-  if (sumsq_unroll) {
-    float acc4[U] = {0.f, 0.f, 0.f, 0.f};
+  // U independent 16-byte loads in flight per lane (one per iteration leaves each wave waiting a full
+  // HBM latency per 1 KiB). Default U = 2: 6.1 TB/s isolated vs 5.7 (U = 4) and 5.6 (U = 1), and the
+  // fastest headline step of the three (scripts/r6/sumsq.sh); GRT_SUMSQ_UNROLL=0 / 4 -> U = 1 / 4
+  if constexpr (U > 1) {
+    float accu[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) accu[u] = 0.f;
     for (; i + (U - 1) * stride < nv; i += U * stride) {
       float a[U][V];
 #pragma unroll
@@ -47,9 +48,10 @@ __global__ __launch_bounds__(kNT) void sumsq_kernel(const T* __restrict__ x, int
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int k = 0; k < V; ++k) acc4[u] += a[u][k] * a[u][k];
+        for (int k = 0; k < V; ++k) accu[u] += a[u][k] * a[u][k];
     }
-    acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+    if constexpr (U == 4) acc = (accu[0] + accu[1]) + (accu[2] + accu[3]);
+    else acc = accu[0] + accu[1];
   }
   for (; i < nv; i += stride) {
     float a[V];
@@ -396,12 +398,23 @@ unsigned grid_for(int64_t work) {
 int optim_sumsq_blocks() { return kSumBlocks; }
 
 void sumsq_accumulate(DType dt, const void* x, int64_t n, float* ws, int slot, hipStream_t s) {
-  static const bool unroll = [] { const char* e = std::getenv("GRT_SUMSQ_UNROLL"); return !(e && e[0] == '0'); }();
+  static const int unroll = [] {
+    const char* e = std::getenv("GRT_SUMSQ_UNROLL");
+    return e && e[0] == '0' ? 1 : e && e[0] == '4' ? 4 : 2;
+  }();
   float* out = ws + (int64_t)slot * kSumBlocks;
-  if (dt == DType::BF16)
-    hipLaunchKernelGGL(sumsq_kernel<bf16>, dim3(kSumBlocks), dim3(kNT), 0, s, (const bf16*)x, n, out, unroll);
-  else
-    hipLaunchKernelGGL(sumsq_kernel<float>, dim3(kSumBlocks), dim3(kNT), 0, s, (const float*)x, n, out, unroll);
+  const dim3 g(kSumBlocks), b(kNT);
+  if (dt == DType::BF16) {
+    const bf16* xb = (const bf16*)x;
+    if (unroll == 4) hipLaunchKernelGGL((sumsq_kernel<bf16, 4>), g, b, 0, s, xb, n, out);
+    else if (unroll == 2) hipLaunchKernelGGL((sumsq_kernel<bf16, 2>), g, b, 0, s, xb, n, out);
+    else hipLaunchKernelGGL((sumsq_kernel<bf16, 1>), g, b, 0, s, xb, n, out);
+  } else {
+    const float* xf = (const float*)x;
+    if (unroll == 4) hipLaunchKernelGGL((sumsq_kernel<float, 4>), g, b, 0, s, xf, n, out);
+    else if (unroll == 2) hipLaunchKernelGGL((sumsq_kernel<float, 2>), g, b, 0, s, xf, n, out);
+    else hipLaunchKernelGGL((sumsq_kernel<float, 1>), g, b, 0, s, xf, n, out);
+  }
 }
 
 void clip_coef_finalize(const float* ws, int nparts, float max_norm, float prescale, float* out,
