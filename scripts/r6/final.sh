@@ -1,5 +1,5 @@
 # round-6 end state on one box: full GPU suite + smoke, headline bench x2, rocprofv3 step table
-O=gpurun_out/r6final7; mkdir -p $O
+O=gpurun_out/r6final8; mkdir -p $O
 timeout -k 10 1500 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc = 0 ] || exit $rc
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -5 $O/smoke.log; exit 1; }
